@@ -1,0 +1,252 @@
+"""Headless scene builders for the admm-elastic hot path (host side, numpy).
+
+These replace the reference's GUI sample glue that *feeds* `admm::Solver`
+(SURVEY.md §8f item 2):
+
+* `tri_blocks(nx, ny)`  -- the mesh of mclscene `factory::make_tri_blocks`
+  (admm_anderson_hard_zxu/deps/mclscene/include/MCL/ShapeFactory.hpp:499-548): unit
+  squares with a centre vertex, 4 triangles per square [(d,a,e),(a,b,e),(b,c,e),(c,d,e)].
+  Vertices are indexed directly on the structured grid (corners first, then centres)
+  instead of through mclscene's O(T*n) `refine()` merge -- the connectivity is the same,
+  only the vertex numbering differs.
+* `tet_blocks(cx, cy, cz)` -- `factory::make_tet_blocks` (ShapeFactory.hpp:436-496), five
+  tets per unit cube with the reference's corner labelling (a..h) and tet table.
+* lumped masses as `TriangleMesh::weighted_masses` (TriangleMesh.hpp:281-296) and
+  `TetMesh::weighted_masses` (TetMesh.hpp:297-315), bound per node x3 like
+  `binding::add_trimesh/add_tetmesh` (samples/utils/AddMeshes.hpp:97-235).
+* pin rules of the samples: windyflag `get_pins` (two corners of the min-x edge,
+  samples/Asia2019/windyflag.cpp:29-61) and the cantilever "x = min face" rule.
+
+A `Scene` is a plain container of fp64/int32 arrays -- exactly what the C ABI
+(`include/aa_admm.h`) takes -- plus the solver settings of the reference's
+`Solver::Settings` (Solver.hpp:45-67). `write_scene` serialises it for the reference
+driver under oracle/ (test infrastructure only).
+"""
+from __future__ import annotations
+
+import dataclasses
+import struct
+from typing import List
+
+import numpy as np
+
+TET, TRI = 0, 1
+LINEAR, NEOHOOKEAN, STVK = 0, 1, 2
+VARIANT_X, VARIANT_H = 0, 1  # admm_anderson_xzu (z-AA) / admm_anderson_hard_zxu ((u,x)-AA)
+
+
+def lame(E: float, nu: float):
+    """mu, lambda, bulk modulus k = lambda + 2/3 mu (EnergyTerm.hpp:35-61)."""
+    mu = E / (2.0 * (1.0 + nu))
+    lam = E * nu / ((1.0 + nu) * (1.0 - 2.0 * nu))
+    return mu, lam, lam + (2.0 / 3.0) * mu
+
+
+@dataclasses.dataclass
+class ElementGroup:
+    kind: int             # TET or TRI
+    material: int         # LINEAR / NEOHOOKEAN / STVK (tets); LINEAR for tris
+    E: float
+    nu: float
+    idx: np.ndarray       # int32 (count, 4) or (count, 3)
+    limit_min: float = -100.0   # Lame defaults (EnergyTerm.hpp:54-55)
+    limit_max: float = 100.0
+
+
+@dataclasses.dataclass
+class Scene:
+    x: np.ndarray                 # (n, 3) fp64 rest/initial positions
+    masses: np.ndarray            # (n,) fp64 lumped node masses
+    groups: List[ElementGroup]
+    pin_idx: np.ndarray           # (p,) int32
+    pin_pts: np.ndarray           # (p, 3) fp64 pin targets for the first step
+    pin_vel: np.ndarray           # (p, 3) fp64 pin displacement per time step
+    variant: int = VARIANT_H
+    dt: float = 1.0 / 30.0
+    gravity: float = -9.8
+    penalty: float = 1.0
+    iters: int = 100
+    accel: int = 1
+    aa_m: int = 6
+    n_steps: int = 1
+    name: str = "scene"
+
+    @property
+    def n_nodes(self) -> int:
+        return int(self.x.shape[0])
+
+    def n_elements(self) -> int:
+        return int(sum(len(g.idx) for g in self.groups))
+
+
+# ----------------------------------------------------------------------------------------
+# mesh generators
+# ----------------------------------------------------------------------------------------
+
+def tri_blocks(nx: int, ny: int):
+    """Vertices (n,3) and triangles (4*nx*ny, 3) of make_tri_blocks(nx, ny)."""
+    nx, ny = max(1, nx), max(1, ny)
+    gx, gy = np.meshgrid(np.arange(nx + 1, dtype=np.float64), np.arange(ny + 1, dtype=np.float64), indexing="ij")
+    corners = np.stack([gx.ravel(), gy.ravel(), np.zeros(gx.size)], axis=1)
+    cx, cy = np.meshgrid(np.arange(nx, dtype=np.float64) + 0.5, np.arange(ny, dtype=np.float64) + 0.5, indexing="ij")
+    centres = np.stack([cx.ravel(), cy.ravel(), np.zeros(cx.size)], axis=1)
+    verts = np.concatenate([corners, centres], axis=0)
+    ix, iy = np.meshgrid(np.arange(nx), np.arange(ny), indexing="ij")
+    ix, iy = ix.ravel(), iy.ravel()          # cell order x-major, y-minor as in the reference loops
+    corner = lambda i, j: i * (ny + 1) + j
+    a = corner(ix, iy)
+    b = corner(ix + 1, iy)
+    c = corner(ix + 1, iy + 1)
+    d = corner(ix, iy + 1)
+    e = (nx + 1) * (ny + 1) + ix * ny + iy
+    tris = np.stack([np.stack([d, a, e], 1), np.stack([a, b, e], 1),
+                     np.stack([b, c, e], 1), np.stack([c, d, e], 1)], axis=1).reshape(-1, 3)
+    return verts, tris.astype(np.int32)
+
+
+def tet_blocks(cx: int, cy: int, cz: int):
+    """Vertices (n,3) and tets (5*cx*cy*cz, 4) of make_tet_blocks(cx, cy, cz)."""
+    cx, cy, cz = max(1, cx), max(1, cy), max(1, cz)
+    g = np.stack(np.meshgrid(np.arange(cx + 1), np.arange(cy + 1), np.arange(cz + 1), indexing="ij"), -1)
+    verts = g.reshape(-1, 3).astype(np.float64)
+    node = lambda i, j, k: (i * (cy + 1) + j) * (cz + 1) + k
+    X, Y, Z = np.meshgrid(np.arange(cx), np.arange(cy), np.arange(cz), indexing="ij")
+    X, Y, Z = X.ravel(), Y.ravel(), Z.ravel()
+    a = node(X + 1, Y + 1, Z + 1)
+    b = node(X, Y + 1, Z + 1)
+    c = node(X, Y + 1, Z)
+    d = node(X + 1, Y + 1, Z)
+    e = node(X + 1, Y, Z + 1)
+    f = node(X, Y, Z + 1)
+    gg = node(X, Y, Z)
+    h = node(X + 1, Y, Z)
+    lab = [a, b, c, d, e, f, gg, h]
+    table = [(0, 5, 7, 4), (5, 7, 2, 0), (5, 0, 2, 1), (7, 2, 0, 3), (5, 2, 7, 6)]
+    tets = np.stack([np.stack([lab[t[0]], lab[t[1]], lab[t[2]], lab[t[3]]], 1) for t in table], 1).reshape(-1, 4)
+    return verts, tets.astype(np.int32)
+
+
+def tri_masses(verts, tris, density=1.0):
+    e1 = verts[tris[:, 1]] - verts[tris[:, 0]]
+    e2 = verts[tris[:, 2]] - verts[tris[:, 0]]
+    area = 0.5 * np.linalg.norm(np.cross(e1, e2), axis=1)
+    m = np.zeros(len(verts))
+    for k in range(3):
+        np.add.at(m, tris[:, k], density * area / 3.0)
+    return m
+
+
+def tet_masses(verts, tets, density=1522.0):
+    B = np.stack([verts[tets[:, k]] - verts[tets[:, 0]] for k in (1, 2, 3)], axis=2)
+    vol = np.abs(np.linalg.det(B)) / 6.0
+    m = np.zeros(len(verts))
+    for k in range(4):
+        np.add.at(m, tets[:, k], density * vol / 4.0)
+    return m
+
+
+# ----------------------------------------------------------------------------------------
+# the BASELINE.json scenes
+# ----------------------------------------------------------------------------------------
+
+def cloth(nx: int = 112, ny: int = 112, size: float = 2.0, *, variant=VARIANT_H, aa_m=6, iters=100,
+          n_steps=1, accel=1) -> Scene:
+    """C2: cloth drop (`make_tri_blocks(112,112)` scaled to `size` m, 50 176 tris).
+
+    Material Lame(50, 0.1) with strain limits [0.95, 1.05] and area density 1 as the
+    windyflag sample (windyflag.cpp:84-87, AddMeshes.hpp:203); two corners of the min-x
+    edge pinned in place (windyflag.cpp:29-61,101); wind omitted (out of scope).
+    """
+    v, t = tri_blocks(nx, ny)
+    v = v * (size / max(nx, ny))
+    m = tri_masses(v, t, 1.0)
+    xmin = v[:, 0].min() + 1e-3 * size / max(nx, ny)
+    cand = np.nonzero(v[:, 0] <= xmin)[0]
+    up = cand[np.argmin(v[cand, 1])]
+    down = cand[np.argmax(v[cand, 1])]
+    pins = np.array([up, down], dtype=np.int32)
+    return Scene(x=v, masses=m, groups=[ElementGroup(TRI, LINEAR, 50.0, 0.1, t, 0.95, 1.05)],
+                 pin_idx=pins, pin_pts=v[pins].copy(), pin_vel=np.zeros((2, 3)), variant=variant,
+                 iters=iters, aa_m=aa_m, n_steps=n_steps, accel=accel, name=f"cloth{nx}x{ny}")
+
+
+def cantilever(cx=20, cy=4, cz=5, material=NEOHOOKEAN, *, variant=VARIANT_X, aa_m=6, iters=50,
+               n_steps=1, accel=1, E=1e7, nu=0.399) -> Scene:
+    """C1: single cantilever `make_tet_blocks(20,4,5)` scaled 1/cy, x = 0 face pinned."""
+    v, t = tet_blocks(cx, cy, cz)
+    v = v / float(cy)
+    m = tet_masses(v, t, 1522.0)
+    pins = np.nonzero(v[:, 0] < v[:, 0].min() + 1e-3)[0].astype(np.int32)
+    return Scene(x=v, masses=m, groups=[ElementGroup(TET, material, E, nu, t)],
+                 pin_idx=pins, pin_pts=v[pins].copy(), pin_vel=np.zeros((len(pins), 3)), variant=variant,
+                 iters=iters, aa_m=aa_m, n_steps=n_steps, accel=accel, name=f"cantilever{cx}x{cy}x{cz}")
+
+
+def beams(dim=3, *, variant=VARIANT_X, aa_m=6, iters=100, n_steps=1, accel=1, materials=(LINEAR, NEOHOOKEAN, STVK)) -> Scene:
+    """C1 beams: three make_tet_blocks(4*dim, dim, dim) beams, 1 m tall, at y = +1.75 / 0 / -1.75,
+    Lame(1e7, 0.399), x-extreme faces pinned and pulled apart by dt per step
+    (samples/Asia2019/beams.cpp:94-167 and its stretch_beams callback)."""
+    xs, groups, pins, pts, vel = [], [], [], [], []
+    off = 0
+    dt = 1.0 / 30.0
+    for i, mat in enumerate(materials):
+        v, t = tet_blocks(4 * dim, dim, dim)
+        lo, hi = v.min(0), v.max(0)
+        v = (v - 0.5 * (lo + hi)) / (hi[1] - lo[1])
+        v[:, 1] += (1.75, 0.0, -1.75)[i % 3]
+        bl, bh = v[:, 0].min() + 1e-2, v[:, 0].max() - 1e-2
+        for j in range(len(v)):
+            if v[j, 0] < bl:
+                pins.append(off + j); pts.append(v[j] - [dt, 0, 0]); vel.append([-dt, 0, 0])
+            if v[j, 0] > bh:
+                pins.append(off + j); pts.append(v[j] + [dt, 0, 0]); vel.append([dt, 0, 0])
+        groups.append(ElementGroup(TET, mat, 1e7, 0.399, t + off))
+        xs.append(v)
+        off += len(v)
+    x = np.concatenate(xs)
+    m = np.concatenate([tet_masses(xs[i], groups[i].idx - sum(len(xx) for xx in xs[:i])) for i in range(len(xs))])
+    return Scene(x=x, masses=m, groups=groups, pin_idx=np.array(pins, np.int32), pin_pts=np.array(pts),
+                 pin_vel=np.array(vel), variant=variant, iters=iters, aa_m=aa_m, n_steps=n_steps, accel=accel,
+                 name=f"beams{dim}")
+
+
+# ----------------------------------------------------------------------------------------
+# reference-driver I/O (test infrastructure; see oracle/ref_drivers/ref_elastic_driver.cpp)
+# ----------------------------------------------------------------------------------------
+
+def write_scene(scene: Scene, path: str) -> None:
+    with open(path, "wb") as f:
+        f.write(b"AASCENE1")
+        f.write(struct.pack("<ii", scene.variant, scene.n_nodes))
+        f.write(np.ascontiguousarray(scene.x, dtype="<f8").tobytes())
+        f.write(np.repeat(np.asarray(scene.masses, dtype="<f8"), 3).tobytes())
+        f.write(struct.pack("<i", len(scene.groups)))
+        for g in scene.groups:
+            f.write(struct.pack("<iiddddi", g.kind, g.material, g.E, g.nu, g.limit_min, g.limit_max, len(g.idx)))
+            f.write(np.ascontiguousarray(g.idx, dtype="<i4").tobytes())
+        f.write(struct.pack("<i", len(scene.pin_idx)))
+        f.write(np.ascontiguousarray(scene.pin_idx, dtype="<i4").tobytes())
+        f.write(np.ascontiguousarray(scene.pin_pts, dtype="<f8").tobytes())
+        f.write(np.ascontiguousarray(scene.pin_vel, dtype="<f8").tobytes())
+        f.write(struct.pack("<dddiiii", scene.dt, scene.gravity, scene.penalty, scene.iters, scene.accel,
+                            scene.aa_m, scene.n_steps))
+
+
+def read_ref_result(path: str, n_nodes: int):
+    """Per time step: dict(prim, comb, reject, x, v) as written by the reference driver."""
+    data = open(path, "rb").read()
+    off = 0
+
+    def take(dtype, count):
+        nonlocal off
+        arr = np.frombuffer(data, dtype=dtype, count=count, offset=off)
+        off += arr.nbytes
+        return arr.copy()
+
+    n_steps = int(take("<i4", 1)[0])
+    steps = []
+    for _ in range(n_steps):
+        nrec = int(take("<i4", 1)[0])
+        steps.append(dict(prim=take("<f8", nrec), comb=take("<f8", nrec), reject=take("<i4", nrec),
+                          x=take("<f8", 3 * n_nodes).reshape(-1, 3), v=take("<f8", 3 * n_nodes).reshape(-1, 3)))
+    return steps

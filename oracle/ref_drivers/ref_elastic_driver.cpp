@@ -1,0 +1,156 @@
+// Headless driver for the REFERENCE admm-elastic solver (test infrastructure only).
+//
+// Compiled by oracle/Makefile directly against the reference sources under
+// /root/reference (Solver.cpp, TetEnergyTerm.cpp, TriEnergyTerm.cpp, ExplicitForce.cpp)
+// -- nothing of the reference is copied into this repository. It replaces the GLFW
+// `Application` loop of the samples (e.g. admm_anderson_hard_zxu/samples/Asia2019/
+// windyflag.cpp:63-183, beams.cpp) with a file-driven loop:
+//
+//   scene file (written by aa-admm_amd/scenes.py: write_scene) -> admm::Solver
+//     add_nodes (Solver.hpp:265-279), create_tets_from_mesh / create_tris_from_mesh
+//     (TetEnergyTerm.hpp:36-51, TriEnergyTerm.hpp:33-47), set_pins (Solver.cpp:280-315),
+//     initialize (Solver.cpp:361-491), step() x n_steps (Solver.cpp:34-234)
+//   -> result file: per time step the per-iteration (prim, comb, reject) rows that
+//      Solver::save() writes (Solver.hpp:130-155) plus the node positions/velocities.
+//
+// Build with -DREF_VARIANT_H for admm_anderson_hard_zxu, without it for admm_anderson_xzu.
+#include "Solver.hpp"
+#include "TetEnergyTerm.hpp"
+#include "TriEnergyTerm.hpp"
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+#include <sys/stat.h>
+
+namespace {
+
+struct Reader {
+    FILE* f;
+    template <typename T> T get() {
+        T v;
+        if (fread(&v, sizeof(T), 1, f) != 1) { fprintf(stderr, "scene: short read\n"); exit(2); }
+        return v;
+    }
+    template <typename T> void arr(std::vector<T>& out, size_t n) {
+        out.resize(n);
+        if (n && fread(out.data(), sizeof(T), n, f) != n) { fprintf(stderr, "scene: short read\n"); exit(2); }
+    }
+};
+
+struct Group {
+    int kind, material;
+    double E, nu, lmin, lmax;
+    int count;
+    std::vector<int> idx;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 3) { fprintf(stderr, "usage: %s scene.bin out.bin\n", argv[0]); return 2; }
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) { perror("scene"); return 2; }
+    Reader r{f};
+    char magic[8];
+    if (fread(magic, 1, 8, f) != 8 || memcmp(magic, "AASCENE1", 8) != 0) { fprintf(stderr, "bad magic\n"); return 2; }
+    const int variant = r.get<int>();
+    const int n = r.get<int>();
+    std::vector<double> x, m;
+    r.arr(x, 3 * (size_t)n);
+    r.arr(m, 3 * (size_t)n);
+    const int n_groups = r.get<int>();
+    std::vector<Group> groups(n_groups);
+    for (auto& g : groups) {
+        g.kind = r.get<int>(); g.material = r.get<int>();
+        g.E = r.get<double>(); g.nu = r.get<double>(); g.lmin = r.get<double>(); g.lmax = r.get<double>();
+        g.count = r.get<int>();
+        r.arr(g.idx, (size_t)g.count * (g.kind == 0 ? 4 : 3));
+    }
+    const int n_pins = r.get<int>();
+    std::vector<int> pin_idx;
+    std::vector<double> pin_pts, pin_vel;
+    r.arr(pin_idx, n_pins);
+    r.arr(pin_pts, 3 * (size_t)n_pins);
+    r.arr(pin_vel, 3 * (size_t)n_pins);
+    const double dt = r.get<double>(), gravity = r.get<double>(), penalty = r.get<double>();
+    const int iters = r.get<int>(), accel = r.get<int>(), aa_m = r.get<int>(), n_steps = r.get<int>();
+    fclose(f);
+#ifdef REF_VARIANT_H
+    if (variant != 1) { fprintf(stderr, "scene asks for the z-AA (X) variant; this is the H build\n"); return 2; }
+#else
+    if (variant != 0) { fprintf(stderr, "scene asks for the (u,x)-AA (H) variant; this is the X build\n"); return 2; }
+    (void)penalty;
+#endif
+
+    admm::Solver solver;
+    solver.add_nodes<double>(x.data(), m.data(), n);
+    for (auto& g : groups) {
+        admm::Lame lame(g.E, g.nu);
+        lame.limit_min = g.lmin;
+        lame.limit_max = g.lmax;
+        if (g.kind == 0) {
+            if (g.material == 0)
+                admm::create_tets_from_mesh<double, admm::TetEnergyTerm>(solver.energyterms, x.data(), g.idx.data(), g.count, lame, 0);
+            else if (g.material == 1)
+                admm::create_tets_from_mesh<double, admm::NeoHookeanTet>(solver.energyterms, x.data(), g.idx.data(), g.count, lame, 0);
+            else
+                admm::create_tets_from_mesh<double, admm::StVKTet>(solver.energyterms, x.data(), g.idx.data(), g.count, lame, 0);
+        } else {
+            admm::create_tris_from_mesh<double, admm::TriEnergyTerm>(solver.energyterms, x.data(), g.idx.data(), g.count, lame, 0);
+        }
+    }
+    auto pins_at = [&](int k) {
+        std::vector<admm::Solver::Vec3> pts(n_pins);
+        for (int i = 0; i < n_pins; ++i)
+            for (int j = 0; j < 3; ++j) pts[i][j] = pin_pts[3 * i + j] + k * pin_vel[3 * i + j];
+        return pts;
+    };
+    solver.set_pins(pin_idx, pins_at(0));
+
+    admm::Solver::Settings st;
+    st.timestep_s = dt;
+    st.gravity = gravity;
+    st.admm_iters = iters;
+    st.verbose = 0;
+    st.Anderson_m = aa_m;
+    st.acceleration_type = accel ? admm::Solver::Settings::ANDERSON : admm::Solver::Settings::NOACC;
+#ifdef REF_VARIANT_H
+    st.penalty = penalty;
+#endif
+    if (!solver.initialize(st)) { fprintf(stderr, "initialize failed\n"); return 1; }
+
+    mkdir("result", 0755);
+    const std::string res = accel ? "result/residual-" + std::to_string(aa_m) + ".txt" : "result/residual-no.txt";
+    FILE* out = fopen(argv[2], "wb");
+    fwrite(&n_steps, sizeof(int), 1, out);
+    for (int k = 1; k <= n_steps; ++k) {
+        solver.set_pins(pin_idx, pins_at(k));
+        solver.step();
+        std::vector<double> prim, comb;
+        std::vector<int> rej;
+        std::ifstream in(res);
+        std::string line;
+        while (std::getline(in, line)) {
+            if (line.empty()) continue;
+            std::istringstream ls(line);
+            double t, p, c;
+            int rj = 0;
+            ls >> t >> p >> c;
+            if (!(ls >> rj)) rj = 0;
+            prim.push_back(p); comb.push_back(c); rej.push_back(rj);
+        }
+        int nrec = (int)prim.size();
+        fwrite(&nrec, sizeof(int), 1, out);
+        fwrite(prim.data(), sizeof(double), nrec, out);
+        fwrite(comb.data(), sizeof(double), nrec, out);
+        fwrite(rej.data(), sizeof(int), nrec, out);
+        fwrite(solver.m_x.data(), sizeof(double), 3 * (size_t)n, out);
+        fwrite(solver.m_v.data(), sizeof(double), 3 * (size_t)n, out);
+    }
+    fclose(out);
+    return 0;
+}
