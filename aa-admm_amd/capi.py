@@ -1,0 +1,241 @@
+"""ctypes binding of libaa_admm.so (include/aa_admm.h) -- the Python host mirror of the
+reference's admm::Solver API (admm_anderson_hard_zxu/src/Solver.hpp:39-262).
+
+This is exactly the stub a maintainer would add on the Python side of the boundary
+(INTEGRATION.md). There is no CPU fallback: if the HIP library is missing or no GPU is
+visible, constructing a context raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libaa_admm.so")
+
+AA_LINEAR, AA_NEOHOOKEAN, AA_STVK = 0, 1, 2
+AA_VARIANT_Z, AA_VARIANT_UX = 0, 1
+NOACC, ANDERSON = 0, 1
+
+EXPORTS = [
+    "aa_last_error", "aa_version", "aa_ctx_create", "aa_ctx_destroy", "aa_ctx_synchronize", "aa_lame_from_young",
+    "aa_settings_default", "aa_elastic_create", "aa_elastic_destroy", "aa_elastic_add_nodes", "aa_elastic_add_tets",
+    "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
+    "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
+    "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats",
+]
+
+
+class Lame(C.Structure):
+    """admm::Lame (EnergyTerm.hpp:35-61)."""
+    _fields_ = [("mu", C.c_double), ("lambda_", C.c_double), ("limit_min", C.c_double), ("limit_max", C.c_double)]
+
+    @classmethod
+    def from_young(cls, E, nu, limit_min=-100.0, limit_max=100.0):
+        mu = E / (2.0 * (1.0 + nu))
+        lam = E * nu / ((1.0 + nu) * (1.0 - 2.0 * nu))
+        return cls(mu, lam, limit_min, limit_max)
+
+
+class Settings(C.Structure):
+    """admm::Solver::Settings (Solver.hpp:45-67) + the variant."""
+    _fields_ = [("timestep_s", C.c_double), ("verbose", C.c_int), ("admm_iters", C.c_int), ("gravity", C.c_double),
+                ("constraint_w", C.c_double), ("anderson_m", C.c_int), ("penalty", C.c_double),
+                ("acceleration_type", C.c_int), ("variant", C.c_int)]
+
+    def __init__(self, **kw):
+        super().__init__(1.0 / 30.0, 1, 500, -9.8, -1.0, 2, 1.0, NOACC, AA_VARIANT_UX)
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+class Runtime(C.Structure):
+    _fields_ = [("global_ms", C.c_double), ("local_ms", C.c_double), ("acceleration_ms", C.c_double),
+                ("initialization_ms", C.c_double), ("step_ms", C.c_double), ("setup_ms", C.c_double),
+                ("iterations", C.c_int), ("rejects", C.c_int), ("nnz_factor", C.c_longlong), ("n_free", C.c_int),
+                ("n_pinned", C.c_int), ("n_elements", C.c_int), ("z_dim", C.c_int)]
+
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"aa_admm HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        L.aa_last_error.restype = C.c_char_p
+        L.aa_version.restype = C.c_char_p
+        _LIB = L
+    return _LIB
+
+
+class AAError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _chk(rc):
+    if rc != 0:
+        raise AAError(rc, lib().aa_last_error().decode())
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+class Context:
+    def __init__(self, device=0):
+        self.h = C.c_void_p()
+        _chk(lib().aa_ctx_create(C.c_int(device), C.byref(self.h)))
+
+    def synchronize(self):
+        _chk(lib().aa_ctx_synchronize(self.h))
+
+    def close(self):
+        if self.h:
+            lib().aa_ctx_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Solver:
+    """Mirror of admm::Solver: add_nodes / create_*_from_mesh / set_pins / initialize / step."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.h = C.c_void_p()
+        _chk(lib().aa_elastic_create(ctx.h, C.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            lib().aa_elastic_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_nodes(self, x, m3):
+        x = np.ascontiguousarray(x, np.float64).reshape(-1)
+        m3 = np.ascontiguousarray(m3, np.float64).reshape(-1)
+        tot = C.c_int()
+        _chk(lib().aa_elastic_add_nodes(self.h, _dp(x), _dp(m3), C.c_int(len(x) // 3), C.byref(tot)))
+        return tot.value
+
+    def add_tets(self, verts, tets, material, lame: Lame, vertex_offset=0):
+        v = np.ascontiguousarray(verts, np.float64).reshape(-1)
+        t = np.ascontiguousarray(tets, np.int32).reshape(-1)
+        _chk(lib().aa_elastic_add_tets(self.h, _dp(v), _ip(t), C.c_int(len(t) // 4), C.c_int(material),
+                                       C.byref(lame), C.c_int(vertex_offset)))
+
+    def add_tris(self, verts, tris, lame: Lame, vertex_offset=0):
+        v = np.ascontiguousarray(verts, np.float64).reshape(-1)
+        t = np.ascontiguousarray(tris, np.int32).reshape(-1)
+        _chk(lib().aa_elastic_add_tris(self.h, _dp(v), _ip(t), C.c_int(len(t) // 3), C.byref(lame),
+                                       C.c_int(vertex_offset)))
+
+    def set_pins(self, inds, points=None):
+        i = np.ascontiguousarray(inds, np.int32).reshape(-1)
+        if points is None:
+            _chk(lib().aa_elastic_set_pins(self.h, _ip(i), None, C.c_int(len(i))))
+        else:
+            p = np.ascontiguousarray(points, np.float64).reshape(-1)
+            _chk(lib().aa_elastic_set_pins(self.h, _ip(i), _dp(p), C.c_int(len(i))))
+
+    def initialize(self, settings: Settings):
+        _chk(lib().aa_elastic_initialize(self.h, C.byref(settings)))
+
+    def step(self):
+        _chk(lib().aa_elastic_step(self.h))
+
+    def num_nodes(self):
+        n = C.c_int()
+        _chk(lib().aa_elastic_num_nodes(self.h, C.byref(n)))
+        return n.value
+
+    @property
+    def x(self):
+        out = np.zeros(3 * self.num_nodes())
+        _chk(lib().aa_elastic_get_x(self.h, _dp(out)))
+        return out.reshape(-1, 3)
+
+    @property
+    def v(self):
+        out = np.zeros(3 * self.num_nodes())
+        _chk(lib().aa_elastic_get_v(self.h, _dp(out)))
+        return out.reshape(-1, 3)
+
+    def history(self, cap=100000):
+        p, c, r = np.zeros(cap), np.zeros(cap), np.zeros(cap, np.int32)
+        n = C.c_int()
+        _chk(lib().aa_elastic_get_history(self.h, _dp(p), _dp(c), _ip(r), C.c_int(cap), C.byref(n)))
+        k = min(n.value, cap)
+        return dict(prim=p[:k].copy(), comb=c[:k].copy(), reject=r[:k].copy())
+
+    def runtime(self) -> Runtime:
+        rt = Runtime()
+        _chk(lib().aa_elastic_runtime(self.h, C.byref(rt)))
+        return rt
+
+    def bench_iterations(self, iters):
+        ms = C.c_double()
+        _chk(lib().aa_elastic_bench_iterations(self.h, C.c_int(iters), C.byref(ms)))
+        return ms.value
+
+    def kernel_stats(self, name):
+        a, b, n = C.c_double(), C.c_double(), C.c_int()
+        _chk(lib().aa_elastic_kernel_stats(self.h, name.encode(), C.byref(a), C.byref(b), C.byref(n)))
+        return dict(avg_ms=a.value, bytes=b.value, launches=n.value)
+
+
+def solver_from_scene(ctx: Context, scene) -> Solver:
+    """Binds a scenes.Scene the way binding::add_trimesh/add_tetmesh + the samples do."""
+    s = Solver(ctx)
+    s.add_nodes(scene.x, np.repeat(np.asarray(scene.masses, np.float64), 3))
+    for g in scene.groups:
+        lame = Lame.from_young(g.E, g.nu, g.limit_min, g.limit_max)
+        if g.kind == 0:
+            s.add_tets(scene.x, g.idx, g.material, lame)
+        else:
+            s.add_tris(scene.x, g.idx, lame)
+    s.set_pins(scene.pin_idx, scene.pin_pts)
+    return s
+
+
+def settings_from_scene(scene) -> Settings:
+    return Settings(timestep_s=scene.dt, admm_iters=scene.iters, gravity=scene.gravity, anderson_m=scene.aa_m,
+                    penalty=scene.penalty, acceleration_type=ANDERSON if scene.accel else NOACC,
+                    variant=scene.variant, verbose=0)
+
+
+def run_scene(ctx: Context, scene, n_steps=None):
+    """Runs the scene like the reference driver; returns per-step dicts (prim, comb, reject, x, v)."""
+    s = solver_from_scene(ctx, scene)
+    s.initialize(settings_from_scene(scene))
+    out = []
+    n_steps = scene.n_steps if n_steps is None else n_steps
+    for k in range(1, n_steps + 1):
+        if np.any(scene.pin_vel != 0):
+            s.set_pins(scene.pin_idx, scene.pin_pts + k * scene.pin_vel)
+        s.step()
+        h = s.history()
+        h["x"], h["v"] = s.x, s.v
+        h["step_ms"] = s.runtime().step_ms
+        out.append(h)
+    return out, s

@@ -1,0 +1,201 @@
+// extern "C" boundary (include/aa_admm.h). Every entry point catches and maps exceptions to
+// status codes; the message is kept per thread for aa_last_error().
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "../../include/aa_admm.h"
+#include "elastic.hpp"
+
+struct aa_ctx_s { aa::Context c; };
+struct aa_elastic_s { aa::ElasticSolver* s; aa_ctx_s* ctx; };
+
+namespace {
+thread_local std::string g_err;
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return AA_OK;
+    } catch (const aa::Error& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of host memory";
+        return AA_ERR_DEVICE;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return AA_ERR_ARG;
+    }
+}
+
+#define NEED(p, what) do { if (!(p)) throw aa::Error(AA_ERR_ARG, what); } while (0)
+}  // namespace
+
+extern "C" {
+
+const char* aa_last_error(void) { return g_err.c_str(); }
+const char* aa_version(void) { return "aa_admm 0.1 (gfx950)"; }
+
+int aa_ctx_create(int device_id, aa_ctx* out) {
+    return guarded([&] {
+        NEED(out, "aa_ctx_create: null out");
+        int n = 0;
+        AA_HIP(hipGetDeviceCount(&n));
+        if (device_id < 0 || device_id >= n) throw aa::Error(AA_ERR_ARG, "aa_ctx_create: no such device");
+        AA_HIP(hipSetDevice(device_id));
+        auto* c = new aa_ctx_s;
+        c->c.device = device_id;
+        AA_HIP(hipStreamCreateWithFlags(&c->c.stream, hipStreamNonBlocking));
+        *out = c;
+    });
+}
+
+int aa_ctx_destroy(aa_ctx ctx) {
+    return guarded([&] {
+        if (!ctx) return;
+        (void)hipStreamSynchronize(ctx->c.stream);
+        (void)hipStreamDestroy(ctx->c.stream);
+        delete ctx;
+    });
+}
+
+int aa_ctx_synchronize(aa_ctx ctx) {
+    return guarded([&] { NEED(ctx, "null ctx"); AA_HIP(hipStreamSynchronize(ctx->c.stream)); });
+}
+
+int aa_lame_from_young(double k, double v, aa_lame* out) {
+    return guarded([&] {
+        NEED(out, "null out");
+        out->mu = k / (2.0 * (1.0 + v));
+        out->lambda = k * v / ((1.0 + v) * (1.0 - 2.0 * v));
+        out->limit_min = -100.0;
+        out->limit_max = 100.0;
+    });
+}
+
+int aa_settings_default(aa_settings* s) {
+    return guarded([&] {
+        NEED(s, "null out");
+        s->timestep_s = 1.0 / 30.0;
+        s->verbose = 1;
+        s->admm_iters = 500;
+        s->gravity = -9.8;
+        s->constraint_w = -1;
+        s->anderson_m = 2;
+        s->penalty = 1.0;
+        s->acceleration_type = 0;
+        s->variant = AA_VARIANT_UX;
+    });
+}
+
+int aa_elastic_create(aa_ctx ctx, aa_elastic* out) {
+    return guarded([&] {
+        NEED(ctx && out, "aa_elastic_create: null argument");
+        AA_HIP(hipSetDevice(ctx->c.device));
+        auto* h = new aa_elastic_s;
+        h->ctx = ctx;
+        h->s = new aa::ElasticSolver(&ctx->c);
+        *out = h;
+    });
+}
+
+int aa_elastic_destroy(aa_elastic h) {
+    return guarded([&] {
+        if (!h) return;
+        (void)hipSetDevice(h->ctx->c.device);
+        delete h->s;
+        delete h;
+    });
+}
+
+int aa_elastic_add_nodes(aa_elastic h, const double* x3, const double* m3, int n, int* total) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        int t = h->s->add_nodes(x3, m3, n);
+        if (total) *total = t;
+    });
+}
+
+int aa_elastic_add_tets(aa_elastic h, const double* verts3, const int* tets4, int n, int material, const aa_lame* lame,
+                        int vertex_offset) {
+    return guarded([&] {
+        NEED(h && lame, "null argument");
+        h->s->add_elements(0, material, verts3, tets4, n, *lame, vertex_offset);
+    });
+}
+
+int aa_elastic_add_tris(aa_elastic h, const double* verts3, const int* tris3, int n, const aa_lame* lame,
+                        int vertex_offset) {
+    return guarded([&] {
+        NEED(h && lame, "null argument");
+        h->s->add_elements(1, AA_LINEAR, verts3, tris3, n, *lame, vertex_offset);
+    });
+}
+
+int aa_elastic_set_pins(aa_elastic h, const int* inds, const double* pts3, int n) {
+    return guarded([&] { NEED(h, "null handle"); h->s->set_pins(inds, pts3, n); });
+}
+
+int aa_elastic_initialize(aa_elastic h, const aa_settings* s) {
+    return guarded([&] {
+        NEED(h && s, "null argument");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        h->s->initialize(*s);
+    });
+}
+
+int aa_elastic_step(aa_elastic h) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        h->s->step();
+    });
+}
+
+int aa_elastic_num_nodes(aa_elastic h, int* n) {
+    return guarded([&] { NEED(h && n, "null argument"); *n = h->s->num_nodes(); });
+}
+
+int aa_elastic_get_x(aa_elastic h, double* x3) {
+    return guarded([&] { NEED(h && x3, "null argument"); h->s->get_x(x3); });
+}
+
+int aa_elastic_get_v(aa_elastic h, double* v3) {
+    return guarded([&] { NEED(h && v3, "null argument"); h->s->get_v(v3); });
+}
+
+int aa_elastic_set_v(aa_elastic h, const double* v3) {
+    return guarded([&] { NEED(h && v3, "null argument"); h->s->set_v(v3); });
+}
+
+int aa_elastic_get_history(aa_elastic h, double* prim, double* comb, int* reject, int cap, int* n) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        int k = h->s->history(prim, comb, reject, cap);
+        if (n) *n = k;
+    });
+}
+
+int aa_elastic_runtime(aa_elastic h, aa_runtime* out) {
+    return guarded([&] { NEED(h && out, "null argument"); *out = h->s->runtime(); });
+}
+
+int aa_elastic_bench_iterations(aa_elastic h, int iters, double* ms) {
+    return guarded([&] {
+        NEED(h && iters >= 0, "bad argument");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        double t = h->s->bench_iterations(iters);
+        if (ms) *ms = t;
+    });
+}
+
+int aa_elastic_kernel_stats(aa_elastic h, const char* name, double* avg_ms, double* bytes, int* launches) {
+    return guarded([&] {
+        NEED(h && name, "null argument");
+        if (!h->s->kernel_stats(name, avg_ms, bytes, launches)) throw aa::Error(AA_ERR_ARG, std::string("no kernel class ") + name);
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// Shared host/device utilities for the aa_admm HIP library (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace aa {
+
+enum Status { OK = 0, ERR_ARG = -1, ERR_STATE = -2, ERR_DEVICE = -3, ERR_NUMERIC = -4 };
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define AA_HIP(call)                                                                                   \
+    do {                                                                                               \
+        hipError_t e_ = (call);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            throw ::aa::Error(::aa::ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_) +    \
+                                                    " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")"); \
+    } while (0)
+
+#define AA_CHECK_LAUNCH() AA_HIP(hipGetLastError())
+
+// Owning device buffer (hipMalloc'd, never resized inside a time step).
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t count) { alloc(count); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; return *this; }
+    ~DevBuf() { release(); }
+    void alloc(size_t count) {
+        release();
+        n = count;
+        if (count) AA_HIP(hipMalloc(&p, count * sizeof(T)));
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr; n = 0;
+    }
+    void upload(const std::vector<T>& h, hipStream_t s) {
+        if (h.size() != n) alloc(h.size());
+        if (n) AA_HIP(hipMemcpyAsync(p, h.data(), n * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+    void upload(const T* h, size_t count, hipStream_t s) {
+        if (count != n) alloc(count);
+        if (n) AA_HIP(hipMemcpyAsync(p, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+    void zero(hipStream_t s) { if (n) AA_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s)); }
+    size_t bytes() const { return n * sizeof(T); }
+};
+
+constexpr int kBlock = 256;
+inline int blocks_for(long long n, int block = kBlock) { return (int)((n + block - 1) / block); }
+
+}  // namespace aa

@@ -1,0 +1,156 @@
+// Hyperelastic per-tet proximal solve, device side (one tet per thread, registers).
+//
+// Same algorithm as the reference's HyperElasticTet::prox
+// (admm_anderson_hard_zxu/src/TetEnergyTerm.cpp:151-162) with the vendored mcloptlib
+// L-BFGS<double,9> (deps/mcloptlib/include/MCL/LBFGS.hpp:135-305): history 6, relative
+// gradient test 1e-6*max(|x|,1), objective-change test 1e-16, at most 100 iterations,
+// Armijo backtracking (ftol 1e-4, factor 0.5), first step 1/|g| then 1. Energies:
+//   NeoHookean  Psi = mu/2 (I1 - log I3 - 3) + lambda/8 (log I3)^2   (TetEnergyTerm.cpp:206-251)
+//   StVK        Psi = mu tr(E^T E) + lambda/2 tr(E)^2, E = (F^T F - I)/2  (:256-307)
+// f(F) = vol (Psi(F) + k/2 |F - v|^2). A line-search step below 1e-20 raises the error flag
+// (the reference throws std::runtime_error there).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace aa {
+namespace dev {
+
+__device__ __forceinline__ double det3cm(const double* x) {  // column-major F(r,c) = x[c*3+r]
+    return x[0] * (x[4] * x[8] - x[7] * x[5]) - x[3] * (x[1] * x[8] - x[7] * x[2]) + x[6] * (x[1] * x[5] - x[4] * x[2]);
+}
+
+// Psi and dPsi/dF (column-major)
+__device__ __forceinline__ double hyper_psi_grad(int mat, double mu, double lambda, const double* x, double* g) {
+    if (mat == 1) {
+        const double J = det3cm(x);
+        double cof[9];  // cofactor matrix, column-major: cof(r,c) at [c*3+r]; F^-T = cof / J
+        cof[0] = x[4] * x[8] - x[7] * x[5];
+        cof[3] = -(x[1] * x[8] - x[7] * x[2]);
+        cof[6] = x[1] * x[5] - x[4] * x[2];
+        cof[1] = -(x[3] * x[8] - x[6] * x[5]);
+        cof[4] = x[0] * x[8] - x[6] * x[2];
+        cof[7] = -(x[0] * x[5] - x[3] * x[2]);
+        cof[2] = x[3] * x[7] - x[6] * x[4];
+        cof[5] = -(x[0] * x[7] - x[6] * x[1]);
+        cof[8] = x[0] * x[4] - x[3] * x[1];
+        const double invJ = 1.0 / J, lJ = log(J);
+        double I1 = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            I1 += x[i] * x[i];
+            const double finvt = cof[i] * invJ;
+            g[i] = mu * (x[i] - finvt) + lambda * lJ * finvt;
+        }
+        const double lI3 = log(J * J);
+        return 0.5 * mu * (I1 - lI3 - 3.0) + 0.125 * lambda * lI3 * lI3;
+    }
+    // StVK
+    double E[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            E[c * 3 + r] = 0.5 * ((x[r * 3 + 0] * x[c * 3 + 0] + x[r * 3 + 1] * x[c * 3 + 1] + x[r * 3 + 2] * x[c * 3 + 2]) -
+                                  (r == c ? 1.0 : 0.0));
+    const double tr = E[0] + E[4] + E[8];
+    double ee = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) ee += E[i] * E[i];
+    double P[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) P[i] = 2.0 * mu * E[i];
+    P[0] += lambda * tr; P[4] += lambda * tr; P[8] += lambda * tr;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            g[c * 3 + r] = x[0 * 3 + r] * P[c * 3 + 0] + x[1 * 3 + r] * P[c * 3 + 1] + x[2 * 3 + r] * P[c * 3 + 2];
+    return mu * ee + 0.5 * lambda * tr * tr;
+}
+
+__device__ __forceinline__ double hyper_eval(int mat, double mu, double lambda, double k, double vol, const double* v,
+                                             const double* x, double* g) {
+    const double psi = hyper_psi_grad(mat, mu, lambda, x, g);
+    double q = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const double d = v[i] - x[i];
+        q += d * d;
+        g[i] = vol * (g[i] + k * (x[i] - v[i]));
+    }
+    return vol * (psi + 0.5 * k * q);
+}
+
+__device__ __forceinline__ double d9(const double* a, const double* b) {
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) s += a[i] * b[i];
+    return s;
+}
+
+// x: in = v (start point), out = prox. Returns iterations; sets *fail on a collapsed line search.
+__device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, double k, double vol, const double* v,
+                                          double* x, int* fail) {
+    double s[6][9], y[6][9], ys_h[6], alpha[6], g[9], gp[9], xp[9], drt[9];
+    double fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
+    double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
+    double fpast = fx;
+    if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return 1;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) drt[i] = -g[i];
+    double step = 1.0 / sqrt(d9(drt, drt));
+    int k_it = 1, end = 0;
+    for (;;) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { xp[i] = x[i]; gp[i] = g[i]; }
+        {
+            const double fx_init = fx, dg_test = 1e-4 * d9(g, drt);
+            for (int it = 0; it < 2000; ++it) {
+#pragma unroll
+                for (int i = 0; i < 9; ++i) x[i] = xp[i] + step * drt[i];
+                fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
+                if (!(fx > fx_init + step * dg_test)) break;
+                if (step < 1e-20 || step > 1e20) { *fail = 1; return k_it; }
+                step *= 0.5;
+            }
+        }
+        xnorm = sqrt(d9(x, x));
+        gnorm = sqrt(d9(g, g));
+        if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return k_it;
+        if (fabs(fpast - fx) < 1e-16) return k_it;
+        fpast = fx;
+        if (k_it >= 100) return k_it;
+        double ys = 0, yy = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double si = x[i] - xp[i], yi = g[i] - gp[i];
+            s[end][i] = si; y[end][i] = yi;
+            ys += yi * si; yy += yi * yi;
+        }
+        ys_h[end] = ys;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) drt[i] = -g[i];
+        const int bound = k_it < 6 ? k_it : 6;
+        end = (end + 1) % 6;
+        int j = end;
+        for (int i = 0; i < bound; ++i) {
+            j = (j + 5) % 6;
+            alpha[j] = d9(s[j], drt) / ys_h[j];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) drt[t] -= alpha[j] * y[j][t];
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) drt[t] *= ys / yy;
+        for (int i = 0; i < bound; ++i) {
+            const double beta = d9(y[j], drt) / ys_h[j];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) drt[t] += (alpha[j] - beta) * s[j][t];
+            j = (j + 1) % 6;
+        }
+        step = 1.0;
+        ++k_it;
+    }
+}
+
+}  // namespace dev
+}  // namespace aa

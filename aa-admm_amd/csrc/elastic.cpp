@@ -1,0 +1,630 @@
+// Host orchestration of the admm-elastic hot path (see elastic.hpp).
+//
+// Reference call stack being replaced:
+//   Solver::initialize  admm_anderson_hard_zxu/src/Solver.cpp:361-491 (X: xzu/src/Solver.cpp:373-498)
+//   Solver::step        admm_anderson_hard_zxu/src/Solver.cpp:34-234  (X: xzu/src/Solver.cpp:34-263)
+// All per-iteration work is enqueued on one HIP stream; the data-dependent branches of the
+// reference (Anderson reject, comb < 1e-20 break) are evaluated by device control kernels
+// and gate the following kernels, so a time step needs exactly one host synchronisation.
+#include "elastic.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <set>
+
+#include "spd_direct.hpp"
+
+namespace aa {
+
+ElasticSolver::~ElasticSolver() {
+    for (auto& kv : kstats_)
+        for (auto e : kv.second.ev) (void)hipEventDestroy(e);
+}
+
+int ElasticSolver::add_nodes(const double* x3, const double* m3, int n) {
+    if (n < 0 || (n > 0 && (!x3 || !m3))) throw Error(ERR_ARG, "add_nodes: bad input");
+    if (initialized_) throw Error(ERR_STATE, "add_nodes after initialize is not supported");
+    x_.insert(x_.end(), x3, x3 + 3 * (size_t)n);
+    v_.insert(v_.end(), 3 * (size_t)n, 0.0);
+    m3_.insert(m3_.end(), m3, m3 + 3 * (size_t)n);
+    return (int)(x_.size() / 3);
+}
+
+// TetEnergyTerm ctor + get_reduction (TetEnergyTerm.cpp:32-72), TriEnergyTerm ctor +
+// get_reduction (TriEnergyTerm.cpp:30-72), EnergyTerm::get_reduction weight check (EnergyTerm.hpp:135-153)
+void ElasticSolver::add_elements(int kind, int material, const double* verts3, const int* idx, int count,
+                                 const aa_lame& lame, int vertex_offset) {
+    if (count < 0 || (count > 0 && (!verts3 || !idx))) throw Error(ERR_ARG, "add_elements: bad input");
+    if (initialized_) throw Error(ERR_STATE, "adding energy terms after initialize is not supported");
+    if (kind == 1) {
+        if (lame.limit_min > 1.0) throw Error(ERR_ARG, "**TriEnergyTerm Error: Strain limit min should be -inf to 1");
+        if (lame.limit_max < 1.0) throw Error(ERR_ARG, "**TriEnergyTerm Error: Strain limit max should be 1 to inf");
+        material = AA_LINEAR;
+    } else if (material < 0 || material > 2) {
+        throw Error(ERR_ARG, "add_tets: unknown material");
+    }
+    HostGroup g;
+    g.kind = kind; g.material = material; g.lame = lame;
+    g.nv = kind == 0 ? 4 : 3; g.ncol = g.nv - 1;
+    const double k = lame.lambda + (2.0 / 3.0) * lame.mu;
+    g.idx.resize((size_t)count * g.nv);
+    g.G.resize((size_t)count * g.ncol * g.nv);
+    g.vol.resize(count); g.w.resize(count);
+    for (int t = 0; t < count; ++t) {
+        const double* P[4];
+        for (int a = 0; a < g.nv; ++a) {
+            const int li = idx[(size_t)t * g.nv + a];
+            if (li < 0) throw Error(ERR_ARG, "add_elements: negative index");
+            P[a] = verts3 + 3 * (size_t)li;
+            g.idx[(size_t)t * g.nv + a] = li + vertex_offset;
+        }
+        double* G = &g.G[(size_t)t * g.ncol * g.nv];
+        double vol;
+        if (kind == 0) {
+            double B[9];
+            for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) B[r * 3 + c] = P[c + 1][r] - P[0][r];
+            double cof[9];
+            cof[0] = B[4] * B[8] - B[5] * B[7]; cof[1] = B[5] * B[6] - B[3] * B[8]; cof[2] = B[3] * B[7] - B[4] * B[6];
+            cof[3] = B[2] * B[7] - B[1] * B[8]; cof[4] = B[0] * B[8] - B[2] * B[6]; cof[5] = B[1] * B[6] - B[0] * B[7];
+            cof[6] = B[1] * B[5] - B[2] * B[4]; cof[7] = B[2] * B[3] - B[0] * B[5]; cof[8] = B[0] * B[4] - B[1] * B[3];
+            const double det = B[0] * cof[0] + B[1] * cof[1] + B[2] * cof[2];
+            double Bi[9];
+            for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Bi[r * 3 + c] = cof[c * 3 + r] / det;
+            vol = det / 6.0;
+            if (vol < 0) throw Error(ERR_NUMERIC, "**TetEnergyTerm Error: Inverted initial tet");
+            for (int r = 0; r < 3; ++r) {
+                G[r * 4 + 0] = -Bi[0 * 3 + r] - Bi[1 * 3 + r] - Bi[2 * 3 + r];
+                for (int a = 1; a < 4; ++a) G[r * 4 + a] = Bi[(a - 1) * 3 + r];
+            }
+        } else {
+            double e12[3], e13[3], n1[3], n2[3];
+            for (int r = 0; r < 3; ++r) { e12[r] = P[1][r] - P[0][r]; e13[r] = P[2][r] - P[0][r]; }
+            double l = std::sqrt(e12[0] * e12[0] + e12[1] * e12[1] + e12[2] * e12[2]);
+            for (int r = 0; r < 3; ++r) n1[r] = e12[r] / l;
+            const double d = e13[0] * n1[0] + e13[1] * n1[1] + e13[2] * n1[2];
+            for (int r = 0; r < 3; ++r) n2[r] = e13[r] - d * n1[r];
+            l = std::sqrt(n2[0] * n2[0] + n2[1] * n2[1] + n2[2] * n2[2]);
+            for (int r = 0; r < 3; ++r) n2[r] /= l;
+            auto dot = [](const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+            const double b00 = dot(n1, e12), b01 = dot(n1, e13), b10 = dot(n2, e12), b11 = dot(n2, e13);
+            const double det = b00 * b11 - b01 * b10;
+            const double invdet = 1.0 / det;
+            const double R[2][2] = {{b11 * invdet, -b01 * invdet}, {-b10 * invdet, b00 * invdet}};
+            vol = 0.5 * det;
+            if (vol < 0) throw Error(ERR_NUMERIC, "**TriEnergyTerm Error: Inverted initial pose");
+            for (int c = 0; c < 2; ++c) {
+                G[c * 3 + 0] = -R[0][c] - R[1][c];
+                G[c * 3 + 1] = R[0][c];
+                G[c * 3 + 2] = R[1][c];
+            }
+        }
+        const double w = std::sqrt(k * vol);
+        if (!(w > 0.0)) throw Error(ERR_NUMERIC, "**EnergyTerm::get_reduction Error: Some weight leq 0");
+        g.vol[t] = vol;
+        g.w[t] = w;
+    }
+    hgroups_.push_back(std::move(g));
+}
+
+// Solver::set_pins (admm_anderson_hard_zxu/src/Solver.cpp:280-315). Pins are kept in a map
+// (like ConstraintSet::pins); each pinned node gets ITS OWN point. (The reference pairs the
+// i-th given point with the i-th pin in sorted order -- identical whenever inds are sorted.)
+void ElasticSolver::set_pins(const int* inds, const double* pts3, int n) {
+    if (n < 0 || (n > 0 && !inds)) throw Error(ERR_ARG, "**Solver::set_pins Error: Bad input.");
+    const bool in_place = pts3 == nullptr;
+    const int nodes = num_nodes();
+    if (nodes == 0 && in_place && n > 0) throw Error(ERR_ARG, "**Solver::set_pins Error: Bad input.");
+    std::map<int, std::array<double, 3>> pins;
+    for (int i = 0; i < n; ++i) {
+        const int id = inds[i];
+        if (id < 0 || id >= nodes) throw Error(ERR_ARG, "**Solver::set_pins Error: Bad input.");
+        std::array<double, 3> p;
+        for (int j = 0; j < 3; ++j) p[j] = in_place ? x_[3 * (size_t)id + j] : pts3[3 * i + j];
+        pins[id] = p;
+    }
+    if (initialized_) {
+        bool same = pins.size() == pins_.size();
+        for (auto it = pins.begin(), jt = pins_.begin(); same && it != pins.end(); ++it, ++jt) same = it->first == jt->first;
+        if (!same) throw Error(ERR_STATE, "set_pins: the pinned node set cannot change after initialize");
+    }
+    pins_ = std::move(pins);
+    pins_dirty_ = true;
+}
+
+void ElasticSolver::initialize(const aa_settings& s_in) {
+    auto t0 = std::chrono::steady_clock::now();
+    st_ = s_in;
+    if (st_.timestep_s <= 0.0) st_.timestep_s = 1.0 / 24.0;  // Solver.cpp:369-373
+    const int n = num_nodes();
+    if (!((int)m3_.size() == 3 * n && 3 * n >= 3)) throw Error(ERR_ARG, "**Solver Error: Problem with node data!");
+    for (int i = 0; i < n; ++i)
+        if (m3_[3 * i] != m3_[3 * i + 1] || m3_[3 * i] != m3_[3 * i + 2])
+            throw Error(ERR_ARG, "initialize: per-node masses must be equal in x, y and z (A = A_s (x) I3)");
+    const bool accel = st_.acceleration_type == 1;
+    if (accel && (st_.anderson_m <= 0 || st_.anderson_m > kMaxM))
+        throw Error(ERR_ARG, "initialize: Anderson window must be in [1, 32]");
+    if (st_.variant != AA_VARIANT_Z && st_.variant != AA_VARIANT_UX) throw Error(ERR_ARG, "initialize: bad variant");
+    if (st_.admm_iters < 0) throw Error(ERR_ARG, "initialize: admm_iters < 0");
+    std::fill(v_.begin(), v_.end(), 0.0);
+
+    n_ = n;
+    np_ = (int)pins_.size();
+    nf_ = n - np_;
+    // ---- free / pinned split and nested-dissection order of the free nodes
+    std::vector<int> free_nodes;
+    std::vector<int> is_pin(n, 0);
+    for (auto& kv : pins_) is_pin[kv.first] = 1;
+    for (int i = 0; i < n; ++i) if (!is_pin[i]) free_nodes.push_back(i);
+    std::vector<int> node2free(n, -1);
+    for (int k = 0; k < nf_; ++k) node2free[free_nodes[k]] = k;
+    std::vector<std::vector<int>> adjl(nf_);
+    for (auto& g : hgroups_)
+        for (size_t t = 0; t < g.idx.size() / g.nv; ++t)
+            for (int a = 0; a < g.nv; ++a) {
+                const int na = g.idx[t * g.nv + a];
+                if (na < 0 || na >= n) throw Error(ERR_ARG, "energy term references a node that does not exist");
+                const int fa = node2free[na];
+                if (fa < 0) continue;
+                for (int b = 0; b < g.nv; ++b) {
+                    const int fb = node2free[g.idx[t * g.nv + b]];
+                    if (fb >= 0 && fb != fa) adjl[fa].push_back(fb);
+                }
+            }
+    std::vector<int> aptr(nf_ + 1, 0), aj;
+    for (int k = 0; k < nf_; ++k) {
+        auto& l = adjl[k];
+        std::sort(l.begin(), l.end());
+        l.erase(std::unique(l.begin(), l.end()), l.end());
+        aptr[k + 1] = aptr[k] + (int)l.size();
+        aj.insert(aj.end(), l.begin(), l.end());
+    }
+    std::vector<double> coords(3 * (size_t)nf_);
+    for (int k = 0; k < nf_; ++k)
+        for (int j = 0; j < 3; ++j) coords[3 * k + j] = x_[3 * (size_t)free_nodes[k] + j];
+    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32);
+    node2int_.assign(n, -1);
+    int2node_.assign(n, -1);
+    for (int q = 0; q < nf_; ++q) { node2int_[free_nodes[tree.perm[q]]] = q; int2node_[q] = free_nodes[tree.perm[q]]; }
+    {
+        int q = nf_;
+        for (auto& kv : pins_) { node2int_[kv.first] = q; int2node_[q] = kv.first; ++q; }
+    }
+    // ---- global matrix A_s = M + pdt2 * sum_e w^2 G^T G  (Solver.cpp:466-467)
+    const double dt2 = st_.timestep_s * st_.timestep_s;
+    pdt2_ = (st_.variant == AA_VARIANT_UX ? st_.penalty : 1.0) * dt2;
+    std::vector<std::vector<std::pair<int, double>>> rows(nf_);
+    for (int q = 0; q < nf_; ++q) rows[q].push_back({q, m3_[3 * (size_t)int2node_[q]]});
+    for (auto& g : hgroups_) {
+        const size_t cnt = g.idx.size() / g.nv;
+        for (size_t t = 0; t < cnt; ++t) {
+            const double w2 = g.w[t] * g.w[t];
+            const double* G = &g.G[t * g.ncol * g.nv];
+            for (int a = 0; a < g.nv; ++a) {
+                const int qa = node2int_[g.idx[t * g.nv + a]];
+                if (qa >= nf_) continue;
+                for (int b = 0; b < g.nv; ++b) {
+                    const int qb = node2int_[g.idx[t * g.nv + b]];
+                    if (qb >= nf_) continue;
+                    double sacc = 0;
+                    for (int c = 0; c < g.ncol; ++c) sacc += G[c * g.nv + a] * G[c * g.nv + b];
+                    rows[qa].push_back({qb, pdt2_ * w2 * sacc});
+                }
+            }
+        }
+    }
+    CsrMatrix A;
+    A.n = nf_;
+    A.ptr.assign(nf_ + 1, 0);
+    for (int q = 0; q < nf_; ++q) {
+        auto& r = rows[q];
+        std::sort(r.begin(), r.end(), [](const std::pair<int, double>& a, const std::pair<int, double>& b) { return a.first < b.first; });
+        for (size_t k = 0; k < r.size();) {
+            size_t k2 = k;
+            double v = 0;
+            while (k2 < r.size() && r[k2].first == r[k].first) v += r[k2++].second;
+            A.col.push_back(r[k].first);
+            A.val.push_back(v);
+            k = k2;
+        }
+        A.ptr[q + 1] = (int)A.col.size();
+        std::vector<std::pair<int, double>>().swap(r);
+    }
+    SupernodalFactor F;
+    try {
+        F = multifrontal_cholesky(A, tree);
+    } catch (const std::runtime_error& e) {
+        throw Error(ERR_NUMERIC, e.what());
+    }
+    solver_.build(F, s());
+
+    // ---- device element groups (internal node ids), z/u offsets, D^T gather rows
+    groups_.clear();
+    groups_.resize(hgroups_.size());
+    long long zoff = 0, yrow = 0;
+    red_blocks_ = 0;
+    std::vector<std::vector<std::pair<long long, double>>> dtr(nf_);
+    for (size_t gi = 0; gi < hgroups_.size(); ++gi) {
+        auto& hg = hgroups_[gi];
+        auto& dg = groups_[gi];
+        const int cnt = (int)(hg.idx.size() / hg.nv);
+        std::vector<int> idx((size_t)hg.nv * cnt);
+        std::vector<double> G((size_t)hg.ncol * hg.nv * cnt);
+        for (int t = 0; t < cnt; ++t) {
+            for (int a = 0; a < hg.nv; ++a) idx[(size_t)a * cnt + t] = node2int_[hg.idx[(size_t)t * hg.nv + a]];
+            for (int c = 0; c < hg.ncol; ++c)
+                for (int a = 0; a < hg.nv; ++a)
+                    G[(size_t)(c * hg.nv + a) * cnt + t] = hg.G[((size_t)t * hg.ncol + c) * hg.nv + a];
+            for (int a = 0; a < hg.nv; ++a) {
+                const int q = node2int_[hg.idx[(size_t)t * hg.nv + a]];
+                if (q >= nf_) continue;
+                for (int c = 0; c < hg.ncol; ++c)
+                    dtr[q].push_back({yrow + (long long)t * hg.ncol + c, hg.G[((size_t)t * hg.ncol + c) * hg.nv + a]});
+            }
+        }
+        dg.idx.upload(idx, s());
+        dg.G.upload(G, s());
+        dg.w.upload(hg.w, s());
+        dg.vol.upload(hg.vol, s());
+        GroupDev& d = dg.d;
+        d.kind = hg.kind; d.mat = hg.material; d.count = cnt; d.nv = hg.nv; d.ncol = hg.ncol; d.dim = 3 * hg.ncol;
+        d.zoff = zoff; d.yrow = yrow;
+        d.idx = dg.idx.p; d.G = dg.G.p; d.w = dg.w.p; d.vol = dg.vol.p;
+        d.mu = hg.lame.mu; d.lambda = hg.lame.lambda; d.k = hg.lame.lambda + (2.0 / 3.0) * hg.lame.mu;
+        d.lmin = hg.lame.limit_min; d.lmax = hg.lame.limit_max;
+        zoff += (long long)d.dim * cnt;
+        yrow += (long long)d.ncol * cnt;
+        red_blocks_ += blocks_for(cnt);
+    }
+    Z_ = zoff;
+    {
+        std::vector<int> ptr(nf_ + 1, 0), row;
+        std::vector<double> val;
+        for (int q = 0; q < nf_; ++q) {
+            auto& r = dtr[q];
+            std::sort(r.begin(), r.end());
+            for (auto& e : r) { row.push_back((int)e.first); val.push_back(e.second); }
+            ptr[q + 1] = (int)row.size();
+        }
+        dt_ptr_.upload(ptr, s()); dt_row_.upload(row, s()); dt_val_.upload(val, s());
+    }
+    // ---- state and work buffers
+    std::vector<double> xs(3 * (size_t)n), ms(n);
+    for (int q = 0; q < n; ++q) {
+        for (int j = 0; j < 3; ++j) xs[3 * (size_t)q + j] = x_[3 * (size_t)int2node_[q] + j];
+        ms[q] = m3_[3 * (size_t)int2node_[q]];
+    }
+    xs_.upload(xs, s());
+    vs_.alloc(3 * (size_t)n); vs_.zero(s());
+    mass_.upload(ms, s());
+    xfull_.alloc(3 * (size_t)n); xlast_.alloc(3 * (size_t)n); cxfull_.alloc(3 * (size_t)n);
+    xfull_.zero(s()); xlast_.zero(s()); cxfull_.zero(s());
+    xbar_.alloc(3 * (size_t)nf_); Mxbar_.alloc(3 * (size_t)nf_); b_.alloc(3 * (size_t)nf_); dx_.alloc(3 * (size_t)nf_);
+    z_.alloc(Z_); u_.alloc(Z_); y_.alloc(Z_); du_.alloc(Z_);
+    if (st_.variant == AA_VARIANT_Z) { dz_.alloc(Z_); lastz_.alloc(Z_); cz_.alloc(Z_); }
+    red_a_.alloc(std::max(1, red_blocks_)); red_b_.alloc(std::max(1, red_blocks_));
+    ctrl_.alloc(1);
+    hist_cap_ = std::max(1, st_.admm_iters);
+    hist_prim_.alloc(hist_cap_); hist_comb_.alloc(hist_cap_); hist_rej_.alloc(hist_cap_);
+    if (accel) {
+        const int m = st_.anderson_m;
+        const long long dim = st_.variant == AA_VARIANT_UX ? Z_ + 3LL * nf_ : Z_;
+        aa_cur_.alloc(dim);
+        aa_dF_.alloc((size_t)m * Z_); aa_dF_.zero(s());
+        aa_dG_.alloc((size_t)m * dim); aa_dG_.zero(s());
+        aa_blocks_ = aa_reduce_blocks(dim);
+        const int mm = m <= 8 ? 8 : (m <= 16 ? 16 : 32);
+        aa_red_.alloc((size_t)aa_blocks_ * (2 + 2 * mm));
+    }
+    AA_HIP(hipStreamSynchronize(s()));
+    initialized_ = true;
+    pins_dirty_ = true;
+    rt_ = aa_runtime{};
+    rt_.nnz_factor = (long long)F.nnz_L;
+    rt_.n_free = nf_; rt_.n_pinned = np_;
+    rt_.n_elements = 0;
+    for (auto& g : groups_) rt_.n_elements += g.d.count;
+    rt_.z_dim = (int)Z_;
+    rt_.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    // algorithmic bytes per launch class (DESIGN.md "roofline accounting")
+    kstats_.clear();
+    double lz = 0, rs = 0;
+    for (auto& g : groups_) {
+        const double per = 4.0 * g.d.nv + 8.0 * g.d.ncol * g.d.nv + 8.0;
+        lz += g.d.count * (per + 3 * 8.0 * g.d.dim);
+        rs += g.d.count * (per + 3 * 8.0 * g.d.dim);
+    }
+    kstats_["local_z"].bytes = lz + 24.0 * n;
+    kstats_["resid"].bytes = rs + 48.0 * n;
+    kstats_["solve"].bytes = solver_.bytes_per_solve();
+    kstats_["rhs"].bytes = 12.0 * (double)dt_row_.n + 8.0 * Z_ + 48.0 * nf_;
+}
+
+void ElasticSolver::upload_pins() {
+    if (!pins_dirty_) return;
+    std::vector<double> p(3 * (size_t)np_);
+    int q = 0;
+    for (auto& kv : pins_) { for (int j = 0; j < 3; ++j) p[3 * q + j] = kv.second[j]; ++q; }
+    if (np_) {
+        const size_t off = 3 * (size_t)nf_;
+        AA_HIP(hipMemcpyAsync(xfull_.p + off, p.data(), p.size() * 8, hipMemcpyHostToDevice, s()));
+        AA_HIP(hipMemcpyAsync(xlast_.p + off, p.data(), p.size() * 8, hipMemcpyHostToDevice, s()));
+        AA_HIP(hipMemcpyAsync(cxfull_.p + off, p.data(), p.size() * 8, hipMemcpyHostToDevice, s()));
+        AA_HIP(hipStreamSynchronize(s()));
+    }
+    pins_dirty_ = false;
+}
+
+void ElasticSolver::ev_begin(const char* name) {
+    if (!instrument_) return;
+    hipEvent_t e;
+    AA_HIP(hipEventCreate(&e));
+    AA_HIP(hipEventRecord(e, s()));
+    kstats_[name].ev.push_back(e);
+}
+void ElasticSolver::ev_end(const char* name) { ev_begin(name); }
+
+void ElasticSolver::local_z_all(const double* xfull, const double* u, double* z, double* y, int mode, bool red) {
+    int off = 0;
+    ev_begin("local_z");
+    for (auto& g : groups_) {
+        launch_local_z(g.d, xfull, u, z, y, nf_, st_.variant, mode, ctrl_.p, red ? red_a_.p : nullptr, off, s());
+        off += blocks_for(g.d.count);
+    }
+    ev_end("local_z");
+}
+
+void ElasticSolver::prologue() {
+    upload_pins();
+    const bool accel = st_.acceleration_type == 1;
+    Ctrl c;
+    std::memset(&c, 0, sizeof(c));
+    c.prev_prim = 1e20;
+    c.cap = hist_cap_;
+    c.aa_m = accel ? st_.anderson_m : 0;
+    c.aa_active = accel ? 1 : 0;
+    AA_HIP(hipMemcpyAsync(ctrl_.p, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s()));
+    launch_predict(n_, nf_, xs_.p, vs_.p, mass_.p, st_.timestep_s, st_.gravity, xbar_.p, Mxbar_.p, xfull_.p, s());
+    for (auto& g : groups_) launch_init_z(g.d, xfull_.p, z_.p, s());
+    u_.zero(s());
+    const long long nx = 3LL * nf_;
+    if (st_.variant == AA_VARIANT_UX) {
+        local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_INIT, false);
+        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
+        solver_.solve(b_.p, xfull_.p, nullptr, 0, s());
+        {
+            int off = 0;
+            for (auto& g : groups_) {
+                launch_resid_update_u(g.d, xfull_.p, xlast_.p, z_.p, u_.p, nf_, ctrl_.p, red_a_.p, red_b_.p, off, s());
+                off += blocks_for(g.d.count);
+            }
+        }
+        launch_copy(du_.p, u_.p, Z_, nullptr, 0, s());
+        launch_copy(dx_.p, xfull_.p, nx, nullptr, 0, s());
+        if (accel) {
+            launch_copy(aa_cur_.p, u_.p, Z_, nullptr, 0, s());
+            launch_copy(aa_cur_.p + Z_, xfull_.p, nx, nullptr, 0, s());
+        }
+    } else {
+        for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 2, 0, ctrl_.p, s());
+        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
+        solver_.solve(b_.p, xfull_.p, nullptr, 0, s());
+        local_z_all(xfull_.p, u_.p, z_.p, nullptr, LZ_INIT, false);
+        launch_copy(dz_.p, z_.p, Z_, nullptr, 0, s());
+        launch_copy(dx_.p, xfull_.p, nx, nullptr, 0, s());
+        launch_copy(du_.p, u_.p, Z_, nullptr, 0, s());
+        if (accel) launch_copy(aa_cur_.p, z_.p, Z_, nullptr, 0, s());
+    }
+}
+
+// admm_anderson_hard_zxu/src/Solver.cpp:130-214
+void ElasticSolver::enqueue_iteration_ux(bool accel) {
+    const long long nx = 3LL * nf_;
+    Ctrl* c = ctrl_.p;
+    local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_NORMAL, true);
+    launch_control(CTL_PRIM_CHECK, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    if (accel) {
+        launch_copy(u_.p, du_.p, Z_, c, 1, s());
+        launch_copy(xfull_.p, dx_.p, nx, c, 1, s());
+        launch_copy(aa_cur_.p, du_.p, Z_, c, 1, s());
+        launch_copy(aa_cur_.p + Z_, dx_.p, nx, c, 1, s());
+        local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_REDO, true);
+    }
+    launch_control(CTL_PRIM_FINAL, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    launch_copy(xlast_.p, xfull_.p, nx, c, 0, s());
+    ev_begin("rhs");
+    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+    ev_end("rhs");
+    ev_begin("solve");
+    solver_.solve(b_.p, xfull_.p, c, 0, s());
+    ev_end("solve");
+    ev_begin("resid");
+    {
+        int off = 0;
+        for (auto& g : groups_) {
+            launch_resid_update_u(g.d, xfull_.p, xlast_.p, z_.p, u_.p, nf_, c, red_a_.p, red_b_.p, off, s());
+            off += blocks_for(g.d.count);
+        }
+    }
+    ev_end("resid");
+    launch_control(CTL_COMB_UX, c, red_a_.p, red_b_.p, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    if (accel) {
+        const int m = st_.anderson_m;
+        Seg2 G{u_.p, Z_, xfull_.p, nx};
+        Seg2 cp{du_.p, Z_, dx_.p, nx};
+        ev_begin("aa");
+        launch_aa_reduce(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, cp, m, s());
+        launch_aa_solve(c, aa_red_.p, aa_blocks_, m, s());
+        launch_aa_mix(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, G, m, s());
+        ev_end("aa");
+    }
+}
+
+// admm_anderson_xzu/src/Solver.cpp:122-251
+void ElasticSolver::enqueue_iteration_z(bool accel) {
+    const long long nx = 3LL * nf_;
+    Ctrl* c = ctrl_.p;
+    for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, accel ? 1 : 0, 0, c, s());
+    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+    ev_begin("solve");
+    solver_.solve(b_.p, xfull_.p, c, 0, s());
+    ev_end("solve");
+    auto prim_all = [&](const double* xf, const double* z, const double* zref, int redo) {
+        int off = 0;
+        for (auto& g : groups_) {
+            launch_prim_z(g.d, xf, z, zref, nf_, redo, c, red_a_.p, zref ? red_b_.p : nullptr, off, s());
+            off += blocks_for(g.d.count);
+        }
+    };
+    prim_all(xfull_.p, z_.p, nullptr, 0);
+    launch_control(CTL_PRIM_CHECK_Z, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    if (accel) {
+        launch_copy(u_.p, du_.p, Z_, c, 1, s());
+        launch_copy(xfull_.p, dx_.p, nx, c, 1, s());
+        launch_copy(z_.p, dz_.p, Z_, c, 1, s());
+        launch_copy(aa_cur_.p, dz_.p, Z_, c, 1, s());   // accelerator.replace(curr_z)
+        for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 0, 1, c, s());
+        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());
+        solver_.solve(b_.p, xfull_.p, c, 1, s());
+        prim_all(xfull_.p, z_.p, nullptr, 1);
+    }
+    launch_control(CTL_PRIM_FINAL_Z, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    if (accel) {
+        const int m = st_.anderson_m;
+        launch_copy(dx_.p, xfull_.p, nx, c, 0, s());
+        launch_copy(du_.p, u_.p, Z_, c, 0, s());
+        local_z_all(xfull_.p, u_.p, dz_.p, nullptr, LZ_NORMAL, false);
+        Seg2 G{dz_.p, Z_, nullptr, 0};
+        Seg2 out{z_.p, Z_, nullptr, 0};
+        Seg2 none{nullptr, 0, nullptr, 0};
+        ev_begin("aa");
+        launch_aa_reduce(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, none, m, s());
+        launch_aa_solve(c, aa_red_.p, aa_blocks_, m, s());
+        launch_aa_mix(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, out, m, s());
+        ev_end("aa");
+        // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
+        for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, dz_.p, u_.p, y_.p, nf_, 2, 0, c, s());
+        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+        solver_.solve(b_.p, cxfull_.p, c, 0, s());
+        local_z_all(cxfull_.p, u_.p, cz_.p, nullptr, LZ_NORMAL, false);
+        prim_all(cxfull_.p, cz_.p, dz_.p, 0);
+    } else {
+        launch_copy(lastz_.p, z_.p, Z_, c, 0, s());
+        local_z_all(xfull_.p, u_.p, z_.p, nullptr, LZ_NORMAL, false);
+        prim_all(xfull_.p, z_.p, lastz_.p, 0);
+    }
+    launch_control(CTL_COMB_Z, c, red_a_.p, red_b_.p, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+}
+
+void ElasticSolver::epilogue_enqueue(bool accel) {
+    const double* src = (st_.variant == AA_VARIANT_UX && accel) ? dx_.p : xfull_.p;
+    launch_finalize(n_, nf_, src, xfull_.p, xs_.p, vs_.p, st_.timestep_s, s());
+}
+
+void ElasticSolver::fetch_results() {
+    Ctrl c;
+    AA_HIP(hipMemcpyAsync(&c, ctrl_.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s()));
+    AA_HIP(hipStreamSynchronize(s()));
+    nrec_ = std::min(c.nrec, hist_cap_);
+    h_prim_.resize(nrec_); h_comb_.resize(nrec_); h_rej_.resize(nrec_);
+    if (nrec_) {
+        AA_HIP(hipMemcpy(h_prim_.data(), hist_prim_.p, nrec_ * 8, hipMemcpyDeviceToHost));
+        AA_HIP(hipMemcpy(h_comb_.data(), hist_comb_.p, nrec_ * 8, hipMemcpyDeviceToHost));
+        AA_HIP(hipMemcpy(h_rej_.data(), hist_rej_.p, nrec_ * 4, hipMemcpyDeviceToHost));
+    }
+    rt_.iterations = c.nrec;
+    rt_.rejects = c.nrej;
+    if (c.fail == 1) throw Error(ERR_NUMERIC, "the line search step became smaller than the minimum value allowed");
+    if (c.fail == 2) throw Error(ERR_NUMERIC, "**TriEnergyTerm TODO: gradient function");
+}
+
+void ElasticSolver::step() {
+    if (!initialized_) throw Error(ERR_STATE, "step() before initialize()");
+    auto t0 = std::chrono::steady_clock::now();
+    const bool accel = st_.acceleration_type == 1;
+    prologue();
+    for (int it = 0; it < st_.admm_iters; ++it) {
+        if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
+        else enqueue_iteration_z(accel);
+    }
+    epilogue_enqueue(accel);
+    fetch_results();
+    // host mirrors of m_x / m_v
+    std::vector<double> xs(3 * (size_t)n_), vs(3 * (size_t)n_);
+    AA_HIP(hipMemcpy(xs.data(), xs_.p, xs.size() * 8, hipMemcpyDeviceToHost));
+    AA_HIP(hipMemcpy(vs.data(), vs_.p, vs.size() * 8, hipMemcpyDeviceToHost));
+    for (int q = 0; q < n_; ++q)
+        for (int j = 0; j < 3; ++j) { x_[3 * (size_t)int2node_[q] + j] = xs[3 * (size_t)q + j]; v_[3 * (size_t)int2node_[q] + j] = vs[3 * (size_t)q + j]; }
+    rt_.step_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void ElasticSolver::get_x(double* out) { std::copy(x_.begin(), x_.end(), out); }
+void ElasticSolver::get_v(double* out) { std::copy(v_.begin(), v_.end(), out); }
+void ElasticSolver::set_v(const double* v3) {
+    std::copy(v3, v3 + v_.size(), v_.begin());
+    if (initialized_) {
+        std::vector<double> vs(3 * (size_t)n_);
+        for (int q = 0; q < n_; ++q) for (int j = 0; j < 3; ++j) vs[3 * (size_t)q + j] = v_[3 * (size_t)int2node_[q] + j];
+        AA_HIP(hipMemcpy(vs_.p, vs.data(), vs.size() * 8, hipMemcpyHostToDevice));
+    }
+}
+
+int ElasticSolver::history(double* prim, double* comb, int* rej, int cap) const {
+    const int n = std::min(cap, nrec_);
+    for (int i = 0; i < n; ++i) {
+        if (prim) prim[i] = h_prim_[i];
+        if (comb) comb[i] = h_comb_[i];
+        if (rej) rej[i] = h_rej_[i];
+    }
+    return nrec_;
+}
+
+double ElasticSolver::bench_iterations(int iters) {
+    if (!initialized_) throw Error(ERR_STATE, "bench before initialize()");
+    const bool accel = st_.acceleration_type == 1;
+    for (auto& kv : kstats_) { for (auto e : kv.second.ev) (void)hipEventDestroy(e); kv.second.ev.clear(); }
+    prologue();
+    AA_HIP(hipStreamSynchronize(s()));
+    instrument_ = true;
+    hipEvent_t e0, e1;
+    AA_HIP(hipEventCreate(&e0)); AA_HIP(hipEventCreate(&e1));
+    AA_HIP(hipEventRecord(e0, s()));
+    for (int it = 0; it < iters; ++it) {
+        if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
+        else enqueue_iteration_z(accel);
+    }
+    AA_HIP(hipEventRecord(e1, s()));
+    AA_HIP(hipEventSynchronize(e1));
+    instrument_ = false;
+    float ms = 0;
+    AA_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+    for (auto& kv : kstats_) {
+        KStat& k = kv.second;
+        k.total_ms = 0; k.launches = 0;
+        for (size_t i = 0; i + 1 < k.ev.size(); i += 2) {
+            float t = 0;
+            AA_HIP(hipEventElapsedTime(&t, k.ev[i], k.ev[i + 1]));
+            k.total_ms += t; k.launches += 1;
+        }
+    }
+    Ctrl c;
+    AA_HIP(hipMemcpy(&c, ctrl_.p, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    rt_.iterations = c.iters_run;
+    rt_.rejects = c.nrej;
+    return ms;
+}
+
+bool ElasticSolver::kernel_stats(const std::string& name, double* avg_ms, double* bytes, int* launches) const {
+    auto it = kstats_.find(name);
+    if (it == kstats_.end()) return false;
+    const KStat& k = it->second;
+    if (avg_ms) *avg_ms = k.launches ? k.total_ms / k.launches : 0.0;
+    if (bytes) *bytes = k.bytes;
+    if (launches) *launches = k.launches;
+    return true;
+}
+
+}  // namespace aa

@@ -1,0 +1,112 @@
+// Host orchestration of the admm-elastic hot path on one MI355X (the reference's
+// admm::Solver, admm_anderson_hard_zxu/src/Solver.{hpp,cpp} and admm_anderson_xzu/src/...).
+#pragma once
+#include <array>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/aa_admm.h"
+#include "common.hpp"
+#include "direct_solve.hpp"
+#include "elastic_kernels.hpp"
+
+namespace aa {
+
+struct Context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+};
+
+class ElasticSolver {
+public:
+    explicit ElasticSolver(Context* ctx) : ctx_(ctx) {}
+    ~ElasticSolver();
+
+    int add_nodes(const double* x3, const double* m3, int n);
+    void add_elements(int kind, int material, const double* verts3, const int* idx, int count, const aa_lame& lame,
+                      int vertex_offset);
+    void set_pins(const int* inds, const double* pts3, int n);
+    void initialize(const aa_settings& s);
+    void step();
+
+    int num_nodes() const { return (int)x_.size() / 3; }
+    void get_x(double* out);
+    void get_v(double* out);
+    void set_v(const double* v3);
+    int history(double* prim, double* comb, int* rej, int cap) const;
+    aa_runtime runtime() const { return rt_; }
+
+    // benchmarking: run `iters` iterations of the ADMM loop body of a fresh time step;
+    // returns device-synchronised wall ms. Per-kernel-class event timings are collected.
+    double bench_iterations(int iters);
+    bool kernel_stats(const std::string& name, double* avg_ms, double* bytes, int* launches) const;
+
+private:
+    struct HostGroup {
+        int kind, material, nv, ncol;
+        aa_lame lame;
+        std::vector<int> idx;       // [count][nv] global node ids
+        std::vector<double> G;      // [count][ncol][nv]
+        std::vector<double> vol, w;
+    };
+    struct DevGroup {
+        DevBuf<int> idx;
+        DevBuf<double> G, w, vol;
+        GroupDev d{};
+    };
+    Context* ctx_;
+    hipStream_t s() const { return ctx_->stream; }
+
+    // host model
+    std::vector<double> x_, v_, m3_;
+    std::vector<HostGroup> hgroups_;
+    std::map<int, std::array<double, 3>> pins_;
+    std::vector<int> pin_order_;
+    aa_settings st_{};
+    bool initialized_ = false;
+
+    // internal numbering: free nodes in nested-dissection order, then pinned (sorted)
+    int n_ = 0, nf_ = 0, np_ = 0;
+    long long Z_ = 0;
+    std::vector<int> node2int_, int2node_;
+    double pdt2_ = 0;
+
+    // device
+    std::vector<DevGroup> groups_;
+    DirectSolver solver_;
+    DevBuf<int> dt_ptr_, dt_row_;
+    DevBuf<double> dt_val_;
+    DevBuf<double> xs_, vs_, mass_, xfull_, xlast_, xbar_, Mxbar_, b_, cxfull_;
+    DevBuf<double> z_, u_, y_, du_, dz_, dx_, lastz_, cz_;
+    DevBuf<double> aa_cur_, aa_dF_, aa_dG_, aa_red_;
+    DevBuf<double> red_a_, red_b_;
+    DevBuf<Ctrl> ctrl_;
+    DevBuf<double> hist_prim_, hist_comb_;
+    DevBuf<int> hist_rej_;
+    int red_blocks_ = 0, aa_blocks_ = 0, hist_cap_ = 0;
+    std::vector<double> h_prim_, h_comb_;
+    std::vector<int> h_rej_;
+    int nrec_ = 0;
+    aa_runtime rt_{};
+    bool pins_dirty_ = true;
+
+    // kernel-class event timing (bench only)
+    bool instrument_ = false;
+    struct KStat { std::vector<hipEvent_t> ev; double bytes = 0; double total_ms = 0; int launches = 0; };
+    std::map<std::string, KStat> kstats_;
+    void ev_begin(const char* name);
+    void ev_end(const char* name);
+
+    void upload_pins();
+    void prologue();
+    void enqueue_iteration_ux(bool accel);
+    void enqueue_iteration_z(bool accel);
+    void epilogue_enqueue(bool accel);
+    void fetch_results();
+    int nb_elems() const { return red_blocks_; }
+    void local_z_all(const double* xfull, const double* u, double* z, double* y, int mode, bool red);
+};
+
+}  // namespace aa

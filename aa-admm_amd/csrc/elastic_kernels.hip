@@ -1,0 +1,741 @@
+// HIP kernels of the admm-elastic hot path (gfx950, wave64, fp64).
+//
+// One thread per energy term for the local step (SoA element data -> coalesced loads; node
+// positions gathered 24 B at a time from an xyz-interleaved array that stays L2/MALL
+// resident), deterministic block partial sums for every residual norm, and a one-block
+// control kernel that makes the reference's data-dependent decisions (Anderson reject,
+// comb < eps break) on the device so the whole ADMM loop is enqueued without host syncs.
+#include "common.hpp"
+#include "device_lbfgs.hpp"
+#include "device_prox.hpp"
+#include "elastic_kernels.hpp"
+
+namespace aa {
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return v;
+}
+
+// deterministic block sum; result valid in thread 0
+__device__ __forceinline__ double block_sum(double v, double* sm) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) sm[wid] = v;
+    __syncthreads();
+    double r = 0;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r += sm[i];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ bool gated(const Ctrl* c, int gate_reject) {
+    if (!c) return false;
+    if (c->done) return true;
+    return gate_reject && !c->reject;
+}
+
+// F = P x_full, Cp = P_pinned x_pin  (EnergyTerm::update_z's D.block*x, Solver.cpp C_fix)
+template <int NV>
+__device__ __forceinline__ void gather_F(const GroupDev& g, int e, const double* __restrict__ xfull, int nf, double* F,
+                                         double* Cp) {
+    constexpr int NC = NV - 1;
+#pragma unroll
+    for (int i = 0; i < 3 * NC; ++i) { F[i] = 0; Cp[i] = 0; }
+#pragma unroll
+    for (int a = 0; a < NV; ++a) {
+        const int v = g.idx[(size_t)a * g.count + e];
+        const double x0 = xfull[3 * (size_t)v], x1 = xfull[3 * (size_t)v + 1], x2 = xfull[3 * (size_t)v + 2];
+        const bool pin = v >= nf;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
+            F[3 * c + 0] += gc * x0; F[3 * c + 1] += gc * x1; F[3 * c + 2] += gc * x2;
+            if (pin) { Cp[3 * c + 0] += gc * x0; Cp[3 * c + 1] += gc * x1; Cp[3 * c + 2] += gc * x2; }
+        }
+    }
+}
+
+template <int NV>
+__device__ __forceinline__ void gather_P(const GroupDev& g, int e, const double* __restrict__ xfull, double* F) {
+    constexpr int NC = NV - 1;
+#pragma unroll
+    for (int i = 0; i < 3 * NC; ++i) F[i] = 0;
+#pragma unroll
+    for (int a = 0; a < NV; ++a) {
+        const int v = g.idx[(size_t)a * g.count + e];
+        const double x0 = xfull[3 * (size_t)v], x1 = xfull[3 * (size_t)v + 1], x2 = xfull[3 * (size_t)v + 2];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
+            F[3 * c + 0] += gc * x0; F[3 * c + 1] += gc * x1; F[3 * c + 2] += gc * x2;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ local step
+template <int NV, int HYPER>
+__global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __restrict__ xfull,
+                                                    const double* __restrict__ u, double* __restrict__ z,
+                                                    double* __restrict__ y, int nf, int variant, int mode, Ctrl* ctrl,
+                                                    double* red, int red_off) {
+    if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
+    __shared__ double sm[kBlock / 64];
+    constexpr int NC = NV - 1, D = 3 * NC;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double part = 0;
+    if (e < g.count) {
+        double F[D], Cp[D], uu[D], vin[D], zz[D];
+        gather_F<NV>(g, e, xfull, nf, F, Cp);
+        const double w = g.w[e];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            uu[i] = u ? u[g.zoff + (size_t)i * g.count + e] : 0.0;
+            vin[i] = F[i] + uu[i] / w;
+        }
+        if constexpr (NV == 3) {
+            dev::tri_prox(vin, zz, variant, g.lmin, g.lmax);
+        } else if constexpr (HYPER == 0) {
+            dev::tet_linear_prox(vin, zz);
+        } else {
+#pragma unroll
+            for (int i = 0; i < D; ++i) zz[i] = vin[i];
+            int fail = 0;
+            dev::hyper_prox(g.mat, g.mu, g.lambda, g.k, g.vol[e], vin, zz, &fail);
+            if (fail && ctrl) ctrl->fail = 1;
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const double r = w * (F[i] - zz[i]);
+            part += r * r;
+            z[g.zoff + (size_t)i * g.count + e] = zz[i];
+        }
+        if (y) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    y[3 * (size_t)(g.yrow + (long long)e * NC + c) + j] = w * (w * zz[3 * c + j] - w * Cp[3 * c + j] - uu[3 * c + j]);
+        }
+    }
+    if (red) {
+        const double s = block_sum(part, sm);
+        if (threadIdx.x == 0) red[red_off + blockIdx.x] = s;
+    }
+}
+
+// r = w(P x - z): prim2 += |r|^2, dual2 += |w P (x - x_last)|^2, u += r
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_resid_u(GroupDev g, const double* __restrict__ xfull,
+                                                    const double* __restrict__ xlast, const double* __restrict__ z,
+                                                    double* __restrict__ u, int nf, Ctrl* ctrl, double* red_a,
+                                                    double* red_b, int red_off) {
+    if (gated(ctrl, 0)) return;
+    __shared__ double sm[kBlock / 64];
+    constexpr int NC = NV - 1, D = 3 * NC;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double pa = 0, pb = 0;
+    if (e < g.count) {
+        double F[D], Fl[D];
+        gather_P<NV>(g, e, xfull, F);
+        gather_P<NV>(g, e, xlast, Fl);
+        const double w = g.w[e];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const size_t o = g.zoff + (size_t)i * g.count + e;
+            const double r = w * (F[i] - z[o]);
+            const double d = w * (F[i] - Fl[i]);
+            pa += r * r;
+            pb += d * d;
+            u[o] += r;
+        }
+    }
+    const double sa = block_sum(pa, sm);
+    const double sb = block_sum(pb, sm);
+    if (threadIdx.x == 0) { red_a[red_off + blockIdx.x] = sa; red_b[red_off + blockIdx.x] = sb; }
+}
+
+// Z variant: u update (mode 0 dual ascent, 1 = W^-1 grad E(z), 2 = keep u) then y = w (w z + c - u)
+template <int NV, int HYPER>
+__global__ __launch_bounds__(kBlock) void k_u_and_y(GroupDev g, const double* __restrict__ xfull,
+                                                    const double* __restrict__ z, double* __restrict__ u,
+                                                    double* __restrict__ y, int nf, int mode, int redo, Ctrl* ctrl) {
+    if (gated(ctrl, redo)) return;
+    constexpr int NC = NV - 1, D = 3 * NC;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= g.count) return;
+    double F[D], Cp[D], zz[D], uu[D];
+    gather_F<NV>(g, e, xfull, nf, F, Cp);
+    const double w = g.w[e];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        const size_t o = g.zoff + (size_t)i * g.count + e;
+        zz[i] = z[o];
+        uu[i] = u[o];
+    }
+    if (mode == 0) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) uu[i] += w * F[i] - w * zz[i];
+    } else if (mode == 1) {
+        double gr[D];
+        if constexpr (NV == 3) {
+            if (ctrl) ctrl->fail = 2;   // TriEnergyTerm::get_gradient throws in the reference
+#pragma unroll
+            for (int i = 0; i < D; ++i) gr[i] = 0;
+        } else if constexpr (HYPER == 0) {
+            dev::tet_linear_grad(zz, g.k * g.vol[e], gr);
+        } else {
+            dev::hyper_psi_grad(g.mat, g.mu, g.lambda, zz, gr);
+#pragma unroll
+            for (int i = 0; i < D; ++i) gr[i] *= g.vol[e];
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) uu[i] = gr[i] / w;
+    }
+    if (mode != 2) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) u[g.zoff + (size_t)i * g.count + e] = uu[i];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            y[3 * (size_t)(g.yrow + (long long)e * NC + c) + j] = w * (w * zz[3 * c + j] - w * Cp[3 * c + j] - uu[3 * c + j]);
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_prim_z(GroupDev g, const double* __restrict__ xfull,
+                                                   const double* __restrict__ z, const double* __restrict__ zref,
+                                                   int nf, int redo, Ctrl* ctrl, double* red_a, double* red_b,
+                                                   int red_off) {
+    if (gated(ctrl, redo)) return;
+    __shared__ double sm[kBlock / 64];
+    constexpr int NC = NV - 1, D = 3 * NC;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double pa = 0, pb = 0;
+    if (e < g.count) {
+        double F[D];
+        gather_P<NV>(g, e, xfull, F);
+        const double w = g.w[e];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const size_t o = g.zoff + (size_t)i * g.count + e;
+            const double zi = z[o];
+            const double r = w * (F[i] - zi);
+            pa += r * r;
+            if (zref) { const double d = w * (zi - zref[o]); pb += d * d; }
+        }
+    }
+    const double sa = block_sum(pa, sm);
+    const double sb = block_sum(pb, sm);
+    if (threadIdx.x == 0) { red_a[red_off + blockIdx.x] = sa; if (red_b) red_b[red_off + blockIdx.x] = sb; }
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_init_z(GroupDev g, const double* __restrict__ xfull, double* __restrict__ z) {
+    constexpr int NC = NV - 1, D = 3 * NC;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= g.count) return;
+    double F[D];
+    gather_P<NV>(g, e, xfull, F);
+#pragma unroll
+    for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * g.count + e] = F[i];
+}
+
+// ------------------------------------------------------------------ global rhs (D^T gather)
+__global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ ptr, const int* __restrict__ row,
+                                                const double* __restrict__ val, const double* __restrict__ y,
+                                                const double* __restrict__ Mxbar, double pdt2, double* __restrict__ b,
+                                                const Ctrl* ctrl, int gate_reject) {
+    if (gated(ctrl, gate_reject)) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nf) return;
+    double s0 = 0, s1 = 0, s2 = 0;
+    for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
+        const double v = val[k];
+        const size_t r = 3 * (size_t)row[k];
+        s0 += v * y[r]; s1 += v * y[r + 1]; s2 += v * y[r + 2];
+    }
+    b[3 * (size_t)i + 0] = Mxbar[3 * (size_t)i + 0] + pdt2 * s0;
+    b[3 * (size_t)i + 1] = Mxbar[3 * (size_t)i + 1] + pdt2 * s1;
+    b[3 * (size_t)i + 2] = Mxbar[3 * (size_t)i + 2] + pdt2 * s2;
+}
+
+// ------------------------------------------------------------------ control (one block)
+__global__ __launch_bounds__(kBlock) void k_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b,
+                                                    int nb, int accel, double* hist_prim, double* hist_comb,
+                                                    int* hist_rej) {
+    if (ctrl->done) return;
+    __shared__ double sm[kBlock / 64];
+    double a = 0, b = 0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) { a += red_a[i]; if (red_b) b += red_b[i]; }
+    a = block_sum(a, sm);
+    b = block_sum(b, sm);
+    if (threadIdx.x != 0) return;
+    switch (op) {
+        case CTL_PRIM_CHECK:
+        case CTL_PRIM_CHECK_Z: {
+            const double prim = sqrt(a);
+            ctrl->prim = prim;
+            ctrl->reject = (accel && ctrl->prev_prim < prim) ? 1 : 0;
+            if (ctrl->reject) {
+                ctrl->nrej += 1;
+                if (op == CTL_PRIM_CHECK) { ctrl->aa_iter = 0; ctrl->aa_col = 0; }  // accelerator->reset
+            }
+            break;
+        }
+        case CTL_PRIM_FINAL:
+        case CTL_PRIM_FINAL_Z:
+            if (ctrl->reject) ctrl->prim = sqrt(a);
+            ctrl->prev_prim = ctrl->prim;
+            break;
+        case CTL_COMB_UX: {
+            const double comb = a + b;
+            ctrl->iters_run += 1;
+            ctrl->comb = comb;
+            if (comb < kCombEps) { ctrl->done = 1; break; }
+            const int k = ctrl->nrec;
+            if (k < ctrl->cap) { hist_prim[k] = ctrl->prim; hist_comb[k] = comb; hist_rej[k] = ctrl->reject; }
+            ctrl->nrec = k + 1;
+            break;
+        }
+        case CTL_COMB_Z: {
+            const double comb = a + b;
+            ctrl->iters_run += 1;
+            ctrl->comb = comb;
+            const int k = ctrl->nrec;
+            if (k < ctrl->cap) { hist_prim[k] = ctrl->prim; hist_comb[k] = comb; hist_rej[k] = ctrl->reject; }
+            ctrl->nrec = k + 1;
+            if (comb < kCombEps) ctrl->done = 1;
+            break;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ dst, const double* __restrict__ src,
+                                                 long long n, const Ctrl* ctrl, int gate_reject) {
+    if (gated(ctrl, gate_reject)) return;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_predict(int nf, double* __restrict__ xs, double* __restrict__ vs,
+                                                    const double* __restrict__ mass, double dt, double gravity,
+                                                    double* __restrict__ xbar, double* __restrict__ Mxbar,
+                                                    double* __restrict__ xfull) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nf) return;
+    if (fabs(gravity) > 0) vs[3 * (size_t)q + 1] += dt * gravity;
+    const double m = mass[q];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const size_t o = 3 * (size_t)q + j;
+        const double xb = xs[o] + dt * vs[o];
+        xbar[o] = xb;
+        Mxbar[o] = m * xb;
+        xfull[o] = xb;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_finalize(int n, int nf, const double* __restrict__ xsrc,
+                                                     const double* __restrict__ xfull, double* __restrict__ xs,
+                                                     double* __restrict__ vs, double dt) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const double inv = 1.0 / dt;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const size_t o = 3 * (size_t)q + j;
+        const double xn = q < nf ? xsrc[o] : xfull[o];
+        vs[o] = (xn - xs[o]) * inv;
+        xs[o] = xn;
+    }
+}
+
+// ------------------------------------------------------------------ Anderson acceleration
+__device__ __forceinline__ double seg_get(const Seg2& s, long long i) { return i < s.na ? s.a[i] : s.b[i - s.na]; }
+__device__ __forceinline__ void seg_set(const Seg2& s, long long i, double v) { if (i < s.na) s.a[i] = v; else s.b[i - s.na] = v; }
+
+// pass 1: dF_j += F, dG_j += G and the partial sums for |dF_j|^2, dF_j.F, dF_j.dF_c, dF_c.F
+template <int MM>
+__global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __restrict__ cur, long long eff,
+                                                      double* __restrict__ dF, double* __restrict__ dG, Ctrl* ctrl,
+                                                      double* red, Seg2 copy_to) {
+    if (ctrl->done || !ctrl->aa_active) return;
+    constexpr int NVAL = 2 + 2 * MM;
+    __shared__ double sm[kBlock / 64][NVAL];
+    const long long dim = G.na + G.nb;
+    const int iter = ctrl->aa_iter, col = ctrl->aa_col, m = ctrl->aa_m;
+    const int mk = iter < m ? iter : m;
+    double acc[NVAL];
+#pragma unroll
+    for (int t = 0; t < NVAL; ++t) acc[t] = 0;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < dim; i += (long long)gridDim.x * blockDim.x) {
+        const double g = seg_get(G, i);
+        if (copy_to.a) seg_set(copy_to, i, g);
+        if (iter == 0) continue;
+        dG[(size_t)col * dim + i] += g;
+        if (i < eff) {
+            const double f = g - cur[i];
+            const double dfj = dF[(size_t)col * eff + i] + f;
+            dF[(size_t)col * eff + i] = dfj;
+            acc[0] += dfj * dfj;
+            acc[1] += dfj * f;
+#pragma unroll
+            for (int c = 0; c < MM; ++c) {
+                if (c < mk && c != col) {
+                    const double dfc = dF[(size_t)c * eff + i];
+                    acc[2 + c] += dfj * dfc;
+                    acc[2 + MM + c] += dfc * f;
+                }
+            }
+        }
+    }
+    if (iter == 0) return;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int t = 0; t < NVAL; ++t) {
+        const double v = wave_sum(acc[t]);
+        if (lane == 0) sm[wid][t] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NVAL) {
+        double s = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sm[w][threadIdx.x];
+        red[(size_t)blockIdx.x * NVAL + threadIdx.x] = s;
+    }
+}
+
+// Eigen CompleteOrthogonalDecomposition::solve of the small normal equations (one thread).
+// Column-pivoted Householder QR with LAPACK norm downdating, rank = #|R_ii| > eps*n*maxpivot,
+// RZ step for the rank-deficient case, minimum-norm solution.
+__device__ void cod_solve_dev(int n, double* A /* n*n col-major, destroyed */, const double* b, double* x) {
+    double hc[kMaxM], nu[kMaxM], nd[kMaxM], zc[kMaxM], c[kMaxM], yv[kMaxM];
+    int perm[kMaxM], tr[kMaxM];
+#define QR(r, cc) A[(cc) * n + (r)]
+    for (int k = 0; k < n; ++k) {
+        double s = 0;
+        for (int r = 0; r < n; ++r) s += QR(r, k) * QR(r, k);
+        nd[k] = nu[k] = sqrt(s);
+    }
+    const double ddt = sqrt(2.220446049250313e-16);
+    double maxpivot = 0;
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        for (int j = k + 1; j < n; ++j) if (nu[j] > nu[big]) big = j;
+        tr[k] = big;
+        if (big != k) {
+            for (int r = 0; r < n; ++r) { double t = QR(r, k); QR(r, k) = QR(r, big); QR(r, big) = t; }
+            double t = nu[k]; nu[k] = nu[big]; nu[big] = t;
+            t = nd[k]; nd[k] = nd[big]; nd[big] = t;
+        }
+        const double c0 = QR(k, k);
+        double tail = 0;
+        for (int r = k + 1; r < n; ++r) tail += QR(r, k) * QR(r, k);
+        double beta, tau;
+        if (tail <= 2.2250738585072014e-308) { tau = 0; beta = c0; for (int r = k + 1; r < n; ++r) QR(r, k) = 0; }
+        else {
+            beta = sqrt(c0 * c0 + tail);
+            if (c0 >= 0) beta = -beta;
+            for (int r = k + 1; r < n; ++r) QR(r, k) /= (c0 - beta);
+            tau = (beta - c0) / beta;
+        }
+        hc[k] = tau;
+        QR(k, k) = beta;
+        maxpivot = fmax(maxpivot, fabs(beta));
+        if (tau != 0)
+            for (int cc = k + 1; cc < n; ++cc) {
+                double t = QR(k, cc);
+                for (int r = k + 1; r < n; ++r) t += QR(r, k) * QR(r, cc);
+                QR(k, cc) -= tau * t;
+                for (int r = k + 1; r < n; ++r) QR(r, cc) -= tau * QR(r, k) * t;
+            }
+        for (int j = k + 1; j < n; ++j) {
+            if (nu[j] != 0) {
+                double t = fabs(QR(k, j)) / nu[j];
+                t = (1.0 + t) * (1.0 - t);
+                t = t < 0 ? 0 : t;
+                const double r2 = nu[j] / nd[j];
+                if (t * r2 * r2 <= ddt) {
+                    double s = 0;
+                    for (int r = k + 1; r < n; ++r) s += QR(r, j) * QR(r, j);
+                    nd[j] = nu[j] = sqrt(s);
+                } else nu[j] *= sqrt(t);
+            }
+        }
+    }
+    for (int i = 0; i < n; ++i) perm[i] = i;
+    for (int k = 0; k < n; ++k) { int t = perm[k]; perm[k] = perm[tr[k]]; perm[tr[k]] = t; }
+    const double thr = fabs(maxpivot) * 2.220446049250313e-16 * n;
+    int rank = 0;
+    for (int i = 0; i < n; ++i) rank += fabs(QR(i, i)) > thr;
+    for (int i = 0; i < n; ++i) zc[i] = 0;
+    if (rank == 0) { for (int i = 0; i < n; ++i) x[i] = 0; return; }
+    if (rank < n) {
+        for (int k = rank - 1; k >= 0; --k) {
+            if (k != rank - 1) for (int r = 0; r <= k; ++r) { double t = QR(r, k); QR(r, k) = QR(r, rank - 1); QR(r, rank - 1) = t; }
+            const double c0 = QR(k, rank - 1);
+            double tail = 0;
+            for (int cc = rank; cc < n; ++cc) tail += QR(k, cc) * QR(k, cc);
+            double beta, tau;
+            if (tail <= 2.2250738585072014e-308) { tau = 0; beta = c0; for (int cc = rank; cc < n; ++cc) QR(k, cc) = 0; }
+            else {
+                beta = sqrt(c0 * c0 + tail);
+                if (c0 >= 0) beta = -beta;
+                for (int cc = rank; cc < n; ++cc) QR(k, cc) /= (c0 - beta);
+                tau = (beta - c0) / beta;
+            }
+            zc[k] = tau;
+            QR(k, rank - 1) = beta;
+            if (k > 0 && tau != 0)
+                for (int r = 0; r < k; ++r) {
+                    double t = QR(r, rank - 1);
+                    for (int cc = rank; cc < n; ++cc) t += QR(r, cc) * QR(k, cc);
+                    QR(r, rank - 1) -= tau * t;
+                    for (int cc = rank; cc < n; ++cc) QR(r, cc) -= tau * t * QR(k, cc);
+                }
+            if (k != rank - 1) for (int r = 0; r <= k; ++r) { double t = QR(r, k); QR(r, k) = QR(r, rank - 1); QR(r, rank - 1) = t; }
+        }
+    }
+    for (int i = 0; i < n; ++i) c[i] = b[i];
+    for (int k = 0; k < rank; ++k) {
+        if (hc[k] == 0) continue;
+        double t = c[k];
+        for (int r = k + 1; r < n; ++r) t += QR(r, k) * c[r];
+        c[k] -= hc[k] * t;
+        for (int r = k + 1; r < n; ++r) c[r] -= hc[k] * QR(r, k) * t;
+    }
+    for (int i = 0; i < n; ++i) yv[i] = 0;
+    for (int i = rank - 1; i >= 0; --i) {
+        double s = c[i];
+        for (int j = i + 1; j < rank; ++j) s -= QR(i, j) * yv[j];
+        yv[i] = s / QR(i, i);
+    }
+    if (rank < n) {
+        for (int k = 0; k < rank; ++k) {
+            if (k != rank - 1) { double t = yv[k]; yv[k] = yv[rank - 1]; yv[rank - 1] = t; }
+            if (zc[k] != 0) {
+                double t = yv[rank - 1];
+                for (int cc = rank; cc < n; ++cc) t += QR(k, cc) * yv[cc];
+                yv[rank - 1] -= zc[k] * t;
+                for (int cc = rank; cc < n; ++cc) yv[cc] -= zc[k] * QR(k, cc) * t;
+            }
+            if (k != rank - 1) { double t = yv[k]; yv[k] = yv[rank - 1]; yv[rank - 1] = t; }
+        }
+    }
+    for (int i = 0; i < n; ++i) x[perm[i]] = yv[i];
+#undef QR
+}
+
+template <int MM>
+__global__ __launch_bounds__(kBlock) void k_aa_solve(Ctrl* ctrl, const double* red, int nb) {
+    if (ctrl->done || !ctrl->aa_active) return;
+    constexpr int NVAL = 2 + 2 * MM;
+    __shared__ double tot[NVAL];
+    const int iter = ctrl->aa_iter;
+    if (iter > 0 && threadIdx.x < NVAL) {
+        double s = 0;
+        for (int b = 0; b < nb; ++b) s += red[(size_t)b * NVAL + threadIdx.x];
+        tot[threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const int m = ctrl->aa_m, col = ctrl->aa_col;
+    if (iter == 0) {
+        ctrl->aa_first = 1; ctrl->aa_j = 0; ctrl->aa_jn = 0; ctrl->aa_mk = 0;
+        ctrl->aa_iter = 1;
+        return;
+    }
+    const int mk = iter < m ? iter : m;
+    const double eps = 1e-14;
+    const double s = fmax(eps, sqrt(tot[0]));
+    ctrl->scale[col] = s;
+    double theta[kMaxM];
+    if (mk == 1) {
+        theta[0] = 0;
+        const double sq = tot[0] / (s * s);
+        ctrl->M[0] = sq;
+        const double dn = sqrt(sq);
+        if (dn > eps) theta[0] = (tot[1] / s) / (dn * dn);
+    } else {
+        double rhs[kMaxM], Mk[kMaxM * kMaxM];
+        for (int c = 0; c < mk; ++c) {
+            if (c == col) continue;
+            const double v = tot[2 + c] / s;
+            ctrl->M[c * m + col] = v;
+            ctrl->M[col * m + c] = v;
+            rhs[c] = tot[2 + MM + c];
+        }
+        ctrl->M[col * m + col] = tot[0] / (s * s);
+        rhs[col] = tot[1] / s;
+        for (int c = 0; c < mk; ++c)
+            for (int r = 0; r < mk; ++r) Mk[c * mk + r] = ctrl->M[c * m + r];
+        cod_solve_dev(mk, Mk, rhs, theta);
+    }
+    for (int c = 0; c < mk; ++c) ctrl->coef[c] = theta[c] / ctrl->scale[c];
+    ctrl->aa_first = 0;
+    ctrl->aa_j = col;
+    ctrl->aa_jn = (col + 1) % m;
+    ctrl->aa_mk = mk;
+    ctrl->aa_s = s;
+    ctrl->aa_col = (col + 1) % m;
+    ctrl->aa_iter = iter + 1;
+}
+
+// pass 2: u = G - dG theta/scale, normalise dF_j, start the next column with -F / -G
+template <int MM>
+__global__ __launch_bounds__(kBlock) void k_aa_mix(Seg2 G, double* __restrict__ cur, long long eff,
+                                                   double* __restrict__ dF, double* __restrict__ dG, Ctrl* ctrl,
+                                                   Seg2 out) {
+    if (ctrl->done || !ctrl->aa_active) return;
+    const long long dim = G.na + G.nb;
+    const int first = ctrl->aa_first, j = ctrl->aa_j, jn = ctrl->aa_jn, mk = ctrl->aa_mk;
+    const double s = ctrl->aa_s;
+    double coef[MM];
+#pragma unroll
+    for (int c = 0; c < MM; ++c) coef[c] = c < mk ? ctrl->coef[c] : 0.0;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < dim; i += (long long)gridDim.x * blockDim.x) {
+        const double g = seg_get(G, i);
+        const double f = i < eff ? g - cur[i] : 0.0;
+        double res;
+        if (first) {
+            res = g;
+        } else {
+            double acc = 0;
+#pragma unroll
+            for (int c = 0; c < MM; ++c)
+                if (c < mk) acc += dG[(size_t)c * dim + i] * coef[c];
+            res = g - acc;
+            if (i < eff) dF[(size_t)j * eff + i] = dF[(size_t)j * eff + i] / s;
+        }
+        if (i < eff) dF[(size_t)jn * eff + i] = -f;
+        dG[(size_t)jn * dim + i] = -g;
+        seg_set(out, i, res);
+        cur[i] = res;
+    }
+}
+
+inline int grid_for(long long n) { long long b = (n + kBlock - 1) / kBlock; return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048); }
+
+}  // namespace
+
+// ============================================================================ launchers
+void launch_local_z(const GroupDev& g, const double* xfull, const double* u, double* z, double* y, int nf,
+                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s) {
+    if (g.count == 0) return;
+    const int nb = blocks_for(g.count);
+    if (g.kind == 1) hipLaunchKernelGGL((k_local_z<3, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
+    else if (g.mat == 0) hipLaunchKernelGGL((k_local_z<4, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
+    else hipLaunchKernelGGL((k_local_z<4, 1>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_resid_update_u(const GroupDev& g, const double* xfull, const double* xlast, const double* z, double* u,
+                           int nf, Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s) {
+    if (g.count == 0) return;
+    const int nb = blocks_for(g.count);
+    if (g.kind == 1) hipLaunchKernelGGL(k_resid_u<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, xlast, z, u, nf, ctrl, red_a, red_b, red_off);
+    else hipLaunchKernelGGL(k_resid_u<4>, dim3(nb), dim3(kBlock), 0, s, g, xfull, xlast, z, u, nf, ctrl, red_a, red_b, red_off);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_u_and_y(const GroupDev& g, const double* xfull, const double* z, double* u, double* y, int nf, int mode,
+                    int redo, Ctrl* ctrl, hipStream_t s) {
+    if (g.count == 0) return;
+    const int nb = blocks_for(g.count);
+    if (g.kind == 1) hipLaunchKernelGGL((k_u_and_y<3, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, z, u, y, nf, mode, redo, ctrl);
+    else if (g.mat == 0) hipLaunchKernelGGL((k_u_and_y<4, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, z, u, y, nf, mode, redo, ctrl);
+    else hipLaunchKernelGGL((k_u_and_y<4, 1>), dim3(nb), dim3(kBlock), 0, s, g, xfull, z, u, y, nf, mode, redo, ctrl);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_prim_z(const GroupDev& g, const double* xfull, const double* z, const double* zref, int nf, int redo,
+                   Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s) {
+    if (g.count == 0) return;
+    const int nb = blocks_for(g.count);
+    if (g.kind == 1) hipLaunchKernelGGL(k_prim_z<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z, zref, nf, redo, ctrl, red_a, red_b, red_off);
+    else hipLaunchKernelGGL(k_prim_z<4>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z, zref, nf, redo, ctrl, red_a, red_b, red_off);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_init_z(const GroupDev& g, const double* xfull, double* z, hipStream_t s) {
+    if (g.count == 0) return;
+    const int nb = blocks_for(g.count);
+    if (g.kind == 1) hipLaunchKernelGGL(k_init_z<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z);
+    else hipLaunchKernelGGL(k_init_z<4>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const double* y, const double* Mxbar,
+                double pdt2, double* b, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
+    if (nf == 0) return;
+    hipLaunchKernelGGL(k_rhs, dim3(blocks_for(nf)), dim3(kBlock), 0, s, nf, ptr, row, val, y, Mxbar, pdt2, b, ctrl, gate_reject);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b, int nblocks, int accel,
+                    double* hist_prim, double* hist_comb, int* hist_rej, hipStream_t s) {
+    hipLaunchKernelGGL(k_control, dim3(1), dim3(kBlock), 0, s, op, ctrl, red_a, red_b, nblocks, accel, hist_prim, hist_comb, hist_rej);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_copy(double* dst, const double* src, long long n, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_copy, dim3(grid_for(n)), dim3(kBlock), 0, s, dst, src, n, ctrl, gate_reject);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_predict(int n, int nf, double* xstate, double* vstate, const double* mass, double dt, double gravity,
+                    double* xbar, double* Mxbar, double* xfull, hipStream_t s) {
+    (void)n;
+    if (nf == 0) return;
+    hipLaunchKernelGGL(k_predict, dim3(blocks_for(nf)), dim3(kBlock), 0, s, nf, xstate, vstate, mass, dt, gravity, xbar, Mxbar, xfull);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_finalize(int n, int nf, const double* xsrc, const double* xfull, double* xstate, double* vstate, double dt,
+                     hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_finalize, dim3(blocks_for(n)), dim3(kBlock), 0, s, n, nf, xsrc, xfull, xstate, vstate, dt);
+    AA_CHECK_LAUNCH();
+}
+
+int aa_reduce_blocks(long long dim) { return grid_for(dim) < 1024 ? grid_for(dim) : 1024; }
+
+static int mm_bucket(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : 32); }
+
+void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, double* red,
+                      int nblocks, Seg2 copy_to, int m, hipStream_t s) {
+    switch (mm_bucket(m)) {
+        case 8: hipLaunchKernelGGL(k_aa_reduce<8>, dim3(nblocks), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, red, copy_to); break;
+        case 16: hipLaunchKernelGGL(k_aa_reduce<16>, dim3(nblocks), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, red, copy_to); break;
+        default: hipLaunchKernelGGL(k_aa_reduce<32>, dim3(nblocks), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, red, copy_to); break;
+    }
+    AA_CHECK_LAUNCH();
+}
+
+void launch_aa_solve(Ctrl* ctrl, const double* red, int nblocks, int m, hipStream_t s) {
+    switch (mm_bucket(m)) {
+        case 8: hipLaunchKernelGGL(k_aa_solve<8>, dim3(1), dim3(kBlock), 0, s, ctrl, red, nblocks); break;
+        case 16: hipLaunchKernelGGL(k_aa_solve<16>, dim3(1), dim3(kBlock), 0, s, ctrl, red, nblocks); break;
+        default: hipLaunchKernelGGL(k_aa_solve<32>, dim3(1), dim3(kBlock), 0, s, ctrl, red, nblocks); break;
+    }
+    AA_CHECK_LAUNCH();
+}
+
+void launch_aa_mix(Seg2 G, double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, Seg2 out, int m,
+                   hipStream_t s) {
+    const long long dim = G.na + G.nb;
+    switch (mm_bucket(m)) {
+        case 8: hipLaunchKernelGGL(k_aa_mix<8>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
+        case 16: hipLaunchKernelGGL(k_aa_mix<16>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
+        default: hipLaunchKernelGGL(k_aa_mix<32>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
+    }
+    AA_CHECK_LAUNCH();
+}
+
+}  // namespace aa

@@ -1,0 +1,92 @@
+// Device data structures and kernel launchers of the admm-elastic hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace aa {
+
+constexpr int kMaxM = 32;          // largest Anderson window supported on device
+constexpr double kCombEps = 1e-20; // Solver.cpp:93 eps
+
+// One homogeneous block of energy terms (same kind / material / Lame), SoA on device.
+struct GroupDev {
+    int kind;            // 0 tet, 1 tri
+    int mat;             // 0 linear, 1 NeoHookean, 2 StVK
+    int count;           // elements
+    int nv, ncol, dim;   // 4/3/9 for tets, 3/2/6 for tris
+    long long zoff;      // z/u offset: component c of element e at zoff + c*count + e
+    long long yrow;      // first row of this group in the (Z/3) x 3 row array y
+    const int* idx;      // [nv][count] internal node ids
+    const double* G;     // [(c*nv + a)][count]  F[:,c] = sum_a G[c][a] x_a
+    const double* w;     // [count] ADMM weights sqrt(k*vol)
+    const double* vol;   // [count]
+    double mu, lambda, k, lmin, lmax;
+};
+
+// Device-side control block: residual bookkeeping, reject/done flags, Anderson state.
+struct Ctrl {
+    double prim, prev_prim, comb, prim2, dual2;
+    int reject, done, nrec, nrej;
+    int cap, fail, iters_run, pad1;
+    // Anderson acceleration (AndersonAcceleration.h state)
+    int aa_m, aa_iter, aa_col, aa_mk;
+    int aa_j, aa_jn, aa_first, aa_active;
+    double aa_s;
+    double scale[kMaxM], coef[kMaxM];
+    double M[kMaxM * kMaxM];      // normal-equation matrix, column-major m x m
+};
+
+// A vector seen as two concatenated segments (e.g. (u, x) of the UX variant).
+struct Seg2 {
+    double* a; long long na;
+    double* b; long long nb;
+};
+
+struct ElasticLaunch;  // fwd
+
+// ---- launchers (elastic_kernels.hip) ---------------------------------------------------
+enum LocalMode { LZ_NORMAL = 0, LZ_REDO = 1, LZ_INIT = 2 };
+
+// z = prox(P x + u/w); prim partials; optional y = w(w z + c - u). gate: !done (and reject for REDO)
+void launch_local_z(const GroupDev& g, const double* xfull, const double* u, double* z, double* y, int nf,
+                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s);
+// r = w(P x - z); prim2/dual2 partials; u += r (UX variant update_u fused with the residual)
+void launch_resid_update_u(const GroupDev& g, const double* xfull, const double* xlast, const double* z, double* u,
+                           int nf, Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s);
+// Z variant: u += w(Px - z) [mode 0] or u = grad E(z)/w [mode 1]; then y = w(w z + c - u). gate !done (+reject if redo)
+void launch_u_and_y(const GroupDev& g, const double* xfull, const double* z, double* u, double* y, int nf, int mode,
+                    int redo, Ctrl* ctrl, hipStream_t s);
+// prim2 partials of |w(Px - z)|^2 and optionally dual2 partials of |w(z - zref)|^2. gate !done (+reject if redo)
+void launch_prim_z(const GroupDev& g, const double* xfull, const double* z, const double* zref, int nf, int redo,
+                   Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s);
+// b = Mxbar + pdt2 * (D^T rows) . y
+void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const double* y, const double* Mxbar,
+                double pdt2, double* b, const Ctrl* ctrl, int gate_reject, hipStream_t s);
+// control steps
+enum CtlOp { CTL_PRIM_CHECK = 0, CTL_PRIM_FINAL = 1, CTL_COMB_UX = 2, CTL_PRIM_CHECK_Z = 3, CTL_PRIM_FINAL_Z = 4,
+             CTL_COMB_Z = 5 };
+void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b, int nblocks, int accel,
+                    double* hist_prim, double* hist_comb, int* hist_rej, hipStream_t s);
+// dst = src (gate: !done, and reject if gate_reject)
+void launch_copy(double* dst, const double* src, long long n, const Ctrl* ctrl, int gate_reject, hipStream_t s);
+// predictor: v_y += dt g (free); xbar = x + dt v; Mxbar = m xbar; xfull = xbar (free) / xpin (pinned)
+void launch_predict(int n, int nf, double* xstate, double* vstate, const double* mass, double dt, double gravity,
+                    double* xbar, double* Mxbar, double* xfull, hipStream_t s);
+// z = P xbar (initial z = W^-1 (D xbar - C))
+void launch_init_z(const GroupDev& g, const double* xfull, double* z, hipStream_t s);
+// new state: x = xsrc (free) / xfull (pinned); v = (x_new - x_old)/dt
+void launch_finalize(int n, int nf, const double* xsrc, const double* xfull, double* xstate, double* vstate, double dt,
+                     hipStream_t s);
+
+// ---- Anderson acceleration (device-side AndersonAcceleration::compute_impl) -----------
+// G: the fixed-point map output (2 segments); cur: the stored current iterate (current_u_);
+// dF/dG: history (column-major, eff x m / dim x m); copy_to: optional copy of G (the
+// "default" iterate kept for the reject test); out: where the accelerated iterate goes.
+// m: window (selects the register-resident accumulator bucket 8/16/32).
+int aa_reduce_blocks(long long dim);
+void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, double* red,
+                      int nblocks, Seg2 copy_to, int m, hipStream_t s);
+void launch_aa_solve(Ctrl* ctrl, const double* red, int nblocks, int m, hipStream_t s);
+void launch_aa_mix(Seg2 G, double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, Seg2 out, int m,
+                   hipStream_t s);
+
+}  // namespace aa

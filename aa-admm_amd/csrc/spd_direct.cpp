@@ -1,0 +1,225 @@
+// Host-side nested dissection + multifrontal Cholesky (see spd_direct.hpp).
+#include "spd_direct.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <functional>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+
+namespace aa {
+
+// ------------------------------------------------------------------ nested dissection
+namespace {
+struct NdBuilder {
+    int n;
+    const double* xyz;
+    const std::vector<int>& ap;
+    const std::vector<int>& aj;
+    int leaf;
+    std::vector<int> mark, side;
+    int stamp = 0;
+    // output tree under construction (nodes appended in postorder)
+    std::vector<std::vector<int>> piv;       // pivots (old ids) per node
+    std::vector<std::vector<int>> kids;
+
+    NdBuilder(int n_, const double* x_, const std::vector<int>& p_, const std::vector<int>& j_, int l_)
+        : n(n_), xyz(x_), ap(p_), aj(j_), leaf(l_), mark(n_, 0), side(n_, 0) {}
+
+    // returns the list of root node ids of the forest built over `verts`
+    std::vector<int> build(std::vector<int> verts) {
+        if (verts.empty()) return {};
+        if ((int)verts.size() <= leaf) {
+            std::sort(verts.begin(), verts.end());
+            piv.push_back(verts);
+            kids.push_back({});
+            return {(int)piv.size() - 1};
+        }
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (int v : verts)
+            for (int d = 0; d < 3; ++d) { lo[d] = std::min(lo[d], xyz[3 * v + d]); hi[d] = std::max(hi[d], xyz[3 * v + d]); }
+        int ax = 0;
+        for (int d = 1; d < 3; ++d) if (hi[d] - lo[d] > hi[ax] - lo[ax]) ax = d;
+        auto key = [&](int v) { return xyz[3 * v + ax]; };
+        const size_t half = verts.size() / 2;
+        std::nth_element(verts.begin(), verts.begin() + half, verts.end(), [&](int a, int b) {
+            double ka = key(a), kb = key(b);
+            return ka < kb || (ka == kb && a < b);
+        });
+        const int st = ++stamp;
+        for (size_t i = 0; i < verts.size(); ++i) { mark[verts[i]] = st; side[verts[i]] = i < half ? 0 : 1; }
+        std::vector<int> left, right, sep;
+        for (size_t i = 0; i < verts.size(); ++i) {
+            int v = verts[i];
+            if (i >= half) { right.push_back(v); continue; }
+            bool touches = false;
+            for (int k = ap[v]; k < ap[v + 1] && !touches; ++k) {
+                int u = aj[k];
+                touches = mark[u] == st && side[u] == 1;
+            }
+            (touches ? sep : left).push_back(v);
+        }
+        if (left.empty() && right.empty()) {  // degenerate: everything is separator
+            std::sort(sep.begin(), sep.end());
+            piv.push_back(sep);
+            kids.push_back({});
+            return {(int)piv.size() - 1};
+        }
+        std::vector<int> roots = build(std::move(left));
+        std::vector<int> r2 = build(std::move(right));
+        roots.insert(roots.end(), r2.begin(), r2.end());
+        if (sep.empty()) return roots;
+        std::sort(sep.begin(), sep.end());
+        piv.push_back(sep);
+        kids.push_back(roots);
+        return {(int)piv.size() - 1};
+    }
+};
+}  // namespace
+
+NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
+                         int leaf_size) {
+    NdBuilder b(n, xyz, adj_ptr, adj, std::max(1, leaf_size));
+    std::vector<int> all(n);
+    std::iota(all.begin(), all.end(), 0);
+    std::vector<int> roots = b.build(all);
+    // nodes were appended in postorder (children before parents): assign new indices in that order
+    NdTree t;
+    const int nn = (int)b.piv.size();
+    t.beg.resize(nn); t.end.resize(nn); t.parent.assign(nn, -1); t.children = b.kids;
+    int c = 0;
+    for (int s = 0; s < nn; ++s) {
+        t.beg[s] = c;
+        for (int v : b.piv[s]) t.perm.push_back(v);
+        c += (int)b.piv[s].size();
+        t.end[s] = c;
+        for (int k : b.kids[s]) t.parent[k] = s;
+    }
+    (void)roots;
+    if (c != n) throw std::runtime_error("nested_dissection: lost vertices");
+    return t;
+}
+
+// ------------------------------------------------------------------ multifrontal Cholesky
+SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree) {
+    SupernodalFactor F;
+    const int n = A.n, nn = (int)tree.beg.size();
+    F.n = n; F.n_nodes = nn;
+    F.beg = tree.beg; F.end = tree.end; F.parent = tree.parent;
+    F.bnd.resize(nn); F.Linv.resize(nn); F.LBP.resize(nn); F.height.assign(nn, 0);
+    std::vector<std::vector<double>> U(nn);   // update matrices, freed when consumed
+    std::vector<int> pos(n, -1);
+    for (int s = 0; s < nn; ++s) {
+        const int b0 = tree.beg[s], e0 = tree.end[s], p = e0 - b0;
+        // ---- symbolic: boundary rows
+        std::vector<int> bnd;
+        for (int j = b0; j < e0; ++j)
+            for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) if (A.col[k] >= e0) bnd.push_back(A.col[k]);
+        for (int c : tree.children[s]) {
+            for (int i : F.bnd[c]) if (i >= e0) bnd.push_back(i);
+            F.height[s] = std::max(F.height[s], F.height[c] + 1);
+        }
+        std::sort(bnd.begin(), bnd.end());
+        bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+        const int nb = (int)bnd.size(), f = p + nb;
+        for (int j = b0; j < e0; ++j) pos[j] = j - b0;
+        for (int k = 0; k < nb; ++k) pos[bnd[k]] = p + k;
+        // ---- assemble front (lower triangle, row-major f x f)
+        std::vector<double> Fr((size_t)f * f, 0.0);
+        for (int j = b0; j < e0; ++j)
+            for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) {
+                int i = A.col[k];
+                if (i < j) continue;
+                Fr[(size_t)pos[i] * f + pos[j]] += A.val[k];
+            }
+        for (int c : tree.children[s]) {
+            const std::vector<int>& cb = F.bnd[c];
+            const int m = (int)cb.size();
+            const std::vector<double>& Uc = U[c];
+            for (int a = 0; a < m; ++a)
+                for (int bb = 0; bb <= a; ++bb) {
+                    int ra = pos[cb[a]], rb = pos[cb[bb]];
+                    if (ra < rb) std::swap(ra, rb);
+                    Fr[(size_t)ra * f + rb] += Uc[(size_t)a * m + bb];
+                }
+            std::vector<double>().swap(U[c]);
+        }
+        // ---- partial dense Cholesky (right-looking) of the first p columns
+        for (int k = 0; k < p; ++k) {
+            double d = Fr[(size_t)k * f + k];
+            if (!(d > 0.0)) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite");
+            d = std::sqrt(d);
+            Fr[(size_t)k * f + k] = d;
+            const double inv = 1.0 / d;
+            for (int i = k + 1; i < f; ++i) Fr[(size_t)i * f + k] *= inv;
+            for (int i = k + 1; i < f; ++i) {
+                const double lik = Fr[(size_t)i * f + k];
+                if (lik == 0.0) continue;
+                double* row = &Fr[(size_t)i * f];
+                const int jmax = i;  // lower triangle incl. diagonal
+                for (int j = k + 1; j <= jmax; ++j) row[j] -= lik * Fr[(size_t)j * f + k];
+            }
+            F.flops += (double)(f - k) * (f - k);
+        }
+        // ---- outputs: Linv (p x p lower), LBP (nb x p), update matrix (nb x nb lower)
+        std::vector<double> Li((size_t)p * p, 0.0);
+        for (int j = 0; j < p; ++j) {  // solve L * col = e_j  (forward substitution)
+            Li[(size_t)j * p + j] = 1.0 / Fr[(size_t)j * f + j];
+            for (int i = j + 1; i < p; ++i) {
+                double s = 0;
+                for (int k = j; k < i; ++k) s += Fr[(size_t)i * f + k] * Li[(size_t)k * p + j];
+                Li[(size_t)i * p + j] = -s / Fr[(size_t)i * f + i];
+            }
+        }
+        F.Linv[s] = std::move(Li);
+        std::vector<double> LBP((size_t)nb * p);
+        for (int a = 0; a < nb; ++a)
+            for (int j = 0; j < p; ++j) LBP[(size_t)a * p + j] = Fr[(size_t)(p + a) * f + j];
+        F.LBP[s] = std::move(LBP);
+        if (nb > 0) {
+            std::vector<double> Us((size_t)nb * nb);
+            for (int a = 0; a < nb; ++a)
+                for (int bb = 0; bb <= a; ++bb) Us[(size_t)a * nb + bb] = Fr[(size_t)(p + a) * f + p + bb];
+            U[s] = std::move(Us);
+        }
+        F.nnz_L += (size_t)p * (p + 1) / 2 + (size_t)p * nb;
+        F.bnd[s] = std::move(bnd);
+        F.max_height = std::max(F.max_height, F.height[s]);
+    }
+    return F;
+}
+
+void factor_solve_host(const SupernodalFactor& F, std::vector<double>& b) {
+    const int nn = F.n_nodes;
+    std::vector<double> t;
+    for (int s = 0; s < nn; ++s) {  // forward (postorder)
+        const int b0 = F.beg[s], p = F.end[s] - b0, nb = (int)F.bnd[s].size();
+        t.assign((size_t)p * 3, 0.0);
+        for (int i = 0; i < p; ++i)
+            for (int k = 0; k <= i; ++k)
+                for (int c = 0; c < 3; ++c) t[3 * i + c] += F.Linv[s][(size_t)i * p + k] * b[3 * (size_t)(b0 + k) + c];
+        for (int i = 0; i < p; ++i) for (int c = 0; c < 3; ++c) b[3 * (size_t)(b0 + i) + c] = t[3 * i + c];
+        for (int a = 0; a < nb; ++a)
+            for (int j = 0; j < p; ++j)
+                for (int c = 0; c < 3; ++c) b[3 * (size_t)F.bnd[s][a] + c] -= F.LBP[s][(size_t)a * p + j] * t[3 * j + c];
+    }
+    for (int s = nn - 1; s >= 0; --s) {  // backward
+        const int b0 = F.beg[s], p = F.end[s] - b0, nb = (int)F.bnd[s].size();
+        t.assign((size_t)p * 3, 0.0);
+        for (int j = 0; j < p; ++j)
+            for (int c = 0; c < 3; ++c) {
+                double v = b[3 * (size_t)(b0 + j) + c];
+                for (int a = 0; a < nb; ++a) v -= F.LBP[s][(size_t)a * p + j] * b[3 * (size_t)F.bnd[s][a] + c];
+                t[3 * j + c] = v;
+            }
+        for (int j = 0; j < p; ++j)
+            for (int c = 0; c < 3; ++c) {
+                double v = 0;
+                for (int i = j; i < p; ++i) v += F.Linv[s][(size_t)i * p + j] * t[3 * i + c];
+                b[3 * (size_t)(b0 + j) + c] = v;
+            }
+    }
+}
+
+}  // namespace aa

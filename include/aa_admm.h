@@ -1,0 +1,115 @@
+/* aa_admm.h -- C ABI of the MI355X-native Anderson-accelerated ADMM hot path.
+ *
+ * This is the drop-in boundary for the reference's admm-elastic plugin API
+ * (bldeng/AA-ADMM, admm_anderson_{xzu,hard_zxu}/src). Plain pointers and sizes only; no
+ * torch or HIP types. Every call returns AA_OK (0) or a negative status; the message of the
+ * last failure on the calling thread is available from aa_last_error(). The reference
+ * throws std::runtime_error / returns bool at the same points -- the C++ facade in
+ * include/aa_admm.hpp re-raises these codes as std::runtime_error.
+ *
+ * Arrays are fp64 (the reference computes in double throughout, Types.h) and int32 indices
+ * (Eigen's default StorageIndex). Node arrays are xyz-interleaved ("scaled x3" as in
+ * Solver::m_x / m_masses, admm_anderson_hard_zxu/src/Solver.hpp:84-87).
+ */
+#ifndef AA_ADMM_H
+#define AA_ADMM_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AA_OK 0
+#define AA_ERR_ARG -1       /* bad input (reference: "Bad input" runtime_error)            */
+#define AA_ERR_STATE -2     /* call order violated (e.g. step before initialize)           */
+#define AA_ERR_DEVICE -3    /* HIP runtime failure                                         */
+#define AA_ERR_NUMERIC -4   /* inverted element, weight <= 0, matrix not SPD              */
+
+typedef struct aa_ctx_s* aa_ctx;          /* one GPU + one HIP stream                    */
+typedef struct aa_elastic_s* aa_elastic;  /* one admm::Solver instance                   */
+
+/* Element materials (binding::MeshFlags, samples/utils/AddMeshes.hpp:45-50). */
+#define AA_LINEAR 0      /* TetEnergyTerm (corotated-linear via 3x3 SVD) / TriEnergyTerm */
+#define AA_NEOHOOKEAN 1  /* NeoHookeanTet (9-D L-BFGS prox)                              */
+#define AA_STVK 2        /* StVKTet       (9-D L-BFGS prox)                              */
+
+/* Solver variants: the two reference solver copies. */
+#define AA_VARIANT_Z 0   /* admm_anderson_xzu: Anderson on z (Solver.cpp:34-263)            */
+#define AA_VARIANT_UX 1  /* admm_anderson_hard_zxu: Anderson on (u,x) (Solver.cpp:34-234)    */
+
+/* Lame (EnergyTerm.hpp:35-61): mu, lambda and strain limits (tris only). */
+typedef struct {
+    double mu, lambda;
+    double limit_min, limit_max;   /* defaults -100 / 100 = no limiting */
+} aa_lame;
+
+/* Solver::Settings (Solver.hpp:45-67) + variant selection. */
+typedef struct {
+    double timestep_s;      /* -dt   default 1/30                                  */
+    int verbose;            /* -v                                                  */
+    int admm_iters;         /* -it   default 500                                   */
+    double gravity;         /* -g    default -9.8 (applied to y of free nodes)     */
+    double constraint_w;    /* -ck   (unused by the LDLT path, kept for parity)    */
+    int anderson_m;         /* -am   window (>0 with acceleration)                 */
+    double penalty;         /* -ap   (UX variant; the Z variant uses 1)            */
+    int acceleration_type;  /* 0 = NOACC, 1 = ANDERSON  (-a)                       */
+    int variant;            /* AA_VARIANT_Z / AA_VARIANT_UX                        */
+} aa_settings;
+
+/* RuntimeData (Solver.hpp:69-80) plus device-side counters. */
+typedef struct {
+    double global_ms, local_ms, acceleration_ms, initialization_ms;  /* host wall, per step */
+    double step_ms;          /* wall time of the last step() (device-synchronised)  */
+    double setup_ms;         /* initialize(): assembly + ordering + factorisation   */
+    int iterations;          /* ADMM iterations recorded in the last step           */
+    int rejects;             /* Anderson rejections in the last step                */
+    long long nnz_factor;    /* scalar nnz(L) of the global factor                  */
+    int n_free, n_pinned, n_elements, z_dim;
+} aa_runtime;
+
+const char* aa_last_error(void);
+const char* aa_version(void);
+
+/* ---- context --------------------------------------------------------------------- */
+int aa_ctx_create(int device_id, aa_ctx* out);
+int aa_ctx_destroy(aa_ctx ctx);
+int aa_ctx_synchronize(aa_ctx ctx);
+
+/* ---- admm::Solver ------------------------------------------------------------------ */
+int aa_lame_from_young(double youngs, double poisson, aa_lame* out);    /* Lame(k, v)        */
+int aa_settings_default(aa_settings* out);                               /* Settings()        */
+
+int aa_elastic_create(aa_ctx ctx, aa_elastic* out);                      /* Solver()          */
+int aa_elastic_destroy(aa_elastic h);
+/* Solver::add_nodes(x, m, n): x and m are "scaled x3"; returns the node count in *total. */
+int aa_elastic_add_nodes(aa_elastic h, const double* x3, const double* m3, int n_verts, int* total);
+/* create_tets_from_mesh<IN_SCALAR,TYPE>(energyterms, verts, inds, n, lame, vertex_offset)
+ * (TetEnergyTerm.hpp:36-51): rest shape from verts3[inds], node ids inds + vertex_offset. */
+int aa_elastic_add_tets(aa_elastic h, const double* verts3, const int* tets4, int n_tets, int material,
+                        const aa_lame* lame, int vertex_offset);
+/* create_tris_from_mesh<IN_SCALAR,TriEnergyTerm> (TriEnergyTerm.hpp:33-47). */
+int aa_elastic_add_tris(aa_elastic h, const double* verts3, const int* tris3, int n_tris, const aa_lame* lame,
+                        int vertex_offset);
+/* Solver::set_pins(inds, points): points3 == NULL pins in place (Solver.cpp:280-315). */
+int aa_elastic_set_pins(aa_elastic h, const int* inds, const double* points3, int n_pins);
+int aa_elastic_initialize(aa_elastic h, const aa_settings* settings);    /* Solver::initialize */
+int aa_elastic_step(aa_elastic h);                                       /* Solver::step       */
+int aa_elastic_num_nodes(aa_elastic h, int* n);
+int aa_elastic_get_x(aa_elastic h, double* x3);                          /* Solver::m_x        */
+int aa_elastic_get_v(aa_elastic h, double* v3);                          /* Solver::m_v        */
+int aa_elastic_set_v(aa_elastic h, const double* v3);
+/* Per-iteration (prim, comb, reject) of the last step -- the rows Solver::save() writes
+ * (Solver.hpp:130-155). Returns the count in *n (<= cap copied). */
+int aa_elastic_get_history(aa_elastic h, double* prim, double* comb, int* reject, int cap, int* n);
+int aa_elastic_runtime(aa_elastic h, aa_runtime* out);                   /* runtime_data()    */
+
+/* ---- benchmarking hooks (device-resident inputs, no host traffic) ------------------ */
+/* Enqueue `iters` iterations of the ADMM loop of the current time step without the
+ * per-step prologue/epilogue; used by bench.py to time the hot loop alone. */
+int aa_elastic_bench_iterations(aa_elastic h, int iters, double* ms);
+/* Average device time (ms) per launch of the named kernel class over the last bench call,
+ * measured with HIP events on the solver's stream; and its algorithmic bytes per launch. */
+int aa_elastic_kernel_stats(aa_elastic h, const char* name, double* avg_ms, double* bytes, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AA_ADMM_H */

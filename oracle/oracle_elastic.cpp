@@ -241,8 +241,38 @@ struct Elastic {
         np = (int)pins.size();
         nf = n - np;
         node2int.assign(n, -1);
+        // free nodes in reverse Cuthill-McKee order (keeps the envelope factor small); pinned last
+        std::vector<std::vector<int>> adj(n);
+        for (int g = 0; g < n_groups; ++g) {
+            const int nv = g_kind[g] == 0 ? 4 : 3;
+            for (int t = 0; t < g_count[g]; ++t) {
+                const int* id = idx + g_off[g] + (size_t)t * nv;
+                for (int a = 0; a < nv; ++a)
+                    for (int b = 0; b < nv; ++b)
+                        if (a != b) adj[id[a]].push_back(id[b]);
+            }
+        }
+        for (auto& l : adj) { std::sort(l.begin(), l.end()); l.erase(std::unique(l.begin(), l.end()), l.end()); }
+        std::vector<int> order, seen(n, 0);
+        for (int i = 0; i < n; ++i) if (pins.count(i)) seen[i] = 1;
+        for (;;) {
+            int start = -1;
+            for (int i = 0; i < n; ++i)
+                if (!seen[i] && (start < 0 || adj[i].size() < adj[start].size())) start = i;
+            if (start < 0) break;
+            size_t head = order.size();
+            order.push_back(start); seen[start] = 1;
+            while (head < order.size()) {
+                int v0 = order[head++];
+                std::vector<int> nb;
+                for (int u : adj[v0]) if (!seen[u]) { seen[u] = 1; nb.push_back(u); }
+                std::sort(nb.begin(), nb.end(), [&](int a, int b) { return adj[a].size() < adj[b].size() || (adj[a].size() == adj[b].size() && a < b); });
+                order.insert(order.end(), nb.begin(), nb.end());
+            }
+        }
+        std::reverse(order.begin(), order.end());
         int c = 0;
-        for (int i = 0; i < n; ++i) if (!pins.count(i)) { node2int[i] = c++; int2node.push_back(i); }
+        for (int i : order) { node2int[i] = c++; int2node.push_back(i); }
         for (auto& kv : pins) { node2int[kv.first] = c++; int2node.push_back(kv.first); }
         Z = 0;
         for (int g = 0; g < n_groups; ++g) {

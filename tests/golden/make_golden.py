@@ -1,0 +1,139 @@
+"""Generates the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+The reference (bldeng/AA-ADMM) is compiled from its own sources under /root/reference by
+oracle/Makefile (`make -C oracle ref`) into oracle/_ref/ -- headless drivers replace the GUI
+sample loops (oracle/ref_drivers/*.cpp). This script feeds them the scenes below and stores
+inputs + outputs as .npz (data only, no code). Run in the build container:
+
+    make -C oracle ref && python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import struct
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+scenes = importlib.import_module("aa-admm_amd.scenes")
+from golden_io import save_case  # noqa: E402
+
+REF = os.path.join(REPO, "oracle", "_ref")
+
+
+def cases():
+    S = scenes
+    return {
+        "cloth12_ux_aa6": S.cloth(12, 12, iters=40, n_steps=3),
+        "cloth12_ux_noaa": S.cloth(12, 12, iters=40, n_steps=2, accel=0),
+        "cloth12_z_noaa": S.cloth(12, 12, iters=30, n_steps=2, accel=0, variant=S.VARIANT_X),
+        "cantilever_z_nh_aa6": S.cantilever(20, 4, 5, S.NEOHOOKEAN, iters=50, n_steps=1),   # BASELINE configs[0]
+        "cant8_z_lin_aa6": S.cantilever(8, 2, 2, S.LINEAR, iters=30, n_steps=2),
+        "cant8_ux_lin_aa6": S.cantilever(8, 2, 2, S.LINEAR, iters=30, n_steps=2, variant=S.VARIANT_H),
+        "cant8_z_stvk_noaa": S.cantilever(8, 2, 2, S.STVK, iters=30, n_steps=2, accel=0),
+        "beams2_z_aa6": S.beams(2, iters=40, n_steps=2),
+        "beams2_ux_aa6": S.beams(2, iters=40, n_steps=2, variant=S.VARIANT_H),
+        "cloth12_ux_aa1": S.cloth(12, 12, iters=30, n_steps=2, aa_m=1),
+        "cant8_ux_lin_aa3_pen": _with(S.cantilever(8, 2, 2, S.LINEAR, iters=30, n_steps=1, variant=S.VARIANT_H, aa_m=3),
+                                      penalty=4.0),
+    }
+
+
+def _with(scene, **kw):
+    for k, v in kw.items():
+        setattr(scene, k, v)
+    return scene
+
+
+def run_ref(scene, tmp):
+    path_in = os.path.join(tmp, "scene.bin")
+    path_out = os.path.join(tmp, "out.bin")
+    scenes.write_scene(scene, path_in)
+    drv = os.path.join(REF, "ref_elastic_h" if scene.variant == scenes.VARIANT_H else "ref_elastic_x")
+    r = subprocess.run([drv, path_in, path_out], cwd=tmp, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr)
+    return scenes.read_ref_result(path_out, scene.n_nodes)
+
+
+def element_tables(tmp):
+    rng = np.random.default_rng(20191015)
+    out = {}
+    # tets: F = I + 0.3 N, some inverted (flip a column), some near-singular
+    n = 64
+    F = np.eye(3)[None] + 0.3 * rng.standard_normal((n, 3, 3))
+    F[::5, :, 0] *= -1.0                 # inverted
+    F[3::7, :, 2] = F[3::7, :, 1] * 0.5  # rank-deficient
+    Fv = np.transpose(F, (0, 2, 1)).reshape(n, 9)  # column-major vec(F)
+    for op, name, prm in [(0, "tet_linear", (1e7, 0.399, 1.0, 0.0)), (1, "tet_nh", (1e7, 0.399, 0.1, 0.0)),
+                          (2, "tet_stvk", (1e7, 0.399, 0.1, 0.0))]:
+        X = Fv if op == 0 else Fv[1::5].copy()   # hyperelastic: skip inverted inputs (log J of J < 0)
+        if op != 0:
+            X = np.concatenate([np.eye(3).reshape(1, 9) + 0.2 * rng.standard_normal((24, 9))])
+            X = X[np.linalg.det(X.reshape(-1, 3, 3)) > 0.2]
+        buf = struct.pack("<ii", op, len(X)) + b"".join(struct.pack("<4d", *prm) + x.astype("<f8").tobytes() for x in X)
+        out[name] = (X, prm, _run_elem(buf, tmp, 9, len(X)))
+    # tris (H prox) with and without strain limits
+    T = np.concatenate([np.eye(3)[:, :2].T.reshape(1, 6).repeat(32, 0)]) + 0.3 * rng.standard_normal((32, 6))
+    for name, prm in [("tri_h_limits", (50.0, 0.1, 0.95, 1.05)), ("tri_h_free", (50.0, 0.1, -100.0, 100.0))]:
+        buf = struct.pack("<ii", 3, len(T)) + b"".join(struct.pack("<4d", *prm) + t.astype("<f8").tobytes() for t in T)
+        out[name] = (T, prm, _run_elem(buf, tmp, 6, len(T)))
+    # COD solves: SPD, near-singular and rank-deficient normal-equation matrices
+    mats = []
+    for k in (1, 2, 3, 6, 10):
+        for kind in range(3):
+            A = rng.standard_normal((40, k))
+            if kind == 1 and k > 1:
+                A[:, -1] = A[:, 0] + 1e-9 * rng.standard_normal(40)
+            if kind == 2 and k > 2:
+                A[:, 1] = A[:, 0]
+            A /= np.linalg.norm(A, axis=0)
+            M = A.T @ A
+            b = A.T @ rng.standard_normal(40)
+            mats.append((k, M, b))
+    res = []
+    for k, M, b in mats:
+        buf = struct.pack("<ii", 4, 1) + struct.pack("<4d", k, 0, 0, 0) + M.astype("<f8").ravel(order="F").tobytes() + b.astype("<f8").tobytes()
+        res.append(_run_elem(buf, tmp, k, 1)[0])
+    out["cod"] = mats, res
+    return out
+
+
+def _run_elem(buf, tmp, width, count):
+    pin = os.path.join(tmp, "elem.bin")
+    pout = os.path.join(tmp, "elem.out")
+    with open(pin, "wb") as f:
+        f.write(buf)
+    r = subprocess.run([os.path.join(REF, "ref_element"), pin, pout], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr)
+    return np.fromfile(pout, dtype="<f8").reshape(count, width)
+
+
+def main():
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, sc in cases().items():
+            steps = run_ref(sc, tmp)
+            save_case(os.path.join(HERE, name + ".npz"), sc, steps)
+            print(name, [len(s["prim"]) for s in steps])
+        et = element_tables(tmp)
+        arrays = {}
+        for name in ("tet_linear", "tet_nh", "tet_stvk", "tri_h_limits", "tri_h_free"):
+            X, prm, Y = et[name]
+            arrays[name + "_in"], arrays[name + "_prm"], arrays[name + "_out"] = X, np.array(prm), Y
+        mats, res = et["cod"]
+        for i, ((k, M, b), th) in enumerate(zip(mats, res)):
+            arrays[f"cod{i}_M"], arrays[f"cod{i}_b"], arrays[f"cod{i}_theta"] = M, b, th
+        np.savez_compressed(os.path.join(HERE, "elements.npz"), **arrays)
+        print("elements", sorted(k for k in arrays if k.endswith("_out")))
+
+
+if __name__ == "__main__":
+    main()
