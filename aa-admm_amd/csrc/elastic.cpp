@@ -368,12 +368,13 @@ void ElasticSolver::ev_end(const char* name) { ev_begin(name); }
 
 void ElasticSolver::local_z_all(const double* xfull, const double* u, double* z, double* y, int mode, bool red) {
     int off = 0;
-    ev_begin("local_z");
+    const bool timed = mode == LZ_NORMAL && red;
+    if (timed) ev_begin("local_z");
     for (auto& g : groups_) {
         launch_local_z(g.d, xfull, u, z, y, nf_, st_.variant, mode, ctrl_.p, red ? red_a_.p : nullptr, off, s());
         off += blocks_for(g.d.count);
     }
-    ev_end("local_z");
+    if (timed) ev_end("local_z");
 }
 
 void ElasticSolver::prologue() {
@@ -534,7 +535,7 @@ void ElasticSolver::fetch_results() {
         AA_HIP(hipMemcpy(h_comb_.data(), hist_comb_.p, nrec_ * 8, hipMemcpyDeviceToHost));
         AA_HIP(hipMemcpy(h_rej_.data(), hist_rej_.p, nrec_ * 4, hipMemcpyDeviceToHost));
     }
-    rt_.iterations = c.nrec;
+    rt_.iterations = c.iters_run;
     rt_.rejects = c.nrej;
     if (c.fail == 1) throw Error(ERR_NUMERIC, "the line search step became smaller than the minimum value allowed");
     if (c.fail == 2) throw Error(ERR_NUMERIC, "**TriEnergyTerm TODO: gradient function");

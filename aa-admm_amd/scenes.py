@@ -249,4 +249,7 @@ def read_ref_result(path: str, n_nodes: int):
         nrec = int(take("<i4", 1)[0])
         steps.append(dict(prim=take("<f8", nrec), comb=take("<f8", nrec), reject=take("<i4", nrec),
                           x=take("<f8", 3 * n_nodes).reshape(-1, 3), v=take("<f8", 3 * n_nodes).reshape(-1, 3)))
+    if off + 8 * n_steps <= len(data):
+        for s, t in zip(steps, take("<f8", n_steps)):
+            s["step_ms"] = float(t)
     return steps

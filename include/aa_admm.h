@@ -59,7 +59,8 @@ typedef struct {
     double global_ms, local_ms, acceleration_ms, initialization_ms;  /* host wall, per step */
     double step_ms;          /* wall time of the last step() (device-synchronised)  */
     double setup_ms;         /* initialize(): assembly + ordering + factorisation   */
-    int iterations;          /* ADMM iterations recorded in the last step           */
+    int iterations;          /* ADMM iterations executed in the last step (incl. a  
+                                breaking one; history() holds the recorded rows)     */
     int rejects;             /* Anderson rejections in the last step                */
     long long nnz_factor;    /* scalar nnz(L) of the global factor                  */
     int n_free, n_pinned, n_elements, z_dim;

@@ -11,12 +11,14 @@
 //     (TetEnergyTerm.hpp:36-51, TriEnergyTerm.hpp:33-47), set_pins (Solver.cpp:280-315),
 //     initialize (Solver.cpp:361-491), step() x n_steps (Solver.cpp:34-234)
 //   -> result file: per time step the per-iteration (prim, comb, reject) rows that
-//      Solver::save() writes (Solver.hpp:130-155) plus the node positions/velocities.
+//      Solver::save() writes (Solver.hpp:130-155) plus the node positions/velocities,
+//      then a trailer with the wall-clock ms of each step() (initialize excluded).
 //
 // Build with -DREF_VARIANT_H for admm_anderson_hard_zxu, without it for admm_anderson_xzu.
 #include "Solver.hpp"
 #include "TetEnergyTerm.hpp"
 #include "TriEnergyTerm.hpp"
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -127,9 +129,12 @@ int main(int argc, char** argv) {
     const std::string res = accel ? "result/residual-" + std::to_string(aa_m) + ".txt" : "result/residual-no.txt";
     FILE* out = fopen(argv[2], "wb");
     fwrite(&n_steps, sizeof(int), 1, out);
+    std::vector<double> step_ms;
     for (int k = 1; k <= n_steps; ++k) {
         solver.set_pins(pin_idx, pins_at(k));
+        auto t0 = std::chrono::steady_clock::now();
         solver.step();
+        step_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         std::vector<double> prim, comb;
         std::vector<int> rej;
         std::ifstream in(res);
@@ -151,6 +156,7 @@ int main(int argc, char** argv) {
         fwrite(solver.m_x.data(), sizeof(double), 3 * (size_t)n, out);
         fwrite(solver.m_v.data(), sizeof(double), 3 * (size_t)n, out);
     }
+    fwrite(step_ms.data(), sizeof(double), step_ms.size(), out);   // trailer: wall ms of each step()
     fclose(out);
     return 0;
 }

@@ -43,22 +43,18 @@ def test_gpu_matches_oracle(builder, tol, pkg, ctx, oracle):
 
 
 def test_gpu_full_size_cloth_c2(pkg, ctx, oracle):
-    """BASELINE configs[1] at full size (50 176 tris): direct comparison with the oracle over
-    the first 20 iterations, plus size-independent properties over the whole step."""
+    """BASELINE configs[1] at full size (50 176 tris, 100 ADMM iterations): the whole residual
+    curve against the oracle (judged relative to comb_0) plus size-independent properties."""
     sc = scenes.cloth(112, 112, iters=100, n_steps=1)
     got, solver = pkg.capi.run_scene(ctx, sc)
     h = got[0]
     rt = solver.runtime()
     assert rt.n_elements == 50176 and rt.n_free == 25311 and rt.n_pinned == 2
     assert np.all(np.isfinite(h["comb"])) and np.all(np.isfinite(got[0]["x"]))
-    # pinned corners stay exactly at their targets
-    assert np.array_equal(got[0]["x"][sc.pin_idx], sc.pin_pts)
-    # ADMM+AA drives the combined residual down by orders of magnitude within the step
-    assert h["comb"][-1] < 1e-4 * h["comb"][0]
-    short = scenes.cloth(112, 112, iters=20, n_steps=1)
-    want = oracle.run_elastic(short)
-    fails = compare(want, [dict(prim=h["prim"][:20], comb=h["comb"][:20], reject=h["reject"][:20], x=want[0]["x"])],
-                    1e-9, 1.0)
+    assert np.array_equal(got[0]["x"][sc.pin_idx], sc.pin_pts)      # pins exactly at their targets
+    want = oracle.run_elastic(sc)
+    want[-1]["x"] = want[-1]["x"].reshape(-1, 3)
+    fails = compare(want, got, 1e-9, 1e-9)
     assert not fails, fails
 
 
