@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <set>
@@ -20,8 +21,16 @@
 namespace aa {
 
 ElasticSolver::~ElasticSolver() {
+    drop_graph();
     for (auto& kv : kstats_)
         for (auto e : kv.second.ev) (void)hipEventDestroy(e);
+}
+
+void ElasticSolver::drop_graph() {
+    if (gexec_) (void)hipGraphExecDestroy(gexec_);
+    if (graph_) (void)hipGraphDestroy(graph_);
+    gexec_ = nullptr;
+    graph_ = nullptr;
 }
 
 int ElasticSolver::add_nodes(const double* x3, const double* m3, int n) {
@@ -136,6 +145,8 @@ void ElasticSolver::set_pins(const int* inds, const double* pts3, int n) {
 
 void ElasticSolver::initialize(const aa_settings& s_in) {
     auto t0 = std::chrono::steady_clock::now();
+    drop_graph();
+    if (const char* g = std::getenv("AA_ADMM_NO_GRAPH")) use_graph_ = !(g[0] == '1');
     st_ = s_in;
     if (st_.timestep_s <= 0.0) st_.timestep_s = 1.0 / 24.0;  // Solver.cpp:369-373
     const int n = num_nodes();
@@ -184,7 +195,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     std::vector<double> coords(3 * (size_t)nf_);
     for (int k = 0; k < nf_; ++k)
         for (int j = 0; j < 3; ++j) coords[3 * k + j] = x_[3 * (size_t)free_nodes[k] + j];
-    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32);
+    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32, DirectSolver::kTopRows);
     node2int_.assign(n, -1);
     int2node_.assign(n, -1);
     for (int q = 0; q < nf_; ++q) { node2int_[free_nodes[tree.perm[q]]] = q; int2node_[q] = free_nodes[tree.perm[q]]; }
@@ -427,16 +438,12 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
     local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_NORMAL, true);
     launch_control(CTL_PRIM_CHECK, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     if (accel) {
-        launch_copy(u_.p, du_.p, Z_, c, 1, s());
-        launch_copy(xfull_.p, dx_.p, nx, c, 1, s());
-        launch_copy(aa_cur_.p, du_.p, Z_, c, 1, s());
-        launch_copy(aa_cur_.p + Z_, dx_.p, nx, c, 1, s());
+        launch_restore_ux(u_.p, xfull_.p, aa_cur_.p, du_.p, dx_.p, Z_, nx, c, s());
         local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_REDO, true);
     }
     launch_control(CTL_PRIM_FINAL, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
-    launch_copy(xlast_.p, xfull_.p, nx, c, 0, s());
     ev_begin("rhs");
-    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s(), xfull_.p, xlast_.p);
     ev_end("rhs");
     ev_begin("solve");
     solver_.solve(b_.p, xfull_.p, c, 0, s());
@@ -546,9 +553,22 @@ void ElasticSolver::step() {
     auto t0 = std::chrono::steady_clock::now();
     const bool accel = st_.acceleration_type == 1;
     prologue();
-    for (int it = 0; it < st_.admm_iters; ++it) {
-        if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
-        else enqueue_iteration_z(accel);
+    if (use_graph_ && st_.admm_iters > 0) {
+        if (!gexec_) {   // pointers and control flow are fixed after initialize: capture once
+            AA_HIP(hipStreamBeginCapture(s(), hipStreamCaptureModeThreadLocal));
+            for (int it = 0; it < st_.admm_iters; ++it) {
+                if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
+                else enqueue_iteration_z(accel);
+            }
+            AA_HIP(hipStreamEndCapture(s(), &graph_));
+            AA_HIP(hipGraphInstantiate(&gexec_, graph_, nullptr, nullptr, 0));
+        }
+        AA_HIP(hipGraphLaunch(gexec_, s()));
+    } else {
+        for (int it = 0; it < st_.admm_iters; ++it) {
+            if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
+            else enqueue_iteration_z(accel);
+        }
     }
     epilogue_enqueue(accel);
     fetch_results();

@@ -92,6 +92,12 @@ private:
     aa_runtime rt_{};
     bool pins_dirty_ = true;
 
+    // the whole ADMM loop of a time step, captured once into a hipGraph and replayed per step
+    hipGraph_t graph_ = nullptr;
+    hipGraphExec_t gexec_ = nullptr;
+    bool use_graph_ = true;
+    void drop_graph();
+
     // kernel-class event timing (bench only)
     bool instrument_ = false;
     struct KStat { std::vector<hipEvent_t> ev; double bytes = 0; double total_ms = 0; int launches = 0; };

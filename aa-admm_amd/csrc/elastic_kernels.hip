@@ -250,10 +250,16 @@ __global__ __launch_bounds__(kBlock) void k_init_z(GroupDev g, const double* __r
 __global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ ptr, const int* __restrict__ row,
                                                 const double* __restrict__ val, const double* __restrict__ y,
                                                 const double* __restrict__ Mxbar, double pdt2, double* __restrict__ b,
-                                                const Ctrl* ctrl, int gate_reject) {
+                                                const Ctrl* ctrl, int gate_reject, const double* __restrict__ xsrc,
+                                                double* __restrict__ xlast) {
     if (gated(ctrl, gate_reject)) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nf) return;
+    if (xlast) {   // last_x = curr_x (Solver.cpp:170), fused here: it must follow the reject restore
+        xlast[3 * (size_t)i] = xsrc[3 * (size_t)i];
+        xlast[3 * (size_t)i + 1] = xsrc[3 * (size_t)i + 1];
+        xlast[3 * (size_t)i + 2] = xsrc[3 * (size_t)i + 2];
+    }
     double s0 = 0, s1 = 0, s2 = 0;
     for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
         const double v = val[k];
@@ -321,6 +327,18 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ dst, const
     if (gated(ctrl, gate_reject)) return;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
         dst[i] = src[i];
+}
+
+// UX reject (Solver.cpp:150-154): (u, x) = defaults and accelerator->reset(u, x) stores them
+__global__ __launch_bounds__(kBlock) void k_restore_ux(double* __restrict__ u, double* __restrict__ x,
+                                                       double* __restrict__ cur, const double* __restrict__ du,
+                                                       const double* __restrict__ dx, long long nz, long long nx,
+                                                       const Ctrl* ctrl) {
+    if (gated(ctrl, 1)) return;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nz + nx; i += (long long)gridDim.x * blockDim.x) {
+        if (i < nz) { const double v = du[i]; u[i] = v; if (cur) cur[i] = v; }
+        else { const double v = dx[i - nz]; x[i - nz] = v; if (cur) cur[i] = v; }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_predict(int nf, double* __restrict__ xs, double* __restrict__ vs,
@@ -410,124 +428,147 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
     }
 }
 
-// Eigen CompleteOrthogonalDecomposition::solve of the small normal equations (one thread).
-// Column-pivoted Householder QR with LAPACK norm downdating, rank = #|R_ii| > eps*n*maxpivot,
-// RZ step for the rank-deficient case, minimum-norm solution.
-__device__ void cod_solve_dev(int n, double* A /* n*n col-major, destroyed */, const double* b, double* x) {
-    double hc[kMaxM], nu[kMaxM], nd[kMaxM], zc[kMaxM], c[kMaxM], yv[kMaxM];
-    int perm[kMaxM], tr[kMaxM];
-#define QR(r, cc) A[(cc) * n + (r)]
-    for (int k = 0; k < n; ++k) {
+// Eigen CompleteOrthogonalDecomposition::solve of the small normal equations, block-cooperative:
+// column-pivoted Householder QR with LAPACK norm downdating (Eigen/src/QR/ColPivHouseholderQR.h
+// :482-579), rank = #|R_ii| > eps*n*|maxpivot| (:255-263), RZ step + minimum-norm solve
+// (Eigen/src/QR/CompleteOrthogonalDecomposition.h:410-525). All state lives in LDS; each column
+// update / norm downdate runs on its own thread with the same operation order as the serial
+// algorithm, so the result is the serial result bit for bit.
+struct CodLds {
+    double A[kMaxM * kMaxM];   // column-major n x n
+    double hc[kMaxM], nu[kMaxM], nd[kMaxM], zc[kMaxM], c[kMaxM], y[kMaxM];
+    double bc[4];              // beta, tau, c0 broadcast
+    int tr[kMaxM], perm[kMaxM], big, rank;
+};
+
+__device__ void cod_solve_block(int n, CodLds& S, const double* b, double* x) {
+    const int t = threadIdx.x;
+#define QR(r, cc) S.A[(cc) * n + (r)]
+    if (t < n) {
         double s = 0;
-        for (int r = 0; r < n; ++r) s += QR(r, k) * QR(r, k);
-        nd[k] = nu[k] = sqrt(s);
+        for (int r = 0; r < n; ++r) s += QR(r, t) * QR(r, t);
+        S.nd[t] = S.nu[t] = sqrt(s);
     }
+    __syncthreads();
     const double ddt = sqrt(2.220446049250313e-16);
-    double maxpivot = 0;
+    double maxpivot = 0;   // tracked by thread 0
     for (int k = 0; k < n; ++k) {
-        int big = k;
-        for (int j = k + 1; j < n; ++j) if (nu[j] > nu[big]) big = j;
-        tr[k] = big;
-        if (big != k) {
-            for (int r = 0; r < n; ++r) { double t = QR(r, k); QR(r, k) = QR(r, big); QR(r, big) = t; }
-            double t = nu[k]; nu[k] = nu[big]; nu[big] = t;
-            t = nd[k]; nd[k] = nd[big]; nd[big] = t;
-        }
-        const double c0 = QR(k, k);
-        double tail = 0;
-        for (int r = k + 1; r < n; ++r) tail += QR(r, k) * QR(r, k);
-        double beta, tau;
-        if (tail <= 2.2250738585072014e-308) { tau = 0; beta = c0; for (int r = k + 1; r < n; ++r) QR(r, k) = 0; }
-        else {
-            beta = sqrt(c0 * c0 + tail);
-            if (c0 >= 0) beta = -beta;
-            for (int r = k + 1; r < n; ++r) QR(r, k) /= (c0 - beta);
-            tau = (beta - c0) / beta;
-        }
-        hc[k] = tau;
-        QR(k, k) = beta;
-        maxpivot = fmax(maxpivot, fabs(beta));
-        if (tau != 0)
-            for (int cc = k + 1; cc < n; ++cc) {
-                double t = QR(k, cc);
-                for (int r = k + 1; r < n; ++r) t += QR(r, k) * QR(r, cc);
-                QR(k, cc) -= tau * t;
-                for (int r = k + 1; r < n; ++r) QR(r, cc) -= tau * QR(r, k) * t;
-            }
-        for (int j = k + 1; j < n; ++j) {
-            if (nu[j] != 0) {
-                double t = fabs(QR(k, j)) / nu[j];
-                t = (1.0 + t) * (1.0 - t);
-                t = t < 0 ? 0 : t;
-                const double r2 = nu[j] / nd[j];
-                if (t * r2 * r2 <= ddt) {
-                    double s = 0;
-                    for (int r = k + 1; r < n; ++r) s += QR(r, j) * QR(r, j);
-                    nd[j] = nu[j] = sqrt(s);
-                } else nu[j] *= sqrt(t);
+        if (t == 0) {
+            int big = k;
+            for (int j = k + 1; j < n; ++j) if (S.nu[j] > S.nu[big]) big = j;
+            S.tr[k] = big;
+            S.big = big;
+            if (big != k) {
+                double tt = S.nu[k]; S.nu[k] = S.nu[big]; S.nu[big] = tt;
+                tt = S.nd[k]; S.nd[k] = S.nd[big]; S.nd[big] = tt;
             }
         }
-    }
-    for (int i = 0; i < n; ++i) perm[i] = i;
-    for (int k = 0; k < n; ++k) { int t = perm[k]; perm[k] = perm[tr[k]]; perm[tr[k]] = t; }
-    const double thr = fabs(maxpivot) * 2.220446049250313e-16 * n;
-    int rank = 0;
-    for (int i = 0; i < n; ++i) rank += fabs(QR(i, i)) > thr;
-    for (int i = 0; i < n; ++i) zc[i] = 0;
-    if (rank == 0) { for (int i = 0; i < n; ++i) x[i] = 0; return; }
-    if (rank < n) {
-        for (int k = rank - 1; k >= 0; --k) {
-            if (k != rank - 1) for (int r = 0; r <= k; ++r) { double t = QR(r, k); QR(r, k) = QR(r, rank - 1); QR(r, rank - 1) = t; }
-            const double c0 = QR(k, rank - 1);
+        __syncthreads();
+        const int big = S.big;
+        if (big != k && t < n) { const double tt = QR(t, k); QR(t, k) = QR(t, big); QR(t, big) = tt; }
+        __syncthreads();
+        if (t == 0) {
+            const double c0 = QR(k, k);
             double tail = 0;
-            for (int cc = rank; cc < n; ++cc) tail += QR(k, cc) * QR(k, cc);
+            for (int r = k + 1; r < n; ++r) tail += QR(r, k) * QR(r, k);
             double beta, tau;
-            if (tail <= 2.2250738585072014e-308) { tau = 0; beta = c0; for (int cc = rank; cc < n; ++cc) QR(k, cc) = 0; }
-            else {
-                beta = sqrt(c0 * c0 + tail);
-                if (c0 >= 0) beta = -beta;
-                for (int cc = rank; cc < n; ++cc) QR(k, cc) /= (c0 - beta);
-                tau = (beta - c0) / beta;
-            }
-            zc[k] = tau;
-            QR(k, rank - 1) = beta;
-            if (k > 0 && tau != 0)
-                for (int r = 0; r < k; ++r) {
-                    double t = QR(r, rank - 1);
-                    for (int cc = rank; cc < n; ++cc) t += QR(r, cc) * QR(k, cc);
-                    QR(r, rank - 1) -= tau * t;
-                    for (int cc = rank; cc < n; ++cc) QR(r, cc) -= tau * t * QR(k, cc);
+            if (tail <= 2.2250738585072014e-308) { tau = 0; beta = c0; }
+            else { beta = sqrt(c0 * c0 + tail); if (c0 >= 0) beta = -beta; tau = (beta - c0) / beta; }
+            S.bc[0] = beta; S.bc[1] = tau; S.bc[2] = c0; S.bc[3] = tail;
+            maxpivot = fmax(maxpivot, fabs(beta));
+        }
+        __syncthreads();
+        const double beta = S.bc[0], tau = S.bc[1], c0 = S.bc[2];
+        const bool zero_tail = S.bc[3] <= 2.2250738585072014e-308;
+        if (t > k && t < n) QR(t, k) = zero_tail ? 0.0 : QR(t, k) / (c0 - beta);
+        __syncthreads();
+        if (t == 0) { S.hc[k] = tau; QR(k, k) = beta; }
+        if (tau != 0 && t > k && t < n) {   // apply H_k to column t
+            double tt = QR(k, t);
+            for (int r = k + 1; r < n; ++r) tt += QR(r, k) * QR(r, t);
+            QR(k, t) -= tau * tt;
+            for (int r = k + 1; r < n; ++r) QR(r, t) -= tau * QR(r, k) * tt;
+        }
+        __syncthreads();
+        if (t > k && t < n && S.nu[t] != 0) {   // norm downdate of column t
+            double tt = fabs(QR(k, t)) / S.nu[t];
+            tt = (1.0 + tt) * (1.0 - tt);
+            tt = tt < 0 ? 0 : tt;
+            const double r2 = S.nu[t] / S.nd[t];
+            if (tt * r2 * r2 <= ddt) {
+                double s = 0;
+                for (int r = k + 1; r < n; ++r) s += QR(r, t) * QR(r, t);
+                S.nd[t] = S.nu[t] = sqrt(s);
+            } else S.nu[t] *= sqrt(tt);
+        }
+        __syncthreads();
+    }
+    if (t == 0) {   // rank, RZ (rank-deficient only), Q^T b, triangular solve, Z^T, permutation
+        for (int i = 0; i < n; ++i) S.perm[i] = i;
+        for (int k = 0; k < n; ++k) { const int tt = S.perm[k]; S.perm[k] = S.perm[S.tr[k]]; S.perm[S.tr[k]] = tt; }
+        const double thr = fabs(maxpivot) * 2.220446049250313e-16 * n;
+        int rank = 0;
+        for (int i = 0; i < n; ++i) rank += fabs(QR(i, i)) > thr;
+        for (int i = 0; i < n; ++i) S.zc[i] = 0;
+        if (rank == 0) {
+            for (int i = 0; i < n; ++i) x[i] = 0;
+        } else {
+            if (rank < n) {
+                for (int k = rank - 1; k >= 0; --k) {
+                    if (k != rank - 1) for (int r = 0; r <= k; ++r) { const double tt = QR(r, k); QR(r, k) = QR(r, rank - 1); QR(r, rank - 1) = tt; }
+                    const double c0 = QR(k, rank - 1);
+                    double tail = 0;
+                    for (int cc = rank; cc < n; ++cc) tail += QR(k, cc) * QR(k, cc);
+                    double beta, tau;
+                    if (tail <= 2.2250738585072014e-308) { tau = 0; beta = c0; for (int cc = rank; cc < n; ++cc) QR(k, cc) = 0; }
+                    else {
+                        beta = sqrt(c0 * c0 + tail);
+                        if (c0 >= 0) beta = -beta;
+                        for (int cc = rank; cc < n; ++cc) QR(k, cc) /= (c0 - beta);
+                        tau = (beta - c0) / beta;
+                    }
+                    S.zc[k] = tau;
+                    QR(k, rank - 1) = beta;
+                    if (k > 0 && tau != 0)
+                        for (int r = 0; r < k; ++r) {
+                            double tt = QR(r, rank - 1);
+                            for (int cc = rank; cc < n; ++cc) tt += QR(r, cc) * QR(k, cc);
+                            QR(r, rank - 1) -= tau * tt;
+                            for (int cc = rank; cc < n; ++cc) QR(r, cc) -= tau * tt * QR(k, cc);
+                        }
+                    if (k != rank - 1) for (int r = 0; r <= k; ++r) { const double tt = QR(r, k); QR(r, k) = QR(r, rank - 1); QR(r, rank - 1) = tt; }
                 }
-            if (k != rank - 1) for (int r = 0; r <= k; ++r) { double t = QR(r, k); QR(r, k) = QR(r, rank - 1); QR(r, rank - 1) = t; }
-        }
-    }
-    for (int i = 0; i < n; ++i) c[i] = b[i];
-    for (int k = 0; k < rank; ++k) {
-        if (hc[k] == 0) continue;
-        double t = c[k];
-        for (int r = k + 1; r < n; ++r) t += QR(r, k) * c[r];
-        c[k] -= hc[k] * t;
-        for (int r = k + 1; r < n; ++r) c[r] -= hc[k] * QR(r, k) * t;
-    }
-    for (int i = 0; i < n; ++i) yv[i] = 0;
-    for (int i = rank - 1; i >= 0; --i) {
-        double s = c[i];
-        for (int j = i + 1; j < rank; ++j) s -= QR(i, j) * yv[j];
-        yv[i] = s / QR(i, i);
-    }
-    if (rank < n) {
-        for (int k = 0; k < rank; ++k) {
-            if (k != rank - 1) { double t = yv[k]; yv[k] = yv[rank - 1]; yv[rank - 1] = t; }
-            if (zc[k] != 0) {
-                double t = yv[rank - 1];
-                for (int cc = rank; cc < n; ++cc) t += QR(k, cc) * yv[cc];
-                yv[rank - 1] -= zc[k] * t;
-                for (int cc = rank; cc < n; ++cc) yv[cc] -= zc[k] * QR(k, cc) * t;
             }
-            if (k != rank - 1) { double t = yv[k]; yv[k] = yv[rank - 1]; yv[rank - 1] = t; }
+            for (int i = 0; i < n; ++i) S.c[i] = b[i];
+            for (int k = 0; k < rank; ++k) {
+                if (S.hc[k] == 0) continue;
+                double tt = S.c[k];
+                for (int r = k + 1; r < n; ++r) tt += QR(r, k) * S.c[r];
+                S.c[k] -= S.hc[k] * tt;
+                for (int r = k + 1; r < n; ++r) S.c[r] -= S.hc[k] * QR(r, k) * tt;
+            }
+            for (int i = 0; i < n; ++i) S.y[i] = 0;
+            for (int i = rank - 1; i >= 0; --i) {
+                double s = S.c[i];
+                for (int j = i + 1; j < rank; ++j) s -= QR(i, j) * S.y[j];
+                S.y[i] = s / QR(i, i);
+            }
+            if (rank < n) {
+                for (int k = 0; k < rank; ++k) {
+                    if (k != rank - 1) { const double tt = S.y[k]; S.y[k] = S.y[rank - 1]; S.y[rank - 1] = tt; }
+                    if (S.zc[k] != 0) {
+                        double tt = S.y[rank - 1];
+                        for (int cc = rank; cc < n; ++cc) tt += QR(k, cc) * S.y[cc];
+                        S.y[rank - 1] -= S.zc[k] * tt;
+                        for (int cc = rank; cc < n; ++cc) S.y[cc] -= S.zc[k] * QR(k, cc) * tt;
+                    }
+                    if (k != rank - 1) { const double tt = S.y[k]; S.y[k] = S.y[rank - 1]; S.y[rank - 1] = tt; }
+                }
+            }
+            for (int i = 0; i < n; ++i) x[S.perm[i]] = S.y[i];
         }
     }
-    for (int i = 0; i < n; ++i) x[perm[i]] = yv[i];
+    __syncthreads();
 #undef QR
 }
 
@@ -535,48 +576,68 @@ template <int MM>
 __global__ __launch_bounds__(kBlock) void k_aa_solve(Ctrl* ctrl, const double* red, int nb) {
     if (ctrl->done || !ctrl->aa_active) return;
     constexpr int NVAL = 2 + 2 * MM;
+    constexpr int NCH = kBlock / NVAL;          // block partials are split into NCH chunks per value
     __shared__ double tot[NVAL];
+    __shared__ double part[NCH * NVAL];
     const int iter = ctrl->aa_iter;
-    if (iter > 0 && threadIdx.x < NVAL) {
-        double s = 0;
-        for (int b = 0; b < nb; ++b) s += red[(size_t)b * NVAL + threadIdx.x];
-        tot[threadIdx.x] = s;
+    if (iter > 0) {
+        // thread (chunk c, value v) sums partials c, c+NCH, ... of value v: independent loads,
+        // fixed order -> deterministic
+        if (threadIdx.x < NCH * NVAL) {
+            const int v = threadIdx.x % NVAL, c = threadIdx.x / NVAL;
+            double s = 0;
+            for (int b = c; b < nb; b += NCH) s += red[(size_t)b * NVAL + v];
+            part[c * NVAL + v] = s;
+        }
+        __syncthreads();
+        if (threadIdx.x < NVAL) {
+            double s = 0;
+            for (int c = 0; c < NCH; ++c) s += part[c * NVAL + threadIdx.x];
+            tot[threadIdx.x] = s;
+        }
     }
     __syncthreads();
-    if (threadIdx.x != 0) return;
+    __shared__ CodLds S;
+    __shared__ double sb[kMaxM], sx[kMaxM];
+    __shared__ int s_mk;
     const int m = ctrl->aa_m, col = ctrl->aa_col;
     if (iter == 0) {
-        ctrl->aa_first = 1; ctrl->aa_j = 0; ctrl->aa_jn = 0; ctrl->aa_mk = 0;
-        ctrl->aa_iter = 1;
+        if (threadIdx.x == 0) {
+            ctrl->aa_first = 1; ctrl->aa_j = 0; ctrl->aa_jn = 0; ctrl->aa_mk = 0;
+            ctrl->aa_iter = 1;
+        }
         return;
     }
     const int mk = iter < m ? iter : m;
     const double eps = 1e-14;
     const double s = fmax(eps, sqrt(tot[0]));
-    ctrl->scale[col] = s;
-    double theta[kMaxM];
-    if (mk == 1) {
-        theta[0] = 0;
-        const double sq = tot[0] / (s * s);
-        ctrl->M[0] = sq;
-        const double dn = sqrt(sq);
-        if (dn > eps) theta[0] = (tot[1] / s) / (dn * dn);
-    } else {
-        double rhs[kMaxM], Mk[kMaxM * kMaxM];
-        for (int c = 0; c < mk; ++c) {
-            if (c == col) continue;
-            const double v = tot[2 + c] / s;
-            ctrl->M[c * m + col] = v;
-            ctrl->M[col * m + c] = v;
-            rhs[c] = tot[2 + MM + c];
+    if (threadIdx.x == 0) {
+        ctrl->scale[col] = s;
+        if (mk == 1) {
+            sx[0] = 0;
+            const double sq = tot[0] / (s * s);
+            ctrl->M[0] = sq;
+            const double dn = sqrt(sq);
+            if (dn > eps) sx[0] = (tot[1] / s) / (dn * dn);
+        } else {
+            for (int c = 0; c < mk; ++c) {
+                if (c == col) continue;
+                const double v = tot[2 + c] / s;
+                ctrl->M[c * m + col] = v;
+                ctrl->M[col * m + c] = v;
+                sb[c] = tot[2 + MM + c];
+            }
+            ctrl->M[col * m + col] = tot[0] / (s * s);
+            sb[col] = tot[1] / s;
+            for (int c = 0; c < mk; ++c)
+                for (int r = 0; r < mk; ++r) S.A[c * mk + r] = ctrl->M[c * m + r];
         }
-        ctrl->M[col * m + col] = tot[0] / (s * s);
-        rhs[col] = tot[1] / s;
-        for (int c = 0; c < mk; ++c)
-            for (int r = 0; r < mk; ++r) Mk[c * mk + r] = ctrl->M[c * m + r];
-        cod_solve_dev(mk, Mk, rhs, theta);
+        s_mk = mk;
     }
-    for (int c = 0; c < mk; ++c) ctrl->coef[c] = theta[c] / ctrl->scale[c];
+    __syncthreads();
+    if (s_mk > 1) cod_solve_block(s_mk, S, sb, sx);
+    if (threadIdx.x != 0) return;
+    for (int c = 0; c < mk; ++c) ctrl->coef[c] = sx[c] / ctrl->scale[c];
     ctrl->aa_first = 0;
     ctrl->aa_j = col;
     ctrl->aa_jn = (col + 1) % m;
@@ -671,9 +732,11 @@ void launch_init_z(const GroupDev& g, const double* xfull, double* z, hipStream_
 }
 
 void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const double* y, const double* Mxbar,
-                double pdt2, double* b, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
+                double pdt2, double* b, const Ctrl* ctrl, int gate_reject, hipStream_t s, const double* xsrc,
+                double* xlast) {
     if (nf == 0) return;
-    hipLaunchKernelGGL(k_rhs, dim3(blocks_for(nf)), dim3(kBlock), 0, s, nf, ptr, row, val, y, Mxbar, pdt2, b, ctrl, gate_reject);
+    hipLaunchKernelGGL(k_rhs, dim3(blocks_for(nf)), dim3(kBlock), 0, s, nf, ptr, row, val, y, Mxbar, pdt2, b, ctrl, gate_reject,
+                       xsrc, xlast);
     AA_CHECK_LAUNCH();
 }
 
@@ -686,6 +749,12 @@ void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b
 void launch_copy(double* dst, const double* src, long long n, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_copy, dim3(grid_for(n)), dim3(kBlock), 0, s, dst, src, n, ctrl, gate_reject);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_restore_ux(double* u, double* x, double* cur, const double* du, const double* dx, long long nz,
+                       long long nx, const Ctrl* ctrl, hipStream_t s) {
+    hipLaunchKernelGGL(k_restore_ux, dim3(grid_for(nz + nx)), dim3(kBlock), 0, s, u, x, cur, du, dx, nz, nx, ctrl);
     AA_CHECK_LAUNCH();
 }
 
@@ -704,7 +773,7 @@ void launch_finalize(int n, int nf, const double* xsrc, const double* xfull, dou
     AA_CHECK_LAUNCH();
 }
 
-int aa_reduce_blocks(long long dim) { return grid_for(dim) < 1024 ? grid_for(dim) : 1024; }
+int aa_reduce_blocks(long long dim) { return grid_for(dim) < 512 ? grid_for(dim) : 512; }
 
 static int mm_bucket(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : 32); }
 

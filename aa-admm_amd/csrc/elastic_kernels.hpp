@@ -58,9 +58,13 @@ void launch_u_and_y(const GroupDev& g, const double* xfull, const double* z, dou
 // prim2 partials of |w(Px - z)|^2 and optionally dual2 partials of |w(z - zref)|^2. gate !done (+reject if redo)
 void launch_prim_z(const GroupDev& g, const double* xfull, const double* z, const double* zref, int nf, int redo,
                    Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s);
-// b = Mxbar + pdt2 * (D^T rows) . y
+// b = Mxbar + pdt2 * (D^T rows) . y ; optionally xlast = xsrc (free part) in the same pass
 void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const double* y, const double* Mxbar,
-                double pdt2, double* b, const Ctrl* ctrl, int gate_reject, hipStream_t s);
+                double pdt2, double* b, const Ctrl* ctrl, int gate_reject, hipStream_t s,
+                const double* xsrc = nullptr, double* xlast = nullptr);
+// UX reject: u = du, x = dx, cur = (du, dx) (gate: reject)
+void launch_restore_ux(double* u, double* x, double* cur, const double* du, const double* dx, long long nz,
+                       long long nx, const Ctrl* ctrl, hipStream_t s);
 // control steps
 enum CtlOp { CTL_PRIM_CHECK = 0, CTL_PRIM_FINAL = 1, CTL_COMB_UX = 2, CTL_PRIM_CHECK_Z = 3, CTL_PRIM_FINAL_Z = 4,
              CTL_COMB_Z = 5 };

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <functional>
+#include <omp.h>
 #include <numeric>
 #include <stdexcept>
 #include <string>
@@ -79,24 +80,70 @@ struct NdBuilder {
 }  // namespace
 
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                         int leaf_size) {
+                         int leaf_size, int top_rows) {
     NdBuilder b(n, xyz, adj_ptr, adj, std::max(1, leaf_size));
     std::vector<int> all(n);
     std::iota(all.begin(), all.end(), 0);
     std::vector<int> roots = b.build(all);
-    // nodes were appended in postorder (children before parents): assign new indices in that order
-    NdTree t;
-    const int nn = (int)b.piv.size();
-    t.beg.resize(nn); t.end.resize(nn); t.parent.assign(nn, -1); t.children = b.kids;
-    int c = 0;
-    for (int s = 0; s < nn; ++s) {
-        t.beg[s] = c;
-        for (int v : b.piv[s]) t.perm.push_back(v);
-        c += (int)b.piv[s].size();
-        t.end[s] = c;
-        for (int k : b.kids[s]) t.parent[k] = s;
+    std::vector<std::vector<int>> piv = std::move(b.piv), kids = std::move(b.kids);
+    // ---- amalgamate the top of the tree into one dense supernode: the upper levels have few,
+    // mid-sized supernodes whose level-by-level solve is pure latency; as one dense block they
+    // are a single wide GEMV per sweep.
+    if (top_rows > 0 && roots.size() == 1) {
+        std::vector<std::vector<int>> depth_nodes(1, {roots[0]});
+        long long rows = (long long)piv[roots[0]].size();
+        int K = 1;
+        for (;;) {
+            std::vector<int> next;
+            for (int s : depth_nodes.back()) next.insert(next.end(), kids[s].begin(), kids[s].end());
+            long long add = 0;
+            for (int s : next) add += (long long)piv[s].size();
+            bool all_inner = !next.empty();
+            for (int s : next) all_inner = all_inner && !kids[s].empty();
+            if (!all_inner || rows + add > top_rows) break;
+            rows += add;
+            depth_nodes.push_back(next);
+            ++K;
+        }
+        if (K > 1) {
+            std::vector<char> top(piv.size(), 0);
+            for (auto& d : depth_nodes) for (int s : d) top[s] = 1;
+            std::vector<int> merged, below;
+            std::function<void(int)> post = [&](int s) {   // postorder over the top nodes only
+                for (int c : kids[s]) {
+                    if (top[c]) post(c);
+                    else below.push_back(c);
+                }
+                merged.insert(merged.end(), piv[s].begin(), piv[s].end());
+            };
+            post(roots[0]);
+            piv.push_back(merged);
+            kids.push_back(below);
+            for (int s = 0; s < (int)top.size(); ++s) if (top[s]) { piv[s].clear(); kids[s].clear(); }
+            roots = {(int)piv.size() - 1};
+        }
     }
-    (void)roots;
+    // ---- postorder numbering from the roots (children first)
+    NdTree t;
+    std::vector<int> order;
+    std::function<void(int)> dfs = [&](int s) {
+        for (int c : kids[s]) dfs(c);
+        order.push_back(s);
+    };
+    for (int r : roots) dfs(r);
+    const int nn = (int)order.size();
+    std::vector<int> newid(piv.size(), -1);
+    for (int i = 0; i < nn; ++i) newid[order[i]] = i;
+    t.beg.resize(nn); t.end.resize(nn); t.parent.assign(nn, -1); t.children.resize(nn);
+    int c = 0;
+    for (int i = 0; i < nn; ++i) {
+        const int s = order[i];
+        t.beg[i] = c;
+        for (int v : piv[s]) t.perm.push_back(v);
+        c += (int)piv[s].size();
+        t.end[i] = c;
+        for (int k : kids[s]) { t.children[i].push_back(newid[k]); t.parent[newid[k]] = i; }
+    }
     if (c != n) throw std::runtime_error("nested_dissection: lost vertices");
     return t;
 }
@@ -125,13 +172,14 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree) {
         const int nb = (int)bnd.size(), f = p + nb;
         for (int j = b0; j < e0; ++j) pos[j] = j - b0;
         for (int k = 0; k < nb; ++k) pos[bnd[k]] = p + k;
-        // ---- assemble front (lower triangle, row-major f x f)
-        std::vector<double> Fr((size_t)f * f, 0.0);
+        // ---- assemble front (lower triangle, column-major f x f: Fc(i,j) at j*f + i)
+        std::vector<double> Fc((size_t)f * f, 0.0);
+        auto FC = [&](int i, int j) -> double& { return Fc[(size_t)j * f + i]; };
         for (int j = b0; j < e0; ++j)
             for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) {
                 int i = A.col[k];
                 if (i < j) continue;
-                Fr[(size_t)pos[i] * f + pos[j]] += A.val[k];
+                FC(pos[i], pos[j]) += A.val[k];
             }
         for (int c : tree.children[s]) {
             const std::vector<int>& cb = F.bnd[c];
@@ -141,46 +189,52 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree) {
                 for (int bb = 0; bb <= a; ++bb) {
                     int ra = pos[cb[a]], rb = pos[cb[bb]];
                     if (ra < rb) std::swap(ra, rb);
-                    Fr[(size_t)ra * f + rb] += Uc[(size_t)a * m + bb];
+                    FC(ra, rb) += Uc[(size_t)a * m + bb];
                 }
             std::vector<double>().swap(U[c]);
         }
-        // ---- partial dense Cholesky (right-looking) of the first p columns
+        // ---- partial dense Cholesky (right-looking, column-major) of the first p columns
         for (int k = 0; k < p; ++k) {
-            double d = Fr[(size_t)k * f + k];
+            double* ck = &Fc[(size_t)k * f];
+            const double d = ck[k];
             if (!(d > 0.0)) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite");
-            d = std::sqrt(d);
-            Fr[(size_t)k * f + k] = d;
-            const double inv = 1.0 / d;
-            for (int i = k + 1; i < f; ++i) Fr[(size_t)i * f + k] *= inv;
-            for (int i = k + 1; i < f; ++i) {
-                const double lik = Fr[(size_t)i * f + k];
-                if (lik == 0.0) continue;
-                double* row = &Fr[(size_t)i * f];
-                const int jmax = i;  // lower triangle incl. diagonal
-                for (int j = k + 1; j <= jmax; ++j) row[j] -= lik * Fr[(size_t)j * f + k];
+            const double dk = std::sqrt(d);
+            ck[k] = dk;
+            const double inv = 1.0 / dk;
+            for (int i = k + 1; i < f; ++i) ck[i] *= inv;
+            const long long work = (long long)(f - k) * (f - k);
+#pragma omp parallel for schedule(dynamic, 16) if (work > 200000)
+            for (int j = k + 1; j < f; ++j) {
+                const double ljk = ck[j];
+                if (ljk == 0.0) continue;
+                double* cj = &Fc[(size_t)j * f];
+                for (int i = j; i < f; ++i) cj[i] -= ck[i] * ljk;
             }
             F.flops += (double)(f - k) * (f - k);
         }
-        // ---- outputs: Linv (p x p lower), LBP (nb x p), update matrix (nb x nb lower)
+        // ---- outputs: Linv (p x p lower, row-major), LBP (nb x p, row-major), update matrix (nb x nb)
         std::vector<double> Li((size_t)p * p, 0.0);
-        for (int j = 0; j < p; ++j) {  // solve L * col = e_j  (forward substitution)
-            Li[(size_t)j * p + j] = 1.0 / Fr[(size_t)j * f + j];
-            for (int i = j + 1; i < p; ++i) {
-                double s = 0;
-                for (int k = j; k < i; ++k) s += Fr[(size_t)i * f + k] * Li[(size_t)k * p + j];
-                Li[(size_t)i * p + j] = -s / Fr[(size_t)i * f + i];
+#pragma omp parallel for schedule(dynamic, 8) if (p > 256)
+        for (int j = 0; j < p; ++j) {  // column j of L^-1: column-oriented forward substitution
+            std::vector<double> r((size_t)p, 0.0);
+            r[j] = 1.0;
+            for (int k = j; k < p; ++k) {
+                const double xk = r[k] / FC(k, k);
+                Li[(size_t)k * p + j] = xk;
+                if (xk == 0.0) continue;
+                const double* ck = &Fc[(size_t)k * f];
+                for (int i = k + 1; i < p; ++i) r[i] -= ck[i] * xk;
             }
         }
         F.Linv[s] = std::move(Li);
         std::vector<double> LBP((size_t)nb * p);
         for (int a = 0; a < nb; ++a)
-            for (int j = 0; j < p; ++j) LBP[(size_t)a * p + j] = Fr[(size_t)(p + a) * f + j];
+            for (int j = 0; j < p; ++j) LBP[(size_t)a * p + j] = FC(p + a, j);
         F.LBP[s] = std::move(LBP);
         if (nb > 0) {
             std::vector<double> Us((size_t)nb * nb);
             for (int a = 0; a < nb; ++a)
-                for (int bb = 0; bb <= a; ++bb) Us[(size_t)a * nb + bb] = Fr[(size_t)(p + a) * f + p + bb];
+                for (int bb = 0; bb <= a; ++bb) Us[(size_t)a * nb + bb] = FC(p + a, p + bb);
             U[s] = std::move(Us);
         }
         F.nnz_L += (size_t)p * (p + 1) / 2 + (size_t)p * nb;

@@ -29,7 +29,10 @@ struct NdTree {
     std::vector<int> parent;        // -1 for roots
     std::vector<std::vector<int>> children;
 };
-NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj, int leaf_size);
+// top_rows > 0: the upper levels of the tree (up to top_rows pivots) are amalgamated into
+// one dense root supernode.
+NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
+                         int leaf_size, int top_rows = 0);
 
 struct SupernodalFactor {
     int n = 0;
