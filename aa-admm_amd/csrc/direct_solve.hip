@@ -49,7 +49,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_level(Plan P, const int* __restri
     const double* Lc = P.linv_cm + P.loff[sn];
     for (int r = tid; r < p; r += BLOCK) {
         double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 4
+#pragma unroll 8
         for (int c = 0; c <= r; ++c) {
             const double v = Lc[(size_t)c * p + r];
             a0 += v * f[3 * c]; a1 += v * f[3 * c + 1]; a2 += v * f[3 * c + 2];
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_level(Plan P, const int* __restri
     double* us = U + P.uoff[sn];
     for (int a = tid; a < nb; a += BLOCK) {
         double s0 = f[3 * (p + a)], s1 = f[3 * (p + a) + 1], s2 = f[3 * (p + a) + 2];
-#pragma unroll 4
+#pragma unroll 8
         for (int j = 0; j < p; ++j) {
             const double v = Bc[(size_t)j * nb + a];
             s0 -= v * yl[3 * j]; s1 -= v * yl[3 * j + 1]; s2 -= v * yl[3 * j + 2];
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_level(Plan P, const int* __restri
     for (int j = tid; j < p; j += BLOCK) {
         const size_t o = 3 * (size_t)(b0 + j);
         double s0 = Y[o], s1 = Y[o + 1], s2 = Y[o + 2];
-#pragma unroll 4
+#pragma unroll 8
         for (int a = 0; a < nb; ++a) {
             const double v = Br[(size_t)a * p + j];
             s0 -= v * xb[3 * a]; s1 -= v * xb[3 * a + 1]; s2 -= v * xb[3 * a + 2];
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_level(Plan P, const int* __restri
     const double* Lr = P.linv_rm + P.loff[sn];
     for (int j = tid; j < p; j += BLOCK) {
         double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 4
+#pragma unroll 8
         for (int k = j; k < p; ++k) {
             const double v = Lr[(size_t)k * p + j];
             a0 += v * t[3 * k]; a1 += v * t[3 * k + 1]; a2 += v * t[3 * k + 2];
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_level(Plan P, const int* __restri
 }
 
 // ------------------------------------------------------------------ big supernodes (multi-WG)
-constexpr int kBigRowsPerWG = 8;   // 2 rows per wave
+constexpr int kBigRowsPerWG = 4;   // one row per wave: more waves, more loads in flight
 
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_big_y(int b0, int p, const double* __re
     for (int r = blockIdx.x * kBigRowsPerWG + wid; r < min(p, (int)(blockIdx.x + 1) * kBigRowsPerWG); r += 4) {
         const double* row = L + (size_t)r * p;
         double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 4
+#pragma unroll 8
         for (int c = lane; c <= r; c += 64) {
             const double v = row[c];
             a0 += v * Fg[3 * c]; a1 += v * Fg[3 * c + 1]; a2 += v * Fg[3 * c + 2];
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void k_big_u(int b0, int p, int nb, const doub
     for (int a = blockIdx.x * kBigRowsPerWG + wid; a < min(nb, (int)(blockIdx.x + 1) * kBigRowsPerWG); a += 4) {
         const double* row = LB + (size_t)a * p;
         double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 4
+#pragma unroll 8
         for (int j = lane; j < p; j += 64) {
             const double v = row[j];
             const size_t o = 3 * (size_t)(b0 + j);
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void k_big_t(int b0, int p, int nb, const doub
     for (int j = blockIdx.x * kBigRowsPerWG + wid; j < min(p, (int)(blockIdx.x + 1) * kBigRowsPerWG); j += 4) {
         const double* row = LBt + (size_t)j * nb;
         double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 4
+#pragma unroll 8
         for (int a = lane; a < nb; a += 64) {
             const double v = row[a];
             const size_t q = 3 * (size_t)bi[a];
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void k_big_x(int b0, int p, const double* __re
     for (int j = blockIdx.x * kBigRowsPerWG + wid; j < min(p, (int)(blockIdx.x + 1) * kBigRowsPerWG); j += 4) {
         const double* row = Lt + (size_t)j * p;
         double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 4
+#pragma unroll 8
         for (int k = j + lane; k < p; k += 64) {
             const double v = row[k];
             a0 += v * Tg[3 * k]; a1 += v * Tg[3 * k + 1]; a2 += v * Tg[3 * k + 2];

@@ -436,14 +436,12 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
     const long long nx = 3LL * nf_;
     Ctrl* c = ctrl_.p;
     local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_NORMAL, true);
-    launch_control(CTL_PRIM_CHECK, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
-    if (accel) {
-        launch_restore_ux(u_.p, xfull_.p, aa_cur_.p, du_.p, dx_.p, Z_, nx, c, s());
-        local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_REDO, true);
-    }
-    launch_control(CTL_PRIM_FINAL, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    launch_check_restore_ux(c, red_a_.p, red_blocks_, accel, u_.p, xfull_.p, accel ? aa_cur_.p : nullptr, du_.p, dx_.p,
+                            Z_, nx, s());
+    if (accel) local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_REDO, true);
     ev_begin("rhs");
-    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s(), xfull_.p, xlast_.p);
+    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s(), xfull_.p, xlast_.p,
+               red_a_.p, red_blocks_);
     ev_end("rhs");
     ev_begin("solve");
     solver_.solve(b_.p, xfull_.p, c, 0, s());
@@ -457,16 +455,18 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
         }
     }
     ev_end("resid");
-    launch_control(CTL_COMB_UX, c, red_a_.p, red_b_.p, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     if (accel) {
         const int m = st_.anderson_m;
         Seg2 G{u_.p, Z_, xfull_.p, nx};
         Seg2 cp{du_.p, Z_, dx_.p, nx};
         ev_begin("aa");
-        launch_aa_reduce(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, cp, m, s());
+        launch_aa_reduce(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, cp, m, s(), red_a_.p, red_b_.p,
+                         red_blocks_, hist_prim_.p, hist_comb_.p, hist_rej_.p);
         launch_aa_solve(c, aa_red_.p, aa_blocks_, m, s());
         launch_aa_mix(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, G, m, s());
         ev_end("aa");
+    } else {
+        launch_control(CTL_COMB_UX, c, red_a_.p, red_b_.p, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     }
 }
 

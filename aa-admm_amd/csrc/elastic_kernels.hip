@@ -33,6 +33,18 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
     return r;
 }
 
+// deterministic block sum of red[0..nb) visible to every thread (same order in every block)
+__device__ __forceinline__ double block_sum_all(const double* red, int nb, double* sm) {
+    double a = 0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) a += red[i];
+    a = block_sum(a, sm);
+    if (threadIdx.x == 0) sm[0] = a;
+    __syncthreads();
+    a = sm[0];
+    __syncthreads();
+    return a;
+}
+
 __device__ __forceinline__ bool gated(const Ctrl* c, int gate_reject) {
     if (!c) return false;
     if (c->done) return true;
@@ -250,9 +262,18 @@ __global__ __launch_bounds__(kBlock) void k_init_z(GroupDev g, const double* __r
 __global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ ptr, const int* __restrict__ row,
                                                 const double* __restrict__ val, const double* __restrict__ y,
                                                 const double* __restrict__ Mxbar, double pdt2, double* __restrict__ b,
-                                                const Ctrl* ctrl, int gate_reject, const double* __restrict__ xsrc,
-                                                double* __restrict__ xlast) {
+                                                Ctrl* ctrl, int gate_reject, const double* __restrict__ xsrc,
+                                                double* __restrict__ xlast, const double* __restrict__ red_final,
+                                                int nb_final) {
     if (gated(ctrl, gate_reject)) return;
+    if (red_final && blockIdx.x == 0) {   // prim after a reject recompute; prev_prim = prim
+        __shared__ double sm[kBlock / 64];
+        const double a = block_sum_all(red_final, nb_final, sm);
+        if (threadIdx.x == 0) {
+            if (ctrl->reject) ctrl->prim = sqrt(a);
+            ctrl->prev_prim = ctrl->prim;
+        }
+    }
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nf) return;
     if (xlast) {   // last_x = curr_x (Solver.cpp:170), fused here: it must follow the reject restore
@@ -261,6 +282,7 @@ __global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ 
         xlast[3 * (size_t)i + 2] = xsrc[3 * (size_t)i + 2];
     }
     double s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll 4
     for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
         const double v = val[k];
         const size_t r = 3 * (size_t)row[k];
@@ -329,6 +351,28 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ dst, const
         dst[i] = src[i];
 }
 
+// UX reject test (Solver.cpp:139-146) fused with the restore (Solver.cpp:150-154): every block
+// reduces the prim partials itself (identical order -> identical decision); block 0 records it.
+__global__ __launch_bounds__(kBlock) void k_check_restore_ux(Ctrl* ctrl, const double* __restrict__ red, int nb,
+                                                             int accel, double* __restrict__ u, double* __restrict__ x,
+                                                             double* __restrict__ cur, const double* __restrict__ du,
+                                                             const double* __restrict__ dx, long long nz, long long nx) {
+    if (ctrl->done) return;
+    __shared__ double sm[kBlock / 64];
+    const double prim = sqrt(block_sum_all(red, nb, sm));
+    const bool reject = accel && ctrl->prev_prim < prim;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctrl->prim = prim;
+        ctrl->reject = reject ? 1 : 0;
+        if (reject) { ctrl->nrej += 1; ctrl->aa_iter = 0; ctrl->aa_col = 0; }   // accelerator->reset
+    }
+    if (!reject) return;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nz + nx; i += (long long)gridDim.x * blockDim.x) {
+        if (i < nz) { const double v = du[i]; u[i] = v; if (cur) cur[i] = v; }
+        else { const double v = dx[i - nz]; x[i - nz] = v; if (cur) cur[i] = v; }
+    }
+}
+
 // UX reject (Solver.cpp:150-154): (u, x) = defaults and accelerator->reset(u, x) stores them
 __global__ __launch_bounds__(kBlock) void k_restore_ux(double* __restrict__ u, double* __restrict__ x,
                                                        double* __restrict__ cur, const double* __restrict__ du,
@@ -382,10 +426,28 @@ __device__ __forceinline__ void seg_set(const Seg2& s, long long i, double v) { 
 template <int MM>
 __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __restrict__ cur, long long eff,
                                                       double* __restrict__ dF, double* __restrict__ dG, Ctrl* ctrl,
-                                                      double* red, Seg2 copy_to) {
+                                                      double* red, Seg2 copy_to, const double* comb_a,
+                                                      const double* comb_b, int comb_nb, double* hist_prim,
+                                                      double* hist_comb, int* hist_rej) {
     if (ctrl->done || !ctrl->aa_active) return;
     constexpr int NVAL = 2 + 2 * MM;
     __shared__ double sm[kBlock / 64][NVAL];
+    if (comb_a) {   // combined residual + break test + record, fused (every block decides alike)
+        __shared__ double sc[kBlock / 64];
+        const double comb = block_sum_all(comb_a, comb_nb, sc) + block_sum_all(comb_b, comb_nb, sc);
+        const bool brk = comb < kCombEps;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            ctrl->comb = comb;
+            ctrl->iters_run += 1;
+            if (brk) ctrl->done = 1;
+            else {
+                const int kk = ctrl->nrec;
+                if (kk < ctrl->cap) { hist_prim[kk] = ctrl->prim; hist_comb[kk] = comb; hist_rej[kk] = ctrl->reject; }
+                ctrl->nrec = kk + 1;
+            }
+        }
+        if (brk) return;
+    }
     const long long dim = G.na + G.nb;
     const int iter = ctrl->aa_iter, col = ctrl->aa_col, m = ctrl->aa_m;
     const int mk = iter < m ? iter : m;
@@ -586,6 +648,7 @@ __global__ __launch_bounds__(kBlock) void k_aa_solve(Ctrl* ctrl, const double* r
         if (threadIdx.x < NCH * NVAL) {
             const int v = threadIdx.x % NVAL, c = threadIdx.x / NVAL;
             double s = 0;
+#pragma unroll 8
             for (int b = c; b < nb; b += NCH) s += red[(size_t)b * NVAL + v];
             part[c * NVAL + v] = s;
         }
@@ -732,11 +795,11 @@ void launch_init_z(const GroupDev& g, const double* xfull, double* z, hipStream_
 }
 
 void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const double* y, const double* Mxbar,
-                double pdt2, double* b, const Ctrl* ctrl, int gate_reject, hipStream_t s, const double* xsrc,
-                double* xlast) {
+                double pdt2, double* b, Ctrl* ctrl, int gate_reject, hipStream_t s, const double* xsrc,
+                double* xlast, const double* red_final, int nb_final) {
     if (nf == 0) return;
     hipLaunchKernelGGL(k_rhs, dim3(blocks_for(nf)), dim3(kBlock), 0, s, nf, ptr, row, val, y, Mxbar, pdt2, b, ctrl, gate_reject,
-                       xsrc, xlast);
+                       xsrc, xlast, red_final, nb_final);
     AA_CHECK_LAUNCH();
 }
 
@@ -749,6 +812,13 @@ void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b
 void launch_copy(double* dst, const double* src, long long n, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_copy, dim3(grid_for(n)), dim3(kBlock), 0, s, dst, src, n, ctrl, gate_reject);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_check_restore_ux(Ctrl* ctrl, const double* red, int nb, int accel, double* u, double* x, double* cur,
+                             const double* du, const double* dx, long long nz, long long nx, hipStream_t s) {
+    const int grid = accel ? grid_for(nz + nx) : 1;
+    hipLaunchKernelGGL(k_check_restore_ux, dim3(grid), dim3(kBlock), 0, s, ctrl, red, nb, accel, u, x, cur, du, dx, nz, nx);
     AA_CHECK_LAUNCH();
 }
 
@@ -778,12 +848,15 @@ int aa_reduce_blocks(long long dim) { return grid_for(dim) < 512 ? grid_for(dim)
 static int mm_bucket(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : 32); }
 
 void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, double* red,
-                      int nblocks, Seg2 copy_to, int m, hipStream_t s) {
+                      int nblocks, Seg2 copy_to, int m, hipStream_t s, const double* comb_a, const double* comb_b,
+                      int comb_nb, double* hist_prim, double* hist_comb, int* hist_rej) {
+#define AA_RED_ARGS G, cur, eff, dF, dG, ctrl, red, copy_to, comb_a, comb_b, comb_nb, hist_prim, hist_comb, hist_rej
     switch (mm_bucket(m)) {
-        case 8: hipLaunchKernelGGL(k_aa_reduce<8>, dim3(nblocks), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, red, copy_to); break;
-        case 16: hipLaunchKernelGGL(k_aa_reduce<16>, dim3(nblocks), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, red, copy_to); break;
-        default: hipLaunchKernelGGL(k_aa_reduce<32>, dim3(nblocks), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, red, copy_to); break;
+        case 8: hipLaunchKernelGGL(k_aa_reduce<8>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
+        case 16: hipLaunchKernelGGL(k_aa_reduce<16>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
+        default: hipLaunchKernelGGL(k_aa_reduce<32>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
     }
+#undef AA_RED_ARGS
     AA_CHECK_LAUNCH();
 }
 

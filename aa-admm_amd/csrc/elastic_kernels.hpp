@@ -59,9 +59,14 @@ void launch_u_and_y(const GroupDev& g, const double* xfull, const double* z, dou
 void launch_prim_z(const GroupDev& g, const double* xfull, const double* z, const double* zref, int nf, int redo,
                    Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s);
 // b = Mxbar + pdt2 * (D^T rows) . y ; optionally xlast = xsrc (free part) in the same pass
+// red_final: UX "prim final" fused in block 0 (prim recomputed after a reject; prev_prim = prim)
 void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const double* y, const double* Mxbar,
-                double pdt2, double* b, const Ctrl* ctrl, int gate_reject, hipStream_t s,
-                const double* xsrc = nullptr, double* xlast = nullptr);
+                double pdt2, double* b, Ctrl* ctrl, int gate_reject, hipStream_t s,
+                const double* xsrc = nullptr, double* xlast = nullptr, const double* red_final = nullptr,
+                int nb_final = 0);
+// UX reject test + restore fused (replaces CTL_PRIM_CHECK + launch_restore_ux)
+void launch_check_restore_ux(Ctrl* ctrl, const double* red, int nb, int accel, double* u, double* x, double* cur,
+                             const double* du, const double* dx, long long nz, long long nx, hipStream_t s);
 // UX reject: u = du, x = dx, cur = (du, dx) (gate: reject)
 void launch_restore_ux(double* u, double* x, double* cur, const double* du, const double* dx, long long nz,
                        long long nx, const Ctrl* ctrl, hipStream_t s);
@@ -87,8 +92,11 @@ void launch_finalize(int n, int nf, const double* xsrc, const double* xfull, dou
 // "default" iterate kept for the reject test); out: where the accelerated iterate goes.
 // m: window (selects the register-resident accumulator bucket 8/16/32).
 int aa_reduce_blocks(long long dim);
+// comb_a/comb_b given: the UX combined residual, break test and record are fused in front
 void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, double* red,
-                      int nblocks, Seg2 copy_to, int m, hipStream_t s);
+                      int nblocks, Seg2 copy_to, int m, hipStream_t s, const double* comb_a = nullptr,
+                      const double* comb_b = nullptr, int comb_nb = 0, double* hist_prim = nullptr,
+                      double* hist_comb = nullptr, int* hist_rej = nullptr);
 void launch_aa_solve(Ctrl* ctrl, const double* red, int nblocks, int m, hipStream_t s);
 void launch_aa_mix(Seg2 G, double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, Seg2 out, int m,
                    hipStream_t s);
