@@ -1,0 +1,369 @@
+"""Headless scene builders for the Geometry (ALM) hot path (host side, numpy).
+
+A `GeomScene` holds exactly what the reference's `ALMGeometrySolver<3>` is fed with
+(Geometry/ALMGeometrySolver.h:81-320): hard and soft `Constraint<3>` objects
+(Geometry/Constraint.h), linear regularisation rows (Geometry/LinearRegularization.h:47-87),
+reference surfaces, the penalty and the Anderson window. Constraints of one kind are kept as
+homogeneous groups (same type / index count / weight / hard-soft), which is also how the C ABI
+(`include/aa_admm.h`, `aa_geom_add_constraints`) and the device kernels batch them.
+
+Builders (the callers SURVEY.md §8f item 2 asks to reproduce headlessly):
+
+* `planarity_from_mesh` -- the constraint recipe of `optimize_mesh` in
+  Geometry/PlanarityOpt.cpp:134-246 (soft PointToRefSurface per vertex, relative uniform
+  Laplacians with the interior-valence-4 split and the boundary rule, hard PlaneConstraint
+  per face with more than 3 vertices), applied to any polygon mesh;
+* `pq_heightfield` -- configs[2]: a quad grid on z = 0.15 sin(2 pi x) cos(2 pi y) whose
+  reference surface is the same field triangulated at twice the resolution;
+* `wire_from_mesh` / `wire_grid` -- the recipe of Geometry/WireMeshOpt.cpp:233-289 (one soft
+  ReferenceSurfceConstraint over all points, 4 AngleConstraints per quad, one
+  EdgeLengthConstraint per edge) -- configs[4] uses a sheared height-field quad grid;
+* `read_obj` -- minimal OBJ reader (v / f records) for the reference's own data files.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import struct
+from typing import List, Optional
+
+import numpy as np
+
+# constraint types (Geometry/Constraint.h)
+PLANE, ANGLE, EDGE, CLOSENESS, POINT_TO_REF, REF_SURFACE = 0, 1, 2, 3, 4, 5
+TYPE_NAMES = {PLANE: "plane", ANGLE: "angle", EDGE: "edge", CLOSENESS: "closeness",
+              POINT_TO_REF: "point_to_ref", REF_SURFACE: "ref_surface"}
+N_PARAMS = {PLANE: 0, ANGLE: 2, EDGE: 1, CLOSENESS: 3, POINT_TO_REF: 1, REF_SURFACE: 1}
+# regularisation row kinds (LinearRegularization.h)
+REG_LAPLACIAN, REG_RELATIVE, REG_CLOSENESS = 0, 1, 2
+
+
+@dataclasses.dataclass
+class ConstraintGroup:
+    type: int
+    idx: np.ndarray            # (count, k) int32 point indices (idI_)
+    weight: float              # constructor weight (weight_ = sqrt(weight))
+    hard: bool
+    params: Optional[np.ndarray] = None   # (count, N_PARAMS[type]) fp64
+    # params: EDGE target length; ANGLE (min_radian, max_radian); CLOSENESS target xyz;
+    #         POINT_TO_REF / REF_SURFACE reference-surface id (stored as a double)
+
+    @property
+    def count(self) -> int:
+        return int(self.idx.shape[0])
+
+    @property
+    def k(self) -> int:
+        return int(self.idx.shape[1])
+
+
+@dataclasses.dataclass
+class GeomScene:
+    x0: np.ndarray                                  # (n, 3) initial points (solve_ADMM init_x)
+    groups: List[ConstraintGroup]
+    reg_kind: np.ndarray                            # (r,) int32
+    reg_ptr: np.ndarray                             # (r+1,) int32 into reg_idx / reg_coef
+    reg_idx: np.ndarray                             # int32
+    reg_coef: np.ndarray                            # fp64 raw coefficients (before sqrt(weight))
+    reg_weight: np.ndarray                          # (r,) fp64
+    reg_target: np.ndarray                          # (r, 3) closeness targets (unused otherwise)
+    ref_points: np.ndarray                          # (n, 3) points the relative Laplacians refer to
+    surfaces: List[tuple]                           # [(V (nv,3) fp64, F (nf,3) int32)]
+    penalty: float = 1e5
+    iters: int = 100
+    aa_m: int = 10
+    name: str = "geom"
+
+    @property
+    def n_points(self) -> int:
+        return int(self.x0.shape[0])
+
+    def hard_cols(self) -> int:
+        return int(sum(g.count * cols_per(g.type, g.k) for g in self.groups if g.hard))
+
+    def avg_edge_length(self) -> float:
+        return float(self.__dict__.get("_avg_edge", 0.0))
+
+
+def cols_per(ctype: int, k: int) -> int:
+    """num_transformed_points (Constraint.h:168-174): SUBTRACT_FIRST drops one column."""
+    return k - 1 if ctype in (ANGLE, EDGE) else k
+
+
+class RegBuilder:
+    """Collects LinearRegularization rows (add_uniform_laplacian / add_laplacian /
+    add_relative_* / add_closeness, Geometry/LinearRegularization.h:47-87)."""
+
+    def __init__(self):
+        self.kind, self.idx, self.coef, self.weight, self.target = [], [], [], [], []
+
+    def _add(self, kind, idx, coefs, weight, target=(0.0, 0.0, 0.0)):
+        assert len(idx) == len(coefs)
+        self.kind.append(kind); self.idx.append(list(idx)); self.coef.append(list(coefs))
+        self.weight.append(float(weight)); self.target.append(list(target))
+
+    def uniform_laplacian(self, idx, weight, relative=False):
+        n = len(idx)
+        coefs = [1.0] + [-1.0 / float(n - 1)] * (n - 1)
+        self._add(REG_RELATIVE if relative else REG_LAPLACIAN, idx, coefs, weight)
+
+    def laplacian(self, idx, coefs, weight, relative=False):
+        self._add(REG_RELATIVE if relative else REG_LAPLACIAN, idx, coefs, weight)
+
+    def closeness(self, i, weight, target):
+        self._add(REG_CLOSENESS, [i], [1.0], weight, target)
+
+    def arrays(self):
+        r = len(self.kind)
+        ptr = np.zeros(r + 1, np.int32)
+        for i, l in enumerate(self.idx):
+            ptr[i + 1] = ptr[i] + len(l)
+        flat = lambda ll, dt: np.array([v for l in ll for v in l], dtype=dt)
+        return dict(reg_kind=np.array(self.kind, np.int32), reg_ptr=ptr, reg_idx=flat(self.idx, np.int32),
+                    reg_coef=flat(self.coef, np.float64), reg_weight=np.array(self.weight, np.float64),
+                    reg_target=np.array(self.target, np.float64).reshape(r, 3))
+
+
+# ----------------------------------------------------------------------------------------
+# mesh helpers
+# ----------------------------------------------------------------------------------------
+
+def read_obj(path, float32=True):
+    """Vertices (n,3) fp64 and faces (list of int lists, 0-based) of an OBJ file.
+
+    float32=True rounds coordinates through fp32 like OpenMesh's OBJ reader, which parses
+    `v` records into `float` (Geometry/external/OpenMesh/Core/IO/reader/OBJReader.cc:294,334):
+    the reference applications see exactly these positions."""
+    V, F = [], []
+    with open(path) as f:
+        for line in f:
+            if line.startswith("v "):
+                V.append([float(t) for t in line.split()[1:4]])
+            elif line.startswith("f "):
+                F.append([int(t.split("/")[0]) - 1 for t in line.split()[1:]])
+    V = np.array(V, np.float64)
+    if float32:
+        V = V.astype(np.float32).astype(np.float64)
+    return V, F
+
+
+def edges_of(faces):
+    """Unique undirected edges in first-seen half-edge order, plus per-edge face lists."""
+    eid, edges, efaces = {}, [], []
+    for fi, f in enumerate(faces):
+        for a in range(len(f)):
+            u, v = f[a], f[(a + 1) % len(f)]
+            key = (min(u, v), max(u, v))
+            if key not in eid:
+                eid[key] = len(edges); edges.append((u, v)); efaces.append([])
+            efaces[eid[key]].append(fi)
+    return edges, efaces
+
+
+def average_edge_length(V, faces):
+    """average_edge_length (Geometry/MeshTypes.h:143-156): mean over the unique edges."""
+    edges, _ = edges_of(faces)
+    e = np.array(edges)
+    return float(np.linalg.norm(V[e[:, 0]] - V[e[:, 1]], axis=1).mean())
+
+
+def one_rings(n, faces):
+    """Cyclic one-ring of every interior manifold vertex (neighbours in circulation order)
+    and the boundary neighbours of boundary vertices with the faces of those boundary edges."""
+    nxt = [dict() for _ in range(n)]   # v -> {prev_nb: next_nb} per incident face
+    for f in faces:
+        k = len(f)
+        for a in range(k):
+            v = f[a]
+            nxt[v][f[(a - 1) % k]] = f[(a + 1) % k]
+    edges, efaces = edges_of(faces)
+    bnd_nbs = [[] for _ in range(n)]
+    for (u, v), fl in zip(edges, efaces):
+        if len(fl) == 1:
+            bnd_nbs[u].append((v, fl[0]))
+            bnd_nbs[v].append((u, fl[0]))
+    rings = [None] * n
+    for v in range(n):
+        if bnd_nbs[v] or not nxt[v]:
+            continue
+        start = next(iter(nxt[v]))
+        ring, cur = [start], nxt[v][start]
+        while cur != start and len(ring) <= len(nxt[v]):
+            ring.append(cur)
+            cur = nxt[v].get(cur, start)
+        rings[v] = ring
+    return rings, bnd_nbs
+
+
+def _surface_field(x, y, amp=0.15):
+    return amp * np.sin(2 * np.pi * x) * np.cos(2 * np.pi * y)
+
+
+def quad_grid(nx, ny, shear=0.0, amp=0.15):
+    """(nx+1)(ny+1) points on the height field over [0,1]^2 (optionally sheared in-plane) and
+    nx*ny counter-clockwise quads."""
+    u, v = np.meshgrid(np.linspace(0, 1, nx + 1), np.linspace(0, 1, ny + 1), indexing="ij")
+    u, v = u.ravel(), v.ravel()
+    x = u + shear * np.sin(np.pi * v) * v
+    y = v
+    P = np.stack([x, y, _surface_field(x, y, amp)], 1)
+    node = lambda i, j: i * (ny + 1) + j
+    I, J = np.meshgrid(np.arange(nx), np.arange(ny), indexing="ij")
+    I, J = I.ravel(), J.ravel()
+    Q = np.stack([node(I, J), node(I + 1, J), node(I + 1, J + 1), node(I, J + 1)], 1).astype(np.int32)
+    return P, Q
+
+
+def field_trimesh(nx, ny, shear=0.0, amp=0.15, x_range=None):
+    """Triangulated height field (2 triangles per cell) -- the reference surface."""
+    P, Q = quad_grid(nx, ny, shear, amp)
+    T = np.concatenate([Q[:, [0, 1, 2]], Q[:, [0, 2, 3]]], 0).astype(np.int32)
+    return P, T
+
+
+# ----------------------------------------------------------------------------------------
+# recipes
+# ----------------------------------------------------------------------------------------
+
+def planarity_from_mesh(V, faces, refV, refF, *, iters=100, aa_m=10, penalty=1e5, closeness_weight=1.0,
+                        laplacian_weight=0.0, relative_laplacian_weight=0.1, name="pq") -> GeomScene:
+    """optimize_mesh of Geometry/PlanarityOpt.cpp:134-246 (defaults: main() :322-325)."""
+    n = len(V)
+    groups: List[ConstraintGroup] = []
+    if closeness_weight > 0:
+        groups.append(ConstraintGroup(POINT_TO_REF, np.arange(n, dtype=np.int32)[:, None], closeness_weight, False,
+                                      np.zeros((n, 1))))
+    reg = RegBuilder()
+    rings, bnd = one_rings(n, faces)
+    if laplacian_weight > 0 or relative_laplacian_weight > 0:
+        for v in range(n):
+            if not bnd[v]:
+                ring = rings[v]
+                if ring is None:
+                    continue
+                vhs = [v] + ring
+                rows = [[vhs[0], vhs[1], vhs[3]], [vhs[0], vhs[2], vhs[4]]] if len(vhs) == 5 else [vhs]
+                for r in rows:
+                    if relative_laplacian_weight > 0:
+                        reg.uniform_laplacian(r, relative_laplacian_weight, relative=True)
+                    if laplacian_weight > 0:
+                        reg.uniform_laplacian(r, laplacian_weight)
+            else:
+                nbs = bnd[v]
+                if len(nbs) == 2 and nbs[0][1] != nbs[1][1]:
+                    r = [v, nbs[0][0], nbs[1][0]]
+                    if relative_laplacian_weight > 0:
+                        reg.uniform_laplacian(r, relative_laplacian_weight, relative=True)
+                    if laplacian_weight > 0:
+                        reg.uniform_laplacian(r, laplacian_weight)
+    by_k = {}
+    for f in faces:
+        if len(f) > 3:
+            by_k.setdefault(len(f), []).append(f)
+    for k in sorted(by_k):
+        groups.append(ConstraintGroup(PLANE, np.array(by_k[k], np.int32), 1.0, True))
+    sc = GeomScene(x0=np.asarray(V, np.float64).copy(), groups=groups, ref_points=np.asarray(V, np.float64).copy(),
+                   surfaces=[(np.asarray(refV, np.float64), np.asarray(refF, np.int32))], penalty=penalty,
+                   iters=iters, aa_m=aa_m, name=name, **reg.arrays())
+    sc._avg_edge = average_edge_length(V, faces)
+    return sc
+
+
+def pq_heightfield(nx=317, ny=317, *, iters=100, aa_m=10, ref_factor=2, **kw) -> GeomScene:
+    """configs[2]: planar-quad optimisation of a (nx x ny)-quad height-field grid (100 489
+    faces at 317 x 317), reference surface = the same field triangulated at `ref_factor`x."""
+    V, Q = quad_grid(nx, ny)
+    RV, RF = field_trimesh(ref_factor * nx, ref_factor * ny)
+    return planarity_from_mesh(V, [list(q) for q in Q], RV, RF, iters=iters, aa_m=aa_m,
+                               name=f"pq{nx}x{ny}", **kw)
+
+
+def wire_from_mesh(V, faces, refV, refF, edge_length, *, iters=100, aa_m=20, penalty=1000.0,
+                   min_angle=math.pi * 0.25, max_angle=math.pi * 0.75, closeness_weight=1.0,
+                   name="wire") -> GeomScene:
+    """optimize_mesh of Geometry/WireMeshOpt.cpp:233-289 (laplacian_weight = -1 as in main)."""
+    n = len(V)
+    groups: List[ConstraintGroup] = []
+    if closeness_weight > 0:
+        groups.append(ConstraintGroup(REF_SURFACE, np.arange(n, dtype=np.int32)[:, None], closeness_weight, False,
+                                      np.zeros((n, 1))))
+    ang = []
+    for f in faces:
+        assert len(f) == 4, "WireMeshOpt expects a quad mesh"
+        for i in range(4):
+            ang.append([f[i], f[(i + 1) % 4], f[(i + 3) % 4]])
+    groups.append(ConstraintGroup(ANGLE, np.array(ang, np.int32), 1.0, True,
+                                  np.tile([min_angle, max_angle], (len(ang), 1)).astype(np.float64)))
+    edges, _ = edges_of(faces)
+    groups.append(ConstraintGroup(EDGE, np.array(edges, np.int32), 1.0, True,
+                                  np.full((len(edges), 1), float(edge_length))))
+    reg = RegBuilder()
+    sc = GeomScene(x0=np.asarray(V, np.float64).copy(), groups=groups, ref_points=np.asarray(V, np.float64).copy(),
+                   surfaces=[(np.asarray(refV, np.float64), np.asarray(refF, np.int32))], penalty=penalty,
+                   iters=iters, aa_m=aa_m, name=name, **reg.arrays())
+    sc._avg_edge = average_edge_length(V, faces)
+    return sc
+
+
+def wire_grid(nx=707, ny=707, *, iters=100, aa_m=20, shear=1.2, ref_factor=2, **kw) -> GeomScene:
+    """configs[4]: wire-mesh optimisation of a sheared height-field quad grid (501 264 points
+    at 707 x 707). The in-plane shear drives corner angles below 45 degrees over part of the
+    grid so the angle constraints are active; the edge target is the mean edge length."""
+    V, Q = quad_grid(nx, ny, shear=shear)
+    RV, RF = field_trimesh(ref_factor * nx, ref_factor * ny, shear=shear)
+    faces = [list(q) for q in Q]
+    L = average_edge_length(V, faces)
+    return wire_from_mesh(V, faces, RV, RF, L, iters=iters, aa_m=aa_m, name=f"wire{nx}x{ny}", **kw)
+
+
+# ----------------------------------------------------------------------------------------
+# reference-driver I/O (test infrastructure; oracle/ref_drivers/ref_geom_driver.cpp)
+# ----------------------------------------------------------------------------------------
+
+def write_geom_scene(sc: GeomScene, path: str) -> None:
+    with open(path, "wb") as f:
+        f.write(b"AAGEOM01")
+        f.write(struct.pack("<i", sc.n_points))
+        f.write(np.ascontiguousarray(sc.x0, "<f8").tobytes())
+        f.write(np.ascontiguousarray(sc.ref_points, "<f8").tobytes())
+        f.write(struct.pack("<i", len(sc.surfaces)))
+        for V, F in sc.surfaces:
+            f.write(struct.pack("<ii", len(V), len(F)))
+            f.write(np.ascontiguousarray(V, "<f8").tobytes())
+            f.write(np.ascontiguousarray(F, "<i4").tobytes())
+        f.write(struct.pack("<i", len(sc.groups)))
+        for g in sc.groups:
+            npar = N_PARAMS[g.type]
+            f.write(struct.pack("<iiiidi", int(g.hard), g.type, g.k, g.count, g.weight, npar))
+            f.write(np.ascontiguousarray(g.idx, "<i4").tobytes())
+            if npar:
+                f.write(np.ascontiguousarray(g.params, "<f8").reshape(g.count, npar).tobytes())
+        r = len(sc.reg_kind)
+        f.write(struct.pack("<i", r))
+        for i in range(r):
+            a, b = sc.reg_ptr[i], sc.reg_ptr[i + 1]
+            f.write(struct.pack("<iid", int(sc.reg_kind[i]), int(b - a), float(sc.reg_weight[i])))
+            f.write(np.ascontiguousarray(sc.reg_idx[a:b], "<i4").tobytes())
+            f.write(np.ascontiguousarray(sc.reg_coef[a:b], "<f8").tobytes())
+            f.write(np.ascontiguousarray(sc.reg_target[i], "<f8").tobytes())
+        f.write(struct.pack("<dii", sc.penalty, sc.iters, sc.aa_m))
+
+
+def read_geom_result(path: str, n_points: int):
+    data = open(path, "rb").read()
+    assert data[:8] == b"AAGEOMR1", "bad result file"
+    off = 8
+
+    def take(dtype, count):
+        nonlocal off
+        a = np.frombuffer(data, dtype=dtype, count=count, offset=off)
+        off += a.nbytes
+        return a.copy()
+
+    nrec = int(take("<i4", 1)[0])
+    comb = take("<f8", nrec)
+    t = take("<f8", nrec)
+    x = take("<f8", 3 * n_points).reshape(-1, 3)
+    setup_s, loop_s = take("<f8", 2)
+    n_faces_added = int(take("<i4", 1)[0])
+    return dict(comb=comb, time_s=t, x=x, setup_s=float(setup_s), loop_s=float(loop_s), faces_added=n_faces_added)

@@ -40,6 +40,14 @@ int  oracle_tet_prox_hyper(int material, double mu, double lambda, double k, dou
                            double* out9);
 void oracle_cod_solve(int n, const double* M_colmajor, const double* b, double* theta);
 
+/* Geometry ALM path (ALMGeometrySolver<3>::setup_ADMM + solve_ADMM): reads an AAGEOM01 scene
+ * file, writes an AAGEOMR1 result file (formats: aa-admm_amd/geom_scenes.py). 0 on success. */
+int  oracle_geom_run_file(const char* scene_path, const char* out_path, char* err, int err_cap);
+/* closest points on a triangle mesh (igl AABB::squared_distance semantics) */
+void oracle_closest_point(const double* V, int nv, const int* F, int nf, const double* P, int np, double* out);
+/* Constraint<3>::project_impl of one constraint on transformed points (3 x cols, column-major) */
+void oracle_geom_project(int type, int k, const double* params, const double* in, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -135,3 +135,47 @@ def cod_solve(M, b):
     th = np.zeros(len(bb))
     L.oracle_cod_solve(C.c_int(len(bb)), _p(Mc, C.c_double), _p(bb, C.c_double), _p(th, C.c_double))
     return th
+
+
+def run_geom(scene):
+    """Runs the oracle's ALM restatement on a geom_scenes.GeomScene; dict like read_geom_result
+    (`faces_added` carries the number of x-updates, i.e. accepted + rejected iterations)."""
+    import importlib
+    import sys
+    import tempfile
+    sys.path.insert(0, os.path.dirname(HERE))
+    gs = importlib.import_module("aa-admm_amd.geom_scenes")
+    L = lib()
+    with tempfile.TemporaryDirectory() as tmp:
+        sp, op = os.path.join(tmp, "s.bin"), os.path.join(tmp, "o.bin")
+        gs.write_geom_scene(scene, sp)
+        err = C.create_string_buffer(512)
+        rc = L.oracle_geom_run_file(sp.encode(), op.encode(), err, C.c_int(512))
+        if rc != 0:
+            raise RuntimeError("oracle: " + err.value.decode())
+        res = gs.read_geom_result(op, scene.n_points)
+    res["x_updates"] = res.pop("faces_added")
+    return res
+
+
+def closest_point(V, F, P):
+    L = lib()
+    V = np.ascontiguousarray(V, np.float64)
+    F = np.ascontiguousarray(F, np.int32)
+    P = np.ascontiguousarray(P, np.float64)
+    out = np.zeros_like(P)
+    L.oracle_closest_point(_p(V, C.c_double), C.c_int(len(V)), _p(F, C.c_int), C.c_int(len(F)), _p(P, C.c_double),
+                           C.c_int(len(P)), _p(out, C.c_double))
+    return out
+
+
+def geom_project(ctype, k, params, pts):
+    """Constraint projection of transformed points pts (cols x 3)."""
+    L = lib()
+    prm = np.zeros(3)
+    if params is not None:
+        prm[:len(np.atleast_1d(params))] = np.atleast_1d(params)
+    inp = np.ascontiguousarray(pts, np.float64)
+    out = np.zeros_like(inp)
+    L.oracle_geom_project(C.c_int(ctype), C.c_int(k), _p(prm, C.c_double), _p(inp, C.c_double), _p(out, C.c_double))
+    return out

@@ -11,6 +11,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 scenes = importlib.import_module("aa-admm_amd.scenes")
+geom_scenes = importlib.import_module("aa-admm_amd.geom_scenes")
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
@@ -50,7 +51,72 @@ def load_case(name):
 
 
 def case_names():
-    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f != "elements.npz")
+    return sorted(f[:-4] for f in os.listdir(GOLDEN)
+                  if f.endswith(".npz") and f not in ("elements.npz", "geom_elements.npz") and not f.startswith("geom_"))
+
+
+# ---------------------------------------------------------------------------- Geometry (ALM)
+def save_geom_case(path, sc, outputs):
+    d = dict(x0=sc.x0, ref_points=sc.ref_points, reg_kind=sc.reg_kind, reg_ptr=sc.reg_ptr, reg_idx=sc.reg_idx,
+             reg_coef=sc.reg_coef, reg_weight=sc.reg_weight, reg_target=sc.reg_target,
+             settings=np.array([sc.penalty, sc.iters, sc.aa_m, sc.avg_edge_length()]),
+             g_meta=np.array([[g.type, int(g.hard), g.k] for g in sc.groups], np.int32).reshape(-1, 3),
+             g_weight=np.array([g.weight for g in sc.groups], np.float64))
+    for i, g in enumerate(sc.groups):
+        d[f"g{i}_idx"] = g.idx
+        if g.params is not None:
+            d[f"g{i}_params"] = g.params
+    for i, (V, F) in enumerate(sc.surfaces):
+        d[f"s{i}_V"], d[f"s{i}_F"] = V, F
+    for k, v in outputs.items():
+        d["out_" + k] = v
+    np.savez_compressed(path, **d)
+
+
+def load_geom_case(name):
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    gs = geom_scenes
+    groups = []
+    for i, (t, h, k) in enumerate(d["g_meta"]):
+        groups.append(gs.ConstraintGroup(int(t), d[f"g{i}_idx"].astype(np.int32), float(d["g_weight"][i]), bool(h),
+                                         d[f"g{i}_params"] if f"g{i}_params" in d else None))
+    surfaces, i = [], 0
+    while f"s{i}_V" in d:
+        surfaces.append((d[f"s{i}_V"], d[f"s{i}_F"].astype(np.int32)))
+        i += 1
+    st = d["settings"]
+    sc = gs.GeomScene(x0=d["x0"], groups=groups, reg_kind=d["reg_kind"].astype(np.int32),
+                      reg_ptr=d["reg_ptr"].astype(np.int32), reg_idx=d["reg_idx"].astype(np.int32),
+                      reg_coef=d["reg_coef"], reg_weight=d["reg_weight"], reg_target=d["reg_target"],
+                      ref_points=d["ref_points"], surfaces=surfaces, penalty=float(st[0]), iters=int(st[1]),
+                      aa_m=int(st[2]), name=name)
+    sc._avg_edge = float(st[3])
+    out = {k[4:]: d[k] for k in d.files if k.startswith("out_")}
+    return sc, out
+
+
+def geom_case_names():
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("geom_") and f.endswith(".npz")
+                  and f != "geom_elements.npz")
+
+
+def compare_geom(ref, got, tol_comb, tol_x, n_check=None):
+    """ALM residual curves judged relative to comb_0, plus the solution (get_solution)."""
+    fails = []
+    n = min(len(ref["comb"]), len(got["comb"]))
+    if len(ref["comb"]) != len(got["comb"]):
+        fails.append(f"record count {len(got['comb'])} != {len(ref['comb'])}")
+    if n_check is not None:
+        n = min(n, n_check)
+    c0 = ref["comb"][0]
+    dc = np.max(np.abs(ref["comb"][:n] - got["comb"][:n])) / c0
+    if not dc <= tol_comb:
+        fails.append(f"comb dev {dc:.3e} (tol {tol_comb:g})")
+    xr, xg = ref["x"], got["x"]
+    dx = np.linalg.norm(xr - xg) / np.linalg.norm(xr)
+    if not dx <= tol_x:
+        fails.append(f"final x rel err {dx:.3e} (tol {tol_x:g})")
+    return fails
 
 
 def compare(ref_steps, got_steps, tol_comb, tol_x, n_check=None):
