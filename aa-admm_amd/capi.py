@@ -25,7 +25,14 @@ EXPORTS = [
     "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats",
+    "aa_geom_create", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
+    "aa_geom_add_closeness", "aa_geom_setup", "aa_geom_solve", "aa_geom_get_solution", "aa_geom_get_history",
+    "aa_geom_runtime_info", "aa_geom_closest_points", "aa_geom_bench_iterations", "aa_geom_kernel_stats",
 ]
+
+# Geometry constraint types (Geometry/Constraint.h) and SPD solver types (SolverCommon.h)
+AA_CON_PLANE, AA_CON_ANGLE, AA_CON_EDGE, AA_CON_CLOSENESS, AA_CON_POINT_TO_REF, AA_CON_REF_SURFACE = range(6)
+AA_SPD_LDLT, AA_SPD_LLT = 0, 1
 
 
 class Lame(C.Structure):
@@ -239,3 +246,136 @@ def run_scene(ctx: Context, scene, n_steps=None):
         h["step_ms"] = s.runtime().step_ms
         out.append(h)
     return out, s
+
+
+# ------------------------------------------------------------------------------------------
+# Geometry: ALMGeometrySolver<3> (Geometry/ALMGeometrySolver.h)
+# ------------------------------------------------------------------------------------------
+
+class GeomRuntime(C.Structure):
+    _fields_ = [("setup_ms", C.c_double), ("factor_ms", C.c_double), ("solve_ms", C.c_double),
+                ("iterations", C.c_int), ("accepted", C.c_int), ("rejects", C.c_int), ("n_points", C.c_int),
+                ("nnz_factor", C.c_longlong), ("hard_cols", C.c_longlong), ("soft_cols", C.c_longlong),
+                ("n_constraints", C.c_longlong)]
+
+
+class GeomSolver:
+    """Mirror of ALMGeometrySolver<3>: add_hard/soft constraints, add_*laplacian, add_closeness,
+    setup_ADMM, solve_ADMM, get_solution, function_values_ / elapsed_time_."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.h = C.c_void_p()
+        self.n = 0
+        _chk(lib().aa_geom_create(ctx.h, C.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            lib().aa_geom_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_ref_surface(self, V, F):
+        V = np.ascontiguousarray(V, np.float64).reshape(-1)
+        F = np.ascontiguousarray(F, np.int32).reshape(-1)
+        i = C.c_int()
+        _chk(lib().aa_geom_add_ref_surface(self.h, _dp(V), C.c_int(len(V) // 3), _ip(F), C.c_int(len(F) // 3),
+                                           C.byref(i)))
+        return i.value
+
+    def add_constraints(self, hard, ctype, idx, weight=1.0, params=None):
+        idx = np.ascontiguousarray(idx, np.int32)
+        if idx.ndim == 1:
+            idx = idx[:, None]
+        count, k = idx.shape
+        prm = None if params is None else np.ascontiguousarray(params, np.float64).reshape(count, -1)
+        _chk(lib().aa_geom_add_constraints(self.h, C.c_int(int(hard)), C.c_int(ctype), _ip(idx), C.c_int(k),
+                                           C.c_int(count), C.c_double(weight), None if prm is None else _dp(prm)))
+
+    def add_laplacian(self, idx, coefs, weight, ref_points=None):
+        i = np.ascontiguousarray(idx, np.int32)
+        c = np.ascontiguousarray(coefs, np.float64)
+        r = None if ref_points is None else np.ascontiguousarray(ref_points, np.float64).reshape(-1)
+        _chk(lib().aa_geom_add_laplacian(self.h, _ip(i), _dp(c), C.c_int(len(i)), C.c_double(weight),
+                                         None if r is None else _dp(r)))
+
+    def add_closeness(self, idx, weight, target):
+        t = np.ascontiguousarray(target, np.float64)
+        _chk(lib().aa_geom_add_closeness(self.h, C.c_int(idx), C.c_double(weight), _dp(t)))
+
+    def setup(self, n_points, penalty, spd=AA_SPD_LDLT):
+        self.n = n_points
+        _chk(lib().aa_geom_setup(self.h, C.c_int(n_points), C.c_double(penalty), C.c_int(spd)))
+
+    def solve(self, init_x, rel_eps, max_iter, m):
+        x = np.ascontiguousarray(init_x, np.float64).reshape(-1)
+        _chk(lib().aa_geom_solve(self.h, _dp(x), C.c_double(rel_eps), C.c_int(max_iter), C.c_int(m)))
+
+    def solution(self):
+        out = np.zeros(3 * self.n)
+        _chk(lib().aa_geom_get_solution(self.h, _dp(out)))
+        return out.reshape(-1, 3)
+
+    def history(self, cap=1 << 20):
+        n = C.c_int()
+        _chk(lib().aa_geom_get_history(self.h, None, None, C.c_int(0), C.byref(n)))
+        k = n.value
+        c, t = np.zeros(max(k, 1)), np.zeros(max(k, 1))
+        _chk(lib().aa_geom_get_history(self.h, _dp(c), _dp(t), C.c_int(k), C.byref(n)))
+        return dict(comb=c[:k].copy(), time_s=t[:k].copy())
+
+    def runtime(self) -> GeomRuntime:
+        rt = GeomRuntime()
+        _chk(lib().aa_geom_runtime_info(self.h, C.byref(rt)))
+        return rt
+
+    def closest_points(self, surface, P):
+        P = np.ascontiguousarray(P, np.float64).reshape(-1)
+        out = np.zeros_like(P)
+        _chk(lib().aa_geom_closest_points(self.h, C.c_int(surface), _dp(P), C.c_int(len(P) // 3), _dp(out)))
+        return out.reshape(-1, 3)
+
+    def bench_iterations(self, iters):
+        ms = C.c_double()
+        _chk(lib().aa_geom_bench_iterations(self.h, C.c_int(iters), C.byref(ms)))
+        return ms.value
+
+    def kernel_stats(self, name):
+        a, b, n = C.c_double(), C.c_double(), C.c_int()
+        _chk(lib().aa_geom_kernel_stats(self.h, name.encode(), C.byref(a), C.byref(b), C.byref(n)))
+        return dict(avg_ms=a.value, bytes=b.value, launches=n.value)
+
+
+def geom_from_scene(ctx: Context, sc) -> GeomSolver:
+    """Binds a geom_scenes.GeomScene the way optimize_mesh (PlanarityOpt.cpp / WireMeshOpt.cpp) does."""
+    g = GeomSolver(ctx)
+    sids = [g.add_ref_surface(V, F) for V, F in sc.surfaces]
+    for grp in sc.groups:
+        prm = grp.params
+        if grp.type in (AA_CON_POINT_TO_REF, AA_CON_REF_SURFACE):
+            prm = np.array([[sids[int(p)]] for p in np.asarray(prm).reshape(grp.count, -1)[:, 0]], np.float64)
+        g.add_constraints(grp.hard, grp.type, grp.idx, grp.weight, prm)
+    for i in range(len(sc.reg_kind)):
+        a, b = sc.reg_ptr[i], sc.reg_ptr[i + 1]
+        kind = int(sc.reg_kind[i])
+        if kind == 2:
+            g.add_closeness(int(sc.reg_idx[a]), float(sc.reg_weight[i]), sc.reg_target[i])
+        else:
+            g.add_laplacian(sc.reg_idx[a:b], sc.reg_coef[a:b], float(sc.reg_weight[i]),
+                            sc.ref_points if kind == 1 else None)
+    g.setup(sc.n_points, sc.penalty)
+    return g
+
+
+def run_geom(ctx: Context, sc):
+    """setup_ADMM + solve_ADMM of a GeomScene; returns dict(comb, time_s, x) and the solver."""
+    g = geom_from_scene(ctx, sc)
+    g.solve(sc.x0, 1e-8 * max(sc.avg_edge_length(), 1e-300), sc.iters, sc.aa_m)
+    h = g.history()
+    h["x"] = g.solution()
+    return h, g

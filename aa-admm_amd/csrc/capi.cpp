@@ -6,9 +6,11 @@
 
 #include "../../include/aa_admm.h"
 #include "elastic.hpp"
+#include "geom.hpp"
 
 struct aa_ctx_s { aa::Context c; };
 struct aa_elastic_s { aa::ElasticSolver* s; aa_ctx_s* ctx; };
+struct aa_geom_s { aa::GeomSolver* s; aa_ctx_s* ctx; };
 
 namespace {
 thread_local std::string g_err;
@@ -192,6 +194,101 @@ int aa_elastic_bench_iterations(aa_elastic h, int iters, double* ms) {
 }
 
 int aa_elastic_kernel_stats(aa_elastic h, const char* name, double* avg_ms, double* bytes, int* launches) {
+    return guarded([&] {
+        NEED(h && name, "null argument");
+        if (!h->s->kernel_stats(name, avg_ms, bytes, launches)) throw aa::Error(AA_ERR_ARG, std::string("no kernel class ") + name);
+    });
+}
+
+// ---- Geometry (ALMGeometrySolver<3>) -------------------------------------------------------
+int aa_geom_create(aa_ctx ctx, aa_geom* out) {
+    return guarded([&] {
+        NEED(ctx && out, "aa_geom_create: null argument");
+        AA_HIP(hipSetDevice(ctx->c.device));
+        auto* h = new aa_geom_s;
+        h->ctx = ctx;
+        h->s = new aa::GeomSolver(&ctx->c);
+        *out = h;
+    });
+}
+
+int aa_geom_destroy(aa_geom h) {
+    return guarded([&] {
+        if (!h) return;
+        (void)hipSetDevice(h->ctx->c.device);
+        delete h->s;
+        delete h;
+    });
+}
+
+int aa_geom_add_ref_surface(aa_geom h, const double* V3, int nv, const int* F3, int nf, int* id) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        const int i = h->s->add_ref_surface(V3, nv, F3, nf);
+        if (id) *id = i;
+    });
+}
+
+int aa_geom_add_constraints(aa_geom h, int hard, int type, const int* idx, int k, int count, double weight,
+                            const double* params) {
+    return guarded([&] { NEED(h, "null handle"); h->s->add_constraints(hard, type, idx, k, count, weight, params); });
+}
+
+int aa_geom_add_laplacian(aa_geom h, const int* idx, const double* coefs, int k, double weight, const double* ref3) {
+    return guarded([&] { NEED(h, "null handle"); h->s->add_laplacian(idx, coefs, k, weight, ref3); });
+}
+
+int aa_geom_add_closeness(aa_geom h, int idx, double weight, const double* target3) {
+    return guarded([&] { NEED(h, "null handle"); h->s->add_closeness(idx, weight, target3); });
+}
+
+int aa_geom_setup(aa_geom h, int n_points, double penalty, int spd_solver_type) {
+    return guarded([&] { NEED(h, "null handle"); h->s->setup(n_points, penalty, spd_solver_type); });
+}
+
+int aa_geom_solve(aa_geom h, const double* init_x3, double rel_eps, int max_iter, int m) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        h->s->solve(init_x3, rel_eps, max_iter, m);
+    });
+}
+
+int aa_geom_get_solution(aa_geom h, double* x3) {
+    return guarded([&] { NEED(h && x3, "null argument"); h->s->get_solution(x3); });
+}
+
+int aa_geom_get_history(aa_geom h, double* comb, double* time_s, int cap, int* n) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        const int k = h->s->history(comb, time_s, cap);
+        if (n) *n = k;
+    });
+}
+
+int aa_geom_runtime_info(aa_geom h, aa_geom_runtime* out) {
+    return guarded([&] { NEED(h && out, "null argument"); *out = h->s->runtime(); });
+}
+
+int aa_geom_closest_points(aa_geom h, int surface, const double* p3, int n, double* out3) {
+    return guarded([&] {
+        NEED(h && (n == 0 || (p3 && out3)), "null argument");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        h->s->closest_points(surface, p3, n, out3);
+    });
+}
+
+int aa_geom_bench_iterations(aa_geom h, int iters, double* ms) {
+    return guarded([&] {
+        NEED(h && iters >= 0, "bad argument");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        const double t = h->s->bench_iterations(iters);
+        if (ms) *ms = t;
+    });
+}
+
+int aa_geom_kernel_stats(aa_geom h, const char* name, double* avg_ms, double* bytes, int* launches) {
     return guarded([&] {
         NEED(h && name, "null argument");
         if (!h->s->kernel_stats(name, avg_ms, bytes, launches)) throw aa::Error(AA_ERR_ARG, std::string("no kernel class ") + name);

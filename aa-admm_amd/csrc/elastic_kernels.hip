@@ -429,7 +429,7 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
                                                       double* red, Seg2 copy_to, const double* comb_a,
                                                       const double* comb_b, int comb_nb, double* hist_prim,
                                                       double* hist_comb, int* hist_rej) {
-    if (ctrl->done || !ctrl->aa_active) return;
+    if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
     constexpr int NVAL = 2 + 2 * MM;
     __shared__ double sm[kBlock / 64][NVAL];
     if (comb_a) {   // combined residual + break test + record, fused (every block decides alike)
@@ -636,7 +636,7 @@ __device__ void cod_solve_block(int n, CodLds& S, const double* b, double* x) {
 
 template <int MM>
 __global__ __launch_bounds__(kBlock) void k_aa_solve(Ctrl* ctrl, const double* red, int nb) {
-    if (ctrl->done || !ctrl->aa_active) return;
+    if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
     constexpr int NVAL = 2 + 2 * MM;
     constexpr int NCH = kBlock / NVAL;          // block partials are split into NCH chunks per value
     __shared__ double tot[NVAL];
@@ -715,7 +715,7 @@ template <int MM>
 __global__ __launch_bounds__(kBlock) void k_aa_mix(Seg2 G, double* __restrict__ cur, long long eff,
                                                    double* __restrict__ dF, double* __restrict__ dG, Ctrl* ctrl,
                                                    Seg2 out) {
-    if (ctrl->done || !ctrl->aa_active) return;
+    if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
     const long long dim = G.na + G.nb;
     const int first = ctrl->aa_first, j = ctrl->aa_j, jn = ctrl->aa_jn, mk = ctrl->aa_mk;
     const double s = ctrl->aa_s;

@@ -26,13 +26,15 @@ struct GroupDev {
 struct Ctrl {
     double prim, prev_prim, comb, prim2, dual2;
     int reject, done, nrec, nrej;
-    int cap, fail, iters_run, pad1;
+    int cap, fail, iters_run, aa_skip;   // aa_skip: ALM reject -> no Anderson step this iteration
     // Anderson acceleration (AndersonAcceleration.h state)
     int aa_m, aa_iter, aa_col, aa_mk;
     int aa_j, aa_jn, aa_first, aa_active;
     double aa_s;
     double scale[kMaxM], coef[kMaxM];
     double M[kMaxM * kMaxM];      // normal-equation matrix, column-major m x m
+    // Geometry ALM loop (ALMGeometrySolver.h:186-263): `reset` flag and accepted-iteration cap
+    int alm_reset, max_iter;
 };
 
 // A vector seen as two concatenated segments (e.g. (u, x) of the UX variant).

@@ -1,0 +1,637 @@
+// Host orchestration of the Geometry (ALM) hot path (see geom.hpp).
+//
+// Reference call stack being replaced:
+//   ALMGeometrySolver<3>::add_hard_constraint / add_soft_constraint / add_*laplacian / add_closeness
+//                                              Geometry/ALMGeometrySolver.h:286-318
+//   ALMGeometrySolver<3>::setup_ADMM           Geometry/ALMGeometrySolver.h:81-161
+//   ALMGeometrySolver<3>::solve_ADMM           Geometry/ALMGeometrySolver.h:163-283
+// Every ALM iteration is enqueued on one HIP stream; the accept/reject decision of the
+// reference (comb < prev, reset, Anderson reset) is taken by a device control kernel that
+// gates the following kernels, so the loop runs as replays of a captured hipGraph with one
+// host synchronisation at the end (plus one per extra chunk when rejections extend the loop).
+#include "geom.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cfloat>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+
+#include "spd_direct.hpp"
+
+namespace aa {
+
+namespace {
+
+int n_params(int type) {
+    switch (type) {
+        case GEO_EDGE: return 1;
+        case GEO_ANGLE: return 2;
+        case GEO_CLOSENESS: return 3;
+        case GEO_POINT_TO_REF: case GEO_REF_SURFACE: return 1;
+        default: return 0;
+    }
+}
+int cols_of(int type, int K) { return (type == GEO_ANGLE || type == GEO_EDGE) ? K - 1 : K; }
+
+// rows of one constraint's reduction block D_c (cols x K), Constraint::add_constraint
+// (Geometry/Constraint.h:132-159), weight w folded in
+std::vector<double> reduction_block(int type, int K, double w) {
+    const int C = cols_of(type, K);
+    std::vector<double> D((size_t)C * K, 0.0);
+    if (type == GEO_PLANE) {
+        const double c1 = (1.0 - 1.0 / K) * w, c2 = -w / K;
+        for (int i = 0; i < K; ++i) for (int j = 0; j < K; ++j) D[(size_t)i * K + j] = i == j ? c1 : c2;
+    } else if (type == GEO_ANGLE || type == GEO_EDGE) {
+        for (int i = 1; i < K; ++i) { D[(size_t)(i - 1) * K] = -w; D[(size_t)(i - 1) * K + i] = w; }
+    } else {
+        for (int i = 0; i < K; ++i) D[(size_t)i * K + i] = w;
+    }
+    return D;
+}
+
+// median-split BVH, leaves of <= 4 triangles, depth-first node order
+struct BvhBuilder {
+    const double* V;
+    const int* F;
+    std::vector<int> ids;
+    std::vector<double> cen;
+    std::vector<BvhNode>* nodes;
+    std::vector<BvhTri>* tris;
+    int build(int b, int e) {
+        BvhNode nd{};
+        for (int d = 0; d < 3; ++d) { nd.lo[d] = DBL_MAX; nd.hi[d] = -DBL_MAX; }
+        double clo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, chi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (int i = b; i < e; ++i) {
+            const int t = ids[i];
+            for (int a = 0; a < 3; ++a)
+                for (int d = 0; d < 3; ++d) {
+                    const double v = V[3 * (size_t)F[3 * (size_t)t + a] + d];
+                    nd.lo[d] = std::min(nd.lo[d], v); nd.hi[d] = std::max(nd.hi[d], v);
+                }
+            for (int d = 0; d < 3; ++d) { clo[d] = std::min(clo[d], cen[3 * (size_t)t + d]); chi[d] = std::max(chi[d], cen[3 * (size_t)t + d]); }
+        }
+        const int me = (int)nodes->size();
+        nodes->push_back(nd);
+        if (e - b <= 4) {
+            (*nodes)[me].a = (int)tris->size();
+            (*nodes)[me].b = -(e - b);
+            for (int i = b; i < e; ++i) {
+                BvhTri tr;
+                for (int a = 0; a < 3; ++a)
+                    for (int d = 0; d < 3; ++d) tr.v[3 * a + d] = V[3 * (size_t)F[3 * (size_t)ids[i] + a] + d];
+                tris->push_back(tr);
+            }
+            return me;
+        }
+        int ax = 0;
+        for (int d = 1; d < 3; ++d) if (chi[d] - clo[d] > chi[ax] - clo[ax]) ax = d;
+        const int mid = (b + e) / 2;
+        std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e,
+                         [&](int p, int q) { return cen[3 * (size_t)p + ax] < cen[3 * (size_t)q + ax]; });
+        build(b, mid);
+        const int r = build(mid, e);
+        (*nodes)[me].a = r;
+        (*nodes)[me].b = 0;
+        return me;
+    }
+};
+
+}  // namespace
+
+GeomSolver::~GeomSolver() {
+    drop_graph();
+    for (auto& kv : kstats_)
+        for (auto e : kv.second.ev) (void)hipEventDestroy(e);
+}
+
+void GeomSolver::drop_graph() {
+    if (gexec_) (void)hipGraphExecDestroy(gexec_);
+    if (graph_) (void)hipGraphDestroy(graph_);
+    gexec_ = nullptr;
+    graph_ = nullptr;
+}
+
+int GeomSolver::add_ref_surface(const double* V3, int nv, const int* F3, int nf) {
+    if (nv <= 0 || nf <= 0 || !V3 || !F3) throw Error(ERR_ARG, "add_ref_surface: empty surface");
+    for (long long i = 0; i < 3LL * nf; ++i)
+        if (F3[i] < 0 || F3[i] >= nv) throw Error(ERR_ARG, "add_ref_surface: face index out of range");
+    Surface S;
+    BvhBuilder B;
+    B.V = V3; B.F = F3;
+    B.ids.resize(nf);
+    std::iota(B.ids.begin(), B.ids.end(), 0);
+    B.cen.resize(3 * (size_t)nf);
+    for (int t = 0; t < nf; ++t)
+        for (int d = 0; d < 3; ++d)
+            B.cen[3 * (size_t)t + d] = (V3[3 * (size_t)F3[3 * t] + d] + V3[3 * (size_t)F3[3 * t + 1] + d] + V3[3 * (size_t)F3[3 * t + 2] + d]) / 3.0;
+    B.nodes = &S.nodes;
+    B.tris = &S.tris;
+    S.nodes.reserve(nf);
+    S.tris.reserve(nf);
+    B.build(0, nf);
+    S.dnodes.upload(S.nodes, s());
+    S.dtris.upload(S.tris, s());
+    AA_HIP(hipStreamSynchronize(s()));
+    surfs_.push_back(std::move(S));
+    return (int)surfs_.size() - 1;
+}
+
+// add_hard_constraint / add_soft_constraint of `count` constraints of one type
+// (ALMGeometrySolver.h:286-294; constructors Constraint.h:194-414)
+void GeomSolver::add_constraints(int hard, int type, const int* idx, int k, int count, double weight,
+                                 const double* params) {
+    if (setup_done_) throw Error(ERR_STATE, "constraints must be added before setup_ADMM");
+    if (count < 0) throw Error(ERR_ARG, "add_constraints: negative count");
+    if (count == 0) return;
+    if (type < GEO_PLANE || type > GEO_REF_SURFACE) throw Error(ERR_ARG, "add_constraints: unknown constraint type");
+    const int want = type == GEO_ANGLE ? 3 : type == GEO_EDGE ? 2 : type == GEO_PLANE ? k : 1;
+    if (k != want) throw Error(ERR_ARG, "add_constraints: wrong number of indices for this constraint type");
+    if (type == GEO_PLANE && (k < 3 || k > kGeoMaxK))
+        throw Error(ERR_ARG, "add_constraints: plane constraints need 3..8 points on this device path");
+    if (!(weight >= 0.0)) throw Error(ERR_ARG, "add_constraints: weight must be >= 0");
+    const int P = n_params(type);
+    if (P && !params) throw Error(ERR_ARG, "add_constraints: this constraint type needs parameters");
+    if (!idx && type != GEO_REF_SURFACE) throw Error(ERR_ARG, "add_constraints: null indices");
+    int surf = -1;
+    if (type == GEO_POINT_TO_REF || type == GEO_REF_SURFACE) {
+        surf = (int)params[0];
+        for (int c = 1; c < count; ++c)
+            if ((int)params[(size_t)c * P] != surf) throw Error(ERR_ARG, "add_constraints: one reference surface per call");
+        if (surf < 0 || surf >= (int)surfs_.size()) throw Error(ERR_ARG, "add_constraints: unknown reference surface");
+    }
+    const auto key = std::make_tuple(hard ? 1 : 0, type, k, weight, surf);
+    auto it = group_of_.find(key);
+    if (it == group_of_.end()) {
+        HostGroup g;
+        g.hard = hard ? 1 : 0; g.type = type; g.K = k; g.weight = weight; g.surf = surf;
+        hgroups_.push_back(g);
+        it = group_of_.emplace(key, (int)hgroups_.size() - 1).first;
+    }
+    HostGroup& g = hgroups_[it->second];
+    for (int c = 0; c < count; ++c) {
+        for (int a = 0; a < k; ++a) {
+            const int v = idx ? idx[(size_t)c * k + a] : c;
+            if (v < 0) throw Error(ERR_ARG, "add_constraints: negative point index");
+            g.idx.push_back(v);
+        }
+        for (int p = 0; p < P; ++p) g.prm.push_back(params[(size_t)c * P + p]);
+    }
+}
+
+// LinearRegularization::add_laplacian_helper (Geometry/LinearRegularization.h:119-141)
+void GeomSolver::add_laplacian(const int* idx, const double* coefs, int k, double weight, const double* ref_points3) {
+    if (setup_done_) throw Error(ERR_STATE, "regularization must be added before setup_ADMM");
+    if (k <= 0 || !idx || !coefs) throw Error(ERR_ARG, "add_laplacian: bad input");
+    Reg r;
+    const double sw = std::sqrt(weight);
+    double t[3] = {0, 0, 0};
+    for (int i = 0; i < k; ++i) {
+        if (idx[i] < 0) throw Error(ERR_ARG, "add_laplacian: negative point index");
+        r.idx.push_back(idx[i]);
+        r.coef.push_back(coefs[i] * sw);
+        if (ref_points3)
+            for (int d = 0; d < 3; ++d) t[d] += ref_points3[3 * (size_t)idx[i] + d] * coefs[i];
+    }
+    for (int d = 0; d < 3; ++d) r.tgt[d] = t[d] * sw;
+    regs_.push_back(r);
+}
+
+// LinearRegularization::add_closeness (LinearRegularization.h:75-89)
+void GeomSolver::add_closeness(int idx, double weight, const double* target3) {
+    if (setup_done_) throw Error(ERR_STATE, "regularization must be added before setup_ADMM");
+    if (idx < 0 || !target3) throw Error(ERR_ARG, "add_closeness: bad input");
+    Reg r;
+    const double sw = std::sqrt(weight);
+    r.idx.push_back(idx);
+    r.coef.push_back(sw);
+    for (int d = 0; d < 3; ++d) r.tgt[d] = target3[d] * sw;
+    regs_.push_back(r);
+}
+
+// setup_ADMM (ALMGeometrySolver.h:81-161): global = rho D_h^T D_h + D_s^T D_s + L^T L and
+// rhs_fixed = L^T b. The factorisation needs point positions for the nested-dissection order,
+// so it happens at the first solve (and is reused by later solves).
+void GeomSolver::setup(int n_points, double penalty, int spd_solver_type) {
+    if (setup_done_) throw Error(ERR_STATE, "setup_ADMM called twice");
+    if (n_points <= 0) throw Error(ERR_ARG, "setup_ADMM: n_points must be positive");
+    if (hgroups_.empty()) throw Error(ERR_ARG, "setup_ADMM: no constraints");
+    if (spd_solver_type != AA_SPD_LDLT && spd_solver_type != AA_SPD_LLT)
+        throw Error(ERR_ARG, "setup_ADMM: unsupported SPD solver type");
+    auto t0 = std::chrono::steady_clock::now();
+    n_ = n_points;
+    rho_ = penalty;
+    arows_.assign(n_, {});
+    for (auto& g : hgroups_) {
+        for (int v : g.idx) if (v >= n_) throw Error(ERR_ARG, "constraint references a point index >= n_points");
+        const double w = g.hard ? 1.0 : std::sqrt(g.weight);
+        const std::vector<double> D = reduction_block(g.type, g.K, w);
+        const int C = cols_of(g.type, g.K), K = g.K;
+        std::vector<double> DtD((size_t)K * K, 0.0);
+        for (int a = 0; a < K; ++a)
+            for (int b = 0; b < K; ++b) {
+                double sacc = 0;
+                for (int r = 0; r < C; ++r) sacc += D[(size_t)r * K + a] * D[(size_t)r * K + b];
+                DtD[(size_t)a * K + b] = (g.hard ? rho_ : 1.0) * sacc;
+            }
+        const int cnt = g.count();
+        for (int c = 0; c < cnt; ++c) {
+            const int* id = &g.idx[(size_t)c * K];
+            for (int a = 0; a < K; ++a)
+                for (int b = 0; b < K; ++b)
+                    if (DtD[(size_t)a * K + b] != 0.0) arows_[id[a]].push_back({id[b], DtD[(size_t)a * K + b]});
+        }
+    }
+    rhs_fixed_user_.assign(3 * (size_t)n_, 0.0);
+    for (auto& r : regs_) {
+        for (int v : r.idx) if (v >= n_) throw Error(ERR_ARG, "regularization references a point index >= n_points");
+        for (size_t a = 0; a < r.idx.size(); ++a) {
+            for (size_t b = 0; b < r.idx.size(); ++b) arows_[r.idx[a]].push_back({r.idx[b], r.coef[a] * r.coef[b]});
+            for (int d = 0; d < 3; ++d) rhs_fixed_user_[3 * (size_t)r.idx[a] + d] += r.coef[a] * r.tgt[d];
+        }
+    }
+    for (int i = 0; i < n_; ++i) {
+        auto& row = arows_[i];
+        std::sort(row.begin(), row.end(), [](const std::pair<int, double>& a, const std::pair<int, double>& b) { return a.first < b.first; });
+        size_t w = 0;
+        for (size_t k = 0; k < row.size();) {
+            size_t k2 = k;
+            double v = 0;
+            while (k2 < row.size() && row[k2].first == row[k].first) v += row[k2++].second;
+            row[w++] = {row[k].first, v};
+            k = k2;
+        }
+        row.resize(w);
+        bool diag = false;
+        for (auto& e : row) if (e.first == i && e.second > 0) diag = true;
+        if (!diag) throw Error(ERR_NUMERIC, "Error: SPD solver initialization failed (a point has no constraint)");
+    }
+    setup_done_ = true;
+    factored_ = false;
+    rt_ = aa_geom_runtime{};
+    rt_.n_points = n_;
+    rt_.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void GeomSolver::factor_and_upload(const double* init_x3) {
+    auto t0 = std::chrono::steady_clock::now();
+    drop_graph();
+    // nested-dissection order over the matrix graph, bisected on the initial point positions
+    std::vector<int> aptr(n_ + 1, 0), aj;
+    for (int i = 0; i < n_; ++i) {
+        for (auto& e : arows_[i]) if (e.first != i) aj.push_back(e.first);
+        aptr[i + 1] = (int)aj.size();
+    }
+    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, 32, DirectSolver::kTopRows);
+    int2user_ = tree.perm;
+    user2int_.assign(n_, -1);
+    for (int q = 0; q < n_; ++q) user2int_[int2user_[q]] = q;
+    CsrMatrix A;
+    A.n = n_;
+    A.ptr.assign(n_ + 1, 0);
+    for (int q = 0; q < n_; ++q) {
+        std::vector<std::pair<int, double>> r;
+        for (auto& e : arows_[int2user_[q]]) r.push_back({user2int_[e.first], e.second});
+        std::sort(r.begin(), r.end(), [](const std::pair<int, double>& a, const std::pair<int, double>& b) { return a.first < b.first; });
+        for (auto& e : r) { A.col.push_back(e.first); A.val.push_back(e.second); }
+        A.ptr[q + 1] = (int)A.col.size();
+    }
+    SupernodalFactor F;
+    try {
+        F = multifrontal_cholesky(A, tree);
+    } catch (const std::runtime_error& e) {
+        throw Error(ERR_NUMERIC, std::string("Error: SPD solver initialization failed: ") + e.what());
+    }
+    solver_.build(F, s());
+    rt_.nnz_factor = (long long)F.nnz_L;
+
+    // device constraint groups (internal point ids), z/u offsets, rhs slots
+    groups_.clear();
+    groups_.resize(hgroups_.size());
+    Zh_ = 0; slots_ = 0; red_blocks_ = 0;
+    std::vector<std::vector<int>> pslots(n_);
+    long long soft_cols = 0, ncons = 0;
+    for (size_t gi = 0; gi < hgroups_.size(); ++gi) {
+        const HostGroup& hg = hgroups_[gi];
+        DevGroup& dg = groups_[gi];
+        const int cnt = hg.count(), K = hg.K, P = n_params(hg.type), C = cols_of(hg.type, K);
+        std::vector<int> idx((size_t)K * cnt);
+        std::vector<double> prm((size_t)std::max(P, 1) * cnt, 0.0);
+        for (int e = 0; e < cnt; ++e) {
+            for (int a = 0; a < K; ++a) {
+                const int q = user2int_[hg.idx[(size_t)e * K + a]];
+                idx[(size_t)a * cnt + e] = q;
+                pslots[q].push_back((int)(slots_ + (long long)e * K + a));
+            }
+            for (int p = 0; p < P; ++p) prm[(size_t)p * cnt + e] = hg.prm[(size_t)e * P + p];
+        }
+        dg.idx.upload(idx, s());
+        dg.prm.upload(prm, s());
+        GeoGroupDev& d = dg.d;
+        d.type = hg.type; d.K = K; d.cols = C; d.hard = hg.hard; d.count = cnt;
+        d.sw = std::sqrt(hg.weight);
+        d.yscale = hg.hard ? rho_ : hg.weight;
+        d.uoff = hg.hard ? Zh_ : 0;
+        d.slot0 = slots_;
+        d.idx = dg.idx.p;
+        d.prm = dg.prm.p;
+        d.warm = nullptr;
+        d.surf = SurfDev{nullptr, nullptr, 0, 0};
+        if (hg.surf >= 0) {
+            dg.warm.alloc(cnt);
+            d.warm = dg.warm.p;
+            d.surf = surfs_[hg.surf].dev();
+        }
+        if (hg.hard) { Zh_ += 3LL * C * cnt; red_blocks_ += geo_u_blocks(cnt); }
+        else soft_cols += (long long)C * cnt;
+        slots_ += (long long)K * cnt;
+        ncons += cnt;
+    }
+    if (slots_ > 0x7fffffffLL) throw Error(ERR_ARG, "too many constraint slots for int32 indexing");
+    {
+        std::vector<int> ptr(n_ + 1, 0), sl;
+        for (int q = 0; q < n_; ++q) {
+            sl.insert(sl.end(), pslots[q].begin(), pslots[q].end());
+            ptr[q + 1] = (int)sl.size();
+        }
+        slot_ptr_.upload(ptr, s());
+        slot_idx_.upload(sl, s());
+    }
+    std::vector<double> rf(3 * (size_t)n_);
+    for (int q = 0; q < n_; ++q)
+        for (int d = 0; d < 3; ++d) rf[3 * (size_t)q + d] = rhs_fixed_user_[3 * (size_t)int2user_[q] + d];
+    rhs_fixed_.upload(rf, s());
+    const size_t nx = 3 * (size_t)n_, nu = std::max<size_t>(1, (size_t)Zh_);
+    b_.alloc(nx); y_.alloc(std::max<size_t>(3, 3 * (size_t)slots_));
+    cur_x_.alloc(nx); new_x_.alloc(nx); def_x_.alloc(nx);
+    cur_u_.alloc(nu); new_u_.alloc(nu); def_u_.alloc(nu); z_.alloc(nu);
+    red_.alloc(std::max(1, red_blocks_));
+    red_.zero(s());
+    ctrl_.alloc(1);
+    clock0_.alloc(1);
+    int khz = 0;
+    AA_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx_->device));
+    clock_khz_ = khz > 0 ? khz : 100000.0;
+    AA_HIP(hipStreamSynchronize(s()));
+    factored_ = true;
+    cur_m_ = -1;
+    rt_.hard_cols = (long long)(Zh_ / 3);
+    rt_.soft_cols = soft_cols;
+    rt_.n_constraints = ncons;
+    rt_.factor_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+
+    // algorithmic bytes per launch class (DESIGN.md "roofline accounting")
+    kstats_.clear();
+    double zb = 24.0 * n_, ub = 48.0 * n_;
+    for (auto& g : groups_) {
+        const GeoGroupDev& d = g.d;
+        const double per = 4.0 * d.K + 8.0 * n_params(d.type) + 24.0 * d.K + (d.surf.nodes ? 8.0 : 0.0) +
+                           (d.hard ? 48.0 * d.cols : 0.0);
+        zb += per * d.count;
+        if (d.hard) ub += (4.0 * d.K + 72.0 * d.cols) * d.count;
+    }
+    kstats_["z"].bytes = zb;
+    kstats_["u"].bytes = ub;
+    kstats_["rhs"].bytes = 4.0 * (n_ + 1) + 28.0 * (double)slots_ + 48.0 * n_;
+    kstats_["solve"].bytes = solver_.bytes_per_solve();
+}
+
+void GeomSolver::prepare_m(int m) {
+    if (m == cur_m_) return;
+    drop_graph();
+    const long long dim = Zh_ + 3LL * n_;
+    if (m > 0) {
+        aa_cur_.alloc(dim);
+        aa_dF_.alloc((size_t)m * dim); aa_dF_.zero(s());
+        aa_dG_.alloc((size_t)m * dim); aa_dG_.zero(s());
+        aa_blocks_ = aa_reduce_blocks(dim);
+        const int mm = m <= 8 ? 8 : (m <= 16 ? 16 : 32);
+        aa_red_.alloc((size_t)aa_blocks_ * (2 + 2 * mm));
+        kstats_["aa"].bytes = 8.0 * dim * (2.0 * std::min(m, 32) + 8.0);
+    } else {
+        aa_cur_.release(); aa_dF_.release(); aa_dG_.release(); aa_red_.release();
+        aa_blocks_ = 0;
+        kstats_["aa"].bytes = 16.0 * dim * 2;
+    }
+    cur_m_ = m;
+}
+
+void GeomSolver::prologue(const double* init_x3, int max_iter, int m, int cap) {
+    std::vector<double> x(3 * (size_t)n_);
+    for (int q = 0; q < n_; ++q)
+        for (int d = 0; d < 3; ++d) x[3 * (size_t)q + d] = init_x3[3 * (size_t)int2user_[q] + d];
+    cur_x_.upload(x, s());
+    def_x_.upload(x, s());
+    cur_u_.zero(s());
+    def_u_.zero(s());
+    if (m > 0) {
+        AA_HIP(hipMemsetAsync(aa_cur_.p, 0, (size_t)Zh_ * 8, s()));
+        AA_HIP(hipMemcpyAsync(aa_cur_.p + Zh_, cur_x_.p, x.size() * 8, hipMemcpyDeviceToDevice, s()));
+    }
+    for (auto& g : groups_)
+        if (g.d.warm) AA_HIP(hipMemsetAsync(g.d.warm, 0xff, (size_t)g.d.count * sizeof(int), s()));
+    cap = std::max(1, cap);
+    if (cap > hist_cap_) {
+        hist_cap_ = cap;
+        hist_comb_.alloc(cap);
+        hist_clock_.alloc(cap);
+    }
+    Ctrl c;
+    std::memset(&c, 0, sizeof(c));
+    c.prev_prim = DBL_MAX;
+    c.cap = hist_cap_;
+    c.max_iter = max_iter;
+    c.aa_m = m;
+    c.aa_active = m > 0 ? 1 : 0;
+    AA_HIP(hipMemcpyAsync(ctrl_.p, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s()));
+    launch_geo_start(ctrl_.p, clock0_.p, s());
+}
+
+void GeomSolver::ev_mark(const char* name) {
+    if (!instrument_) return;
+    hipEvent_t e;
+    AA_HIP(hipEventCreate(&e));
+    AA_HIP(hipEventRecord(e, s()));
+    kstats_[name].ev.push_back(e);
+}
+
+// one pass of the while-loop body of solve_ADMM (ALMGeometrySolver.h:197-267)
+void GeomSolver::enqueue_iteration(int m) {
+    Ctrl* c = ctrl_.p;
+    const long long nx = 3LL * n_;
+    ev_mark("z");
+    for (auto& g : groups_) launch_geo_z(g.d, cur_x_.p, cur_u_.p, z_.p, y_.p, c, s());   // ADMM_z_update
+    ev_mark("z");
+    ev_mark("rhs");
+    launch_geo_rhs(n_, slot_ptr_.p, slot_idx_.p, y_.p, rhs_fixed_.p, b_.p, c, s());     // ADMM_x_update rhs
+    ev_mark("rhs");
+    ev_mark("solve");
+    solver_.solve(b_.p, new_x_.p, c, 0, s());                                           // SPD_solver_->solve
+    ev_mark("solve");
+    ev_mark("u");
+    int off = 0;
+    for (auto& g : groups_) {                                                            // ADMM_u_update + residual
+        if (!g.d.hard) continue;
+        launch_geo_u(g.d, new_x_.p, cur_x_.p, z_.p, cur_u_.p, new_u_.p, c, red_.p, off, s());
+        off += geo_u_blocks(g.d.count);
+    }
+    ev_mark("u");
+    ev_mark("aa");
+    launch_geo_control(c, red_.p, red_blocks_, m > 0, hist_comb_.p, hist_clock_.p, s());
+    if (m > 0) {
+        launch_geo_restore(cur_u_.p, cur_x_.p, aa_cur_.p, def_u_.p, def_x_.p, Zh_, nx, c, s());
+        Seg2 G{new_u_.p, Zh_, new_x_.p, nx};
+        Seg2 cp{def_u_.p, Zh_, def_x_.p, nx};
+        Seg2 out{cur_u_.p, Zh_, cur_x_.p, nx};
+        launch_aa_reduce(G, aa_cur_.p, Zh_ + nx, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, cp, m, s());
+        launch_aa_solve(c, aa_red_.p, aa_blocks_, m, s());
+        launch_aa_mix(G, aa_cur_.p, Zh_ + nx, aa_dF_.p, aa_dG_.p, c, out, m, s());
+    } else {
+        if (Zh_) launch_copy(cur_u_.p, new_u_.p, Zh_, c, 0, s());
+        launch_copy(cur_x_.p, new_x_.p, nx, c, 0, s());
+    }
+    ev_mark("aa");
+}
+
+void GeomSolver::fetch_results() {
+    Ctrl c;
+    AA_HIP(hipMemcpyAsync(&c, ctrl_.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s()));
+    AA_HIP(hipStreamSynchronize(s()));
+    const int nrec = std::min(c.nrec, hist_cap_);
+    h_comb_.resize(nrec);
+    h_time_.resize(nrec);
+    std::vector<unsigned long long> clk(nrec);
+    unsigned long long c0 = 0;
+    if (nrec) {
+        AA_HIP(hipMemcpy(h_comb_.data(), hist_comb_.p, nrec * 8, hipMemcpyDeviceToHost));
+        AA_HIP(hipMemcpy(clk.data(), hist_clock_.p, nrec * 8, hipMemcpyDeviceToHost));
+    }
+    AA_HIP(hipMemcpy(&c0, clock0_.p, 8, hipMemcpyDeviceToHost));
+    for (int k = 0; k < nrec; ++k) h_time_[k] = (double)(clk[k] - c0) / (clock_khz_ * 1e3);
+    rt_.iterations = c.iters_run;
+    rt_.accepted = c.nrec;
+    rt_.rejects = c.nrej;
+}
+
+// solve_ADMM (ALMGeometrySolver.h:163-283). rel_residual_eps is accepted for API parity: the
+// reference computes its threshold but the stopping test is commented out (:258-263).
+void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_iter, int m) {
+    (void)rel_residual_eps;
+    if (!setup_done_) throw Error(ERR_STATE, "Error: solver not initialized yet");
+    if (!init_x3) throw Error(ERR_ARG, "solve_ADMM: null init_x");
+    if (m < 0 || m > kMaxM) throw Error(ERR_ARG, "solve_ADMM: Anderson window must be in [0, 32]");
+    if (max_iter < 0) throw Error(ERR_ARG, "solve_ADMM: max_iter < 0");
+    auto t0 = std::chrono::steady_clock::now();
+    if (!factored_) factor_and_upload(init_x3);
+    prepare_m(m);
+    last_init_.assign(init_x3, init_x3 + 3 * (size_t)n_);
+    prologue(init_x3, max_iter, m, max_iter);
+    const int target = std::max(1, max_iter);
+    const int chunk = std::min(target, 64);
+    const bool use_graph = !(std::getenv("AA_ADMM_NO_GRAPH") && std::getenv("AA_ADMM_NO_GRAPH")[0] == '1');
+    auto run_chunk = [&]() {
+        if (use_graph) {
+            if (!gexec_ || graph_chunk_ != chunk || graph_m_ != m) {
+                drop_graph();
+                AA_HIP(hipStreamBeginCapture(s(), hipStreamCaptureModeThreadLocal));
+                for (int i = 0; i < chunk; ++i) enqueue_iteration(m);
+                AA_HIP(hipStreamEndCapture(s(), &graph_));
+                AA_HIP(hipGraphInstantiate(&gexec_, graph_, nullptr, nullptr, 0));
+                graph_chunk_ = chunk;
+                graph_m_ = m;
+            }
+            AA_HIP(hipGraphLaunch(gexec_, s()));
+        } else {
+            for (int i = 0; i < chunk; ++i) enqueue_iteration(m);
+        }
+    };
+    // no rejection: exactly ceil(target / chunk) chunks; each rejection adds one x-update
+    // (a rejected iteration is always followed by an accepted one, so <= 2 target + 1 passes)
+    const int first = (target + chunk - 1) / chunk;
+    for (int i = 0; i < first; ++i) run_chunk();
+    int passes = first * chunk;
+    for (;;) {
+        Ctrl c;
+        AA_HIP(hipMemcpyAsync(&c, ctrl_.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s()));
+        AA_HIP(hipStreamSynchronize(s()));
+        if (c.done) break;
+        if (passes > 2 * target + 2 * chunk) throw Error(ERR_NUMERIC, "solve_ADMM: the loop did not terminate");
+        run_chunk();
+        passes += chunk;
+    }
+    fetch_results();
+    have_solution_ = true;
+    rt_.solve_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// get_solution (ALMGeometrySolver.h:280-282) = default_x_: the x of the last accepted iteration,
+// which is the last x-update since the loop always ends on an acceptance
+void GeomSolver::get_solution(double* x3) const {
+    if (!have_solution_) throw Error(ERR_STATE, "get_solution before solve_ADMM");
+    std::vector<double> x(3 * (size_t)n_);
+    AA_HIP(hipMemcpy(x.data(), new_x_.p, x.size() * 8, hipMemcpyDeviceToHost));
+    for (int q = 0; q < n_; ++q)
+        for (int d = 0; d < 3; ++d) x3[3 * (size_t)int2user_[q] + d] = x[3 * (size_t)q + d];
+}
+
+int GeomSolver::history(double* comb, double* time_s, int cap) const {
+    const int n = std::min(cap, (int)h_comb_.size());
+    for (int i = 0; i < n; ++i) {
+        if (comb) comb[i] = h_comb_[i];
+        if (time_s) time_s[i] = h_time_[i];
+    }
+    return (int)h_comb_.size();
+}
+
+void GeomSolver::closest_points(int surface, const double* p3, int n, double* out3) {
+    if (surface < 0 || surface >= (int)surfs_.size()) throw Error(ERR_ARG, "closest_points: unknown surface");
+    if (n <= 0) return;
+    DevBuf<double> p, c(3 * (size_t)n);
+    p.upload(p3, 3 * (size_t)n, s());
+    launch_closest(surfs_[surface].dev(), p.p, c.p, n, s());
+    AA_HIP(hipMemcpyAsync(out3, c.p, 24 * (size_t)n, hipMemcpyDeviceToHost, s()));
+    AA_HIP(hipStreamSynchronize(s()));
+}
+
+double GeomSolver::bench_iterations(int iters) {
+    if (!setup_done_ || !factored_ || cur_m_ < 0) throw Error(ERR_STATE, "bench before solve_ADMM");
+    for (auto& kv : kstats_) { for (auto e : kv.second.ev) (void)hipEventDestroy(e); kv.second.ev.clear(); }
+    prologue(last_init_.data(), 1 << 30, cur_m_, iters + 1);
+    AA_HIP(hipStreamSynchronize(s()));
+    instrument_ = true;
+    hipEvent_t e0, e1;
+    AA_HIP(hipEventCreate(&e0)); AA_HIP(hipEventCreate(&e1));
+    AA_HIP(hipEventRecord(e0, s()));
+    for (int it = 0; it < iters; ++it) enqueue_iteration(cur_m_);
+    AA_HIP(hipEventRecord(e1, s()));
+    AA_HIP(hipEventSynchronize(e1));
+    instrument_ = false;
+    float ms = 0;
+    AA_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+    for (auto& kv : kstats_) {
+        KStat& k = kv.second;
+        k.total_ms = 0; k.launches = 0;
+        for (size_t i = 0; i + 1 < k.ev.size(); i += 2) {
+            float t = 0;
+            AA_HIP(hipEventElapsedTime(&t, k.ev[i], k.ev[i + 1]));
+            k.total_ms += t; k.launches += 1;
+        }
+    }
+    fetch_results();
+    return ms;
+}
+
+bool GeomSolver::kernel_stats(const std::string& name, double* avg_ms, double* bytes, int* launches) const {
+    auto it = kstats_.find(name);
+    if (it == kstats_.end()) return false;
+    const KStat& k = it->second;
+    if (avg_ms) *avg_ms = k.launches ? k.total_ms / k.launches : 0.0;
+    if (bytes) *bytes = k.bytes;
+    if (launches) *launches = k.launches;
+    return true;
+}
+
+}  // namespace aa

@@ -1,0 +1,114 @@
+// Host orchestration of the Geometry (ALM) hot path on one MI355X: the reference's
+// ALMGeometrySolver<3> (Geometry/ALMGeometrySolver.h) with its Constraint<3> plugins
+// (Geometry/Constraint.h), LinearRegularization (Geometry/LinearRegularization.h) and the
+// AndersonAcceleration on (u, x) (Geometry/AndersonAcceleration.h).
+#pragma once
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/aa_admm.h"
+#include "common.hpp"
+#include "direct_solve.hpp"
+#include "elastic.hpp"
+#include "geom_kernels.hpp"
+
+namespace aa {
+
+class GeomSolver {
+public:
+    explicit GeomSolver(Context* ctx) : ctx_(ctx) {}
+    ~GeomSolver();
+
+    int add_ref_surface(const double* V3, int nv, const int* F3, int nf);
+    void add_constraints(int hard, int type, const int* idx, int k, int count, double weight, const double* params);
+    void add_laplacian(const int* idx, const double* coefs, int k, double weight, const double* ref_points3);
+    void add_closeness(int idx, double weight, const double* target3);
+    void setup(int n_points, double penalty, int spd_solver_type);
+    void solve(const double* init_x3, double rel_residual_eps, int max_iter, int anderson_m);
+    void get_solution(double* x3) const;
+    int history(double* comb, double* time_s, int cap) const;
+    aa_geom_runtime runtime() const { return rt_; }
+    void closest_points(int surface, const double* p3, int n, double* out3);
+
+    double bench_iterations(int iters);
+    bool kernel_stats(const std::string& name, double* avg_ms, double* bytes, int* launches) const;
+
+private:
+    struct HostGroup {
+        int hard, type, K, surf;
+        double weight;
+        std::vector<int> idx;      // [count][K] user point ids
+        std::vector<double> prm;   // [count][P]
+        int count() const { return (int)(idx.size() / K); }
+    };
+    struct DevGroup {
+        DevBuf<int> idx, warm;
+        DevBuf<double> prm;
+        GeoGroupDev d{};
+    };
+    struct Surface {
+        std::vector<BvhNode> nodes;
+        std::vector<BvhTri> tris;
+        DevBuf<BvhNode> dnodes;
+        DevBuf<BvhTri> dtris;
+        SurfDev dev() const { return SurfDev{dnodes.p, dtris.p, (int)nodes.size(), (int)tris.size()}; }
+    };
+    struct Reg { std::vector<int> idx; std::vector<double> coef; double tgt[3]; };
+
+    Context* ctx_;
+    hipStream_t s() const { return ctx_->stream; }
+
+    // host model
+    std::vector<HostGroup> hgroups_;
+    std::map<std::tuple<int, int, int, double, int>, int> group_of_;
+    std::vector<Surface> surfs_;
+    std::vector<Reg> regs_;
+    int n_ = 0;
+    double rho_ = 1.0;
+    bool setup_done_ = false, factored_ = false;
+
+    // internal numbering: points in nested-dissection order (fixed at the first solve, which
+    // is the first time point positions are known: ALMGeometrySolver::solve_ADMM(init_x, ...))
+    std::vector<int> user2int_, int2user_;
+    std::vector<std::vector<std::pair<int, double>>> arows_;   // assembled global matrix (user ids)
+    std::vector<double> rhs_fixed_user_;
+    long long Zh_ = 0, slots_ = 0;
+    int red_blocks_ = 0;
+
+    // device
+    std::vector<DevGroup> groups_;
+    DirectSolver solver_;
+    DevBuf<int> slot_ptr_, slot_idx_;
+    DevBuf<double> rhs_fixed_, b_, y_;
+    DevBuf<double> cur_x_, new_x_, def_x_, cur_u_, new_u_, def_u_, z_;
+    DevBuf<double> aa_cur_, aa_dF_, aa_dG_, aa_red_, red_;
+    DevBuf<Ctrl> ctrl_;
+    DevBuf<double> hist_comb_;
+    DevBuf<unsigned long long> hist_clock_, clock0_;
+    int aa_blocks_ = 0, cur_m_ = -1, hist_cap_ = 0;
+    bool have_solution_ = false;
+    std::vector<double> last_init_;
+    std::vector<double> h_comb_, h_time_;
+    aa_geom_runtime rt_{};
+    double clock_khz_ = 0;
+
+    hipGraph_t graph_ = nullptr;
+    hipGraphExec_t gexec_ = nullptr;
+    int graph_chunk_ = 0, graph_m_ = -1;
+    void drop_graph();
+
+    bool instrument_ = false;
+    struct KStat { std::vector<hipEvent_t> ev; double bytes = 0; double total_ms = 0; int launches = 0; };
+    std::map<std::string, KStat> kstats_;
+    void ev_mark(const char* name);
+
+    void factor_and_upload(const double* init_x3);
+    void prepare_m(int m);
+    void prologue(const double* init_x3, int max_iter, int m, int cap);
+    void enqueue_iteration(int m);
+    void fetch_results();
+};
+
+}  // namespace aa

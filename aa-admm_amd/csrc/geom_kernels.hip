@@ -1,0 +1,503 @@
+// HIP kernels of the Geometry (ALM) hot path (gfx950, wave64, fp64).
+//
+// One thread per constraint: the K point positions are gathered (24 B each, the point array
+// stays L2/MALL resident), transformed (mean-centring / subtract-first / identity), projected
+// in registers, and the thread writes its z columns (SoA, coalesced) and its K rows of the
+// global right-hand side (slot rows, gathered per point by a fixed-order CSR pass: no atomics,
+// deterministic). Projections (Geometry/Constraint.h):
+//   plane  -- best-fit plane through the (mean-centred) columns: one-sided Jacobi on the three
+//             coordinate rows (relative accuracy, same left singular vectors as the reference's
+//             Eigen JacobiSVD), normal = the row rotation of the smallest row norm;
+//   angle  -- the closed-form rotation of Constraint.h:243-291;
+//   edge   -- v |v|^-1 L;   closeness -- identity (Constraint.h:319-322 never overrides);
+//   closest point on a reference surface -- stack traversal of a depth-first BVH with exact
+//             box pruning, warm-started from the previous iteration's triangle.
+#include "common.hpp"
+#include "geom_kernels.hpp"
+
+namespace aa {
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ double block_sum(double v, double* sm) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) sm[wid] = v;
+    __syncthreads();
+    double r = 0;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r += sm[i];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ bool gated(const Ctrl* c) { return c && c->done; }
+
+// ------------------------------------------------------------------ transforms (Constraint.h:73-94)
+// out: 3*cols values, column-major (column c at out[3c..3c+2])
+template <int T, int K>
+__device__ __forceinline__ void transform(const GeoGroupDev& g, int e, const double* __restrict__ x, double* out) {
+    double p[3 * K];
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        const int v = g.idx[(size_t)a * g.count + e];
+        p[3 * a] = x[3 * (size_t)v]; p[3 * a + 1] = x[3 * (size_t)v + 1]; p[3 * a + 2] = x[3 * (size_t)v + 2];
+    }
+    if constexpr (T == GEO_ANGLE || T == GEO_EDGE) {          // SUBTRACT_FIRST
+#pragma unroll
+        for (int a = 1; a < K; ++a)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) out[3 * (a - 1) + d] = p[3 * a + d] - p[d];
+    } else if constexpr (T == GEO_PLANE) {                     // MEAN_CENTERING
+        double m[3] = {0, 0, 0};
+#pragma unroll
+        for (int a = 0; a < K; ++a)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) m[d] += p[3 * a + d];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) m[d] /= K;
+#pragma unroll
+        for (int a = 0; a < K; ++a)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) out[3 * a + d] = p[3 * a + d] - m[d];
+    } else {                                                   // IDENTITY
+#pragma unroll
+        for (int i = 0; i < 3 * K; ++i) out[i] = p[i];
+    }
+}
+
+// rhs slot rows: y_a = s * (T^T q)_a
+template <int T, int K>
+__device__ __forceinline__ void write_slots(const GeoGroupDev& g, int e, const double* q, double s, double* __restrict__ y) {
+    double* yr = y + 3 * (size_t)(g.slot0 + (long long)e * K);
+    if constexpr (T == GEO_ANGLE || T == GEO_EDGE) {
+        double f[3] = {0, 0, 0};
+#pragma unroll
+        for (int a = 1; a < K; ++a)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { f[d] -= q[3 * (a - 1) + d]; yr[3 * a + d] = s * q[3 * (a - 1) + d]; }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) yr[d] = s * f[d];
+    } else if constexpr (T == GEO_PLANE) {
+        double m[3] = {0, 0, 0};
+#pragma unroll
+        for (int a = 0; a < K; ++a)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) m[d] += q[3 * a + d];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) m[d] /= K;
+#pragma unroll
+        for (int a = 0; a < K; ++a)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) yr[3 * a + d] = s * (q[3 * a + d] - m[d]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 3 * K; ++i) yr[i] = s * q[i];
+    }
+}
+
+// ------------------------------------------------------------------ projections
+// best-fit plane normal of the columns of P (3 x K): one-sided Jacobi over the coordinate rows
+template <int K>
+__device__ void plane_project(double* v) {
+    double R[3][K], W[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int a = 0; a < K; ++a) R[d][a] = v[3 * a + d];
+    for (int sweep = 0; sweep < 30; ++sweep) {
+        bool rotated = false;
+#pragma unroll
+        for (int pr = 0; pr < 3; ++pr) {
+            const int p = pr == 2 ? 1 : 0, q = pr == 0 ? 1 : 2;
+            double a = 0, b = 0, gg = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) { a += R[p][k] * R[p][k]; b += R[q][k] * R[q][k]; gg += R[p][k] * R[q][k]; }
+            if (fabs(gg) > 1e-15 * sqrt(a * b) && gg != 0.0) {
+                rotated = true;
+                const double zeta = (b - a) / (2.0 * gg);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const double rp = R[p][k], rq = R[q][k];
+                    R[p][k] = c * rp - s * rq;
+                    R[q][k] = s * rp + c * rq;
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double wp = W[p][k], wq = W[q][k];
+                    W[p][k] = c * wp - s * wq;
+                    W[q][k] = s * wp + c * wq;
+                }
+            }
+        }
+        if (!rotated) break;
+    }
+    double nr[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        double s = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) s += R[d][k] * R[d][k];
+        nr[d] = s;
+    }
+    int i = 0;
+    if (nr[1] < nr[i]) i = 1;
+    if (nr[2] < nr[i]) i = 2;
+    double n0 = W[i][0], n1 = W[i][1], n2 = W[i][2];
+    const double l = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+    if (l > 0) { n0 /= l; n1 /= l; n2 /= l; }
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        const double dp = n0 * v[3 * a] + n1 * v[3 * a + 1] + n2 * v[3 * a + 2];
+        v[3 * a] -= n0 * dp; v[3 * a + 1] -= n1 * dp; v[3 * a + 2] -= n2 * dp;
+    }
+}
+
+// AngleConstraint::project_impl (Constraint.h:243-291), v = (v1, v2) in place
+__device__ void angle_project(double* v, double min_r, double max_r) {
+    const double min_a = fmax(0.0, min_r), max_a = fmin(M_PI, max_r);
+    const double min_cos = fmin(fmax(cos(min_a), -1.0), 1.0), max_cos = fmin(fmax(cos(max_a), -1.0), 1.0);
+    const double v1s = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const double v2s = v[3] * v[3] + v[4] * v[4] + v[5] * v[5];
+    const double v1n = sqrt(v1s), v2n = sqrt(v2s);
+    double u1[3] = {v[0], v[1], v[2]}, u2[3] = {v[3], v[4], v[5]};
+    if (v1s > 0) { const double r = 1.0 / sqrt(v1s); u1[0] *= r; u1[1] *= r; u1[2] *= r; }
+    if (v2s > 0) { const double r = 1.0 / sqrt(v2s); u2[0] *= r; u2[1] *= r; u2[2] *= r; }
+    const double cg = fmin(fmax(u1[0] * u2[0] + u1[1] * u2[1] + u1[2] * u2[2], -1.0), 1.0);
+    if (!((1.0 - fabs(cg) > 1e-14) && (cg > min_cos || cg < max_cos))) return;
+    const double gamma = acos(cg);
+    double eta = cg > min_cos ? (min_a - gamma) : (gamma - max_a);
+    eta = fmax(eta, 0.0);
+    double theta = 0.5 * atan2(v2s * sin(2 * eta), v1s + v2s * cos(2 * eta));
+    theta = fmax(0.0, fmin(eta, theta));
+    const double phi = eta - theta;
+    double w3[3], w4[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) { w3[d] = u2[d] - u1[d] * cg; w4[d] = u1[d] - u2[d] * cg; }
+    const double l3 = w3[0] * w3[0] + w3[1] * w3[1] + w3[2] * w3[2];
+    const double l4 = w4[0] * w4[0] + w4[1] * w4[1] + w4[2] * w4[2];
+    const double s3 = (l3 > 0 ? 1.0 / sqrt(l3) : 1.0) * (cg > min_cos ? -1.0 : 1.0);
+    const double s4 = (l4 > 0 ? 1.0 / sqrt(l4) : 1.0) * (cg > min_cos ? -1.0 : 1.0);
+    const double ct = cos(theta), st = sin(theta), cp = cos(phi), sp = sin(phi);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        v[d] = (u1[d] * ct + w3[d] * s3 * st) * (v1n * ct);
+        v[3 + d] = (u2[d] * cp + w4[d] * s4 * sp) * (v2n * cp);
+    }
+}
+
+// Ericson closest point on a triangle (igl point_simplex_squared_distance.cpp:40-108)
+__device__ __forceinline__ void closest_on_tri(const double* t, double px, double py, double pz, double& cx,
+                                               double& cy, double& cz) {
+    const double ax = t[0], ay = t[1], az = t[2], bx = t[3], by = t[4], bz = t[5], qx = t[6], qy = t[7], qz = t[8];
+    const double abx = bx - ax, aby = by - ay, abz = bz - az, acx = qx - ax, acy = qy - ay, acz = qz - az;
+    const double apx = px - ax, apy = py - ay, apz = pz - az;
+    const double d1 = abx * apx + aby * apy + abz * apz, d2 = acx * apx + acy * apy + acz * apz;
+    if (d1 <= 0.0 && d2 <= 0.0) { cx = ax; cy = ay; cz = az; return; }
+    const double bpx = px - bx, bpy = py - by, bpz = pz - bz;
+    const double d3 = abx * bpx + aby * bpy + abz * bpz, d4 = acx * bpx + acy * bpy + acz * bpz;
+    if (d3 >= 0.0 && d4 <= d3) { cx = bx; cy = by; cz = bz; return; }
+    const double vc = d1 * d4 - d3 * d2;
+    if (!(ax == bx && ay == by && az == bz) && vc <= 0.0 && d1 >= 0.0 && d3 <= 0.0) {
+        const double v = d1 / (d1 - d3);
+        cx = ax + v * abx; cy = ay + v * aby; cz = az + v * abz; return;
+    }
+    const double cpx = px - qx, cpy = py - qy, cpz = pz - qz;
+    const double d5 = abx * cpx + aby * cpy + abz * cpz, d6 = acx * cpx + acy * cpy + acz * cpz;
+    if (d6 >= 0.0 && d5 <= d6) { cx = qx; cy = qy; cz = qz; return; }
+    const double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {
+        const double w = d2 / (d2 - d6);
+        cx = ax + w * acx; cy = ay + w * acy; cz = az + w * acz; return;
+    }
+    const double va = d3 * d6 - d5 * d4;
+    if (va <= 0.0 && (d4 - d3) >= 0.0 && (d5 - d6) >= 0.0) {
+        const double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        cx = bx + w * (qx - bx); cy = by + w * (qy - by); cz = bz + w * (qz - bz); return;
+    }
+    const double denom = 1.0 / (va + vb + vc);
+    const double v = vb * denom, w = vc * denom;
+    cx = ax + abx * v + acx * w; cy = ay + aby * v + acy * w; cz = az + abz * v + acz * w;
+}
+
+__device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py, double pz) {
+    const double tx = px < nd.lo[0] ? nd.lo[0] - px : (px > nd.hi[0] ? px - nd.hi[0] : 0.0);
+    const double ty = py < nd.lo[1] ? nd.lo[1] - py : (py > nd.hi[1] ? py - nd.hi[1] : 0.0);
+    const double tz = pz < nd.lo[2] ? nd.lo[2] - pz : (pz > nd.hi[2] ? pz - nd.hi[2] : 0.0);
+    return tx * tx + ty * ty + tz * tz;
+}
+
+// exact closest point on the surface; `warm` (a triangle id or -1) seeds the upper bound
+__device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, int warm, double& cx, double& cy,
+                           double& cz) {
+    constexpr int kStack = 64;
+    double best = INFINITY;
+    int best_t = -1;
+    cx = px; cy = py; cz = pz;
+    if (warm >= 0 && warm < S.n_tris) {
+        double qx, qy, qz;
+        closest_on_tri(S.tris[warm].v, px, py, pz, qx, qy, qz);
+        best = (px - qx) * (px - qx) + (py - qy) * (py - qy) + (pz - qz) * (pz - qz);
+        best_t = warm; cx = qx; cy = qy; cz = qz;
+    }
+    if (S.n_nodes == 0) return best_t;
+    int st_node[kStack];
+    double st_d[kStack];
+    int sp = 0;
+    int node = 0;
+    double nd2 = box_d2(S.nodes[0], px, py, pz);
+    for (;;) {
+        if (nd2 < best) {
+            const BvhNode nd = S.nodes[node];
+            if (nd.b < 0) {
+                for (int t = nd.a; t < nd.a - nd.b; ++t) {
+                    if (t == warm) continue;
+                    double qx, qy, qz;
+                    closest_on_tri(S.tris[t].v, px, py, pz, qx, qy, qz);
+                    const double d2 = (px - qx) * (px - qx) + (py - qy) * (py - qy) + (pz - qz) * (pz - qz);
+                    if (d2 < best) { best = d2; best_t = t; cx = qx; cy = qy; cz = qz; }
+                }
+            } else {
+                const int l = node + 1, r = nd.a;
+                const double dl = box_d2(S.nodes[l], px, py, pz), dr = box_d2(S.nodes[r], px, py, pz);
+                const bool left_first = dl <= dr;
+                const int nn = left_first ? l : r, ff = left_first ? r : l;
+                const double dn = left_first ? dl : dr, df = left_first ? dr : dl;
+                if (df < best && sp < kStack) { st_node[sp] = ff; st_d[sp] = df; ++sp; }
+                node = nn; nd2 = dn;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        node = st_node[sp];
+        nd2 = st_d[sp];
+    }
+    return best_t;
+}
+
+// ------------------------------------------------------------------ z step
+template <int T, int K>
+__global__ __launch_bounds__(kBlock) void k_geo_z(GeoGroupDev g, const double* __restrict__ x,
+                                                  const double* __restrict__ u, double* __restrict__ z,
+                                                  double* __restrict__ y, const Ctrl* ctrl) {
+    if (gated(ctrl)) return;
+    constexpr int C = (T == GEO_ANGLE || T == GEO_EDGE) ? K - 1 : K;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= g.count) return;
+    double v[3 * C], uu[3 * C];
+    transform<T, K>(g, e, x, v);
+    if (g.hard) {
+#pragma unroll
+        for (int i = 0; i < 3 * C; ++i) { uu[i] = u[g.uoff + (size_t)i * g.count + e]; v[i] += uu[i]; }
+    }
+    if constexpr (T == GEO_PLANE) {
+        plane_project<K>(v);
+    } else if constexpr (T == GEO_ANGLE) {
+        angle_project(v, g.prm[e], g.prm[(size_t)g.count + e]);
+    } else if constexpr (T == GEO_EDGE) {
+        const double L = g.prm[e];
+        const double s2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+        const double r = s2 > 0 ? L / sqrt(s2) : L;
+        v[0] *= r; v[1] *= r; v[2] *= r;
+    } else if constexpr (T == GEO_POINT_TO_REF || T == GEO_REF_SURFACE) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            double qx, qy, qz;
+            const int w0 = g.warm ? g.warm[e] : -1;
+            const int t = bvh_closest(g.surf, v[3 * c], v[3 * c + 1], v[3 * c + 2], w0, qx, qy, qz);
+            if (g.warm) g.warm[e] = t;
+            v[3 * c] = qx; v[3 * c + 1] = qy; v[3 * c + 2] = qz;
+        }
+    }   // CLOSENESS: identity
+    if (g.hard) {
+#pragma unroll
+        for (int i = 0; i < 3 * C; ++i) { z[g.uoff + (size_t)i * g.count + e] = v[i]; uu[i] = v[i] - uu[i]; }
+        write_slots<T, K>(g, e, uu, g.yscale, y);
+    } else {
+        write_slots<T, K>(g, e, v, g.yscale, y);
+    }
+}
+
+// ------------------------------------------------------------------ dual update + residual partials
+template <int T, int K>
+__global__ __launch_bounds__(kBlock) void k_geo_u(GeoGroupDev g, const double* __restrict__ xnew,
+                                                  const double* __restrict__ xcur, const double* __restrict__ z,
+                                                  const double* __restrict__ u, double* __restrict__ unew,
+                                                  const Ctrl* ctrl, double* red, int red_off) {
+    if (gated(ctrl)) return;
+    __shared__ double sm[kBlock / 64];
+    constexpr int C = (T == GEO_ANGLE || T == GEO_EDGE) ? K - 1 : K;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double part = 0;
+    if (e < g.count) {
+        double dn[3 * C], dp[3 * C];
+        transform<T, K>(g, e, xnew, dn);
+        transform<T, K>(g, e, xcur, dp);
+#pragma unroll
+        for (int i = 0; i < 3 * C; ++i) {
+            const size_t o = g.uoff + (size_t)i * g.count + e;
+            const double zz = z[o];
+            const double r = dn[i] - zz, d = dn[i] - dp[i];
+            part += r * r + d * d;
+            unew[o] = u[o] + r;
+        }
+    }
+    const double s = block_sum(part, sm);
+    if (threadIdx.x == 0) red[red_off + blockIdx.x] = s;
+}
+
+// ------------------------------------------------------------------ rhs gather
+__global__ __launch_bounds__(kBlock) void k_geo_rhs(int n, const int* __restrict__ ptr, const int* __restrict__ slots,
+                                                    const double* __restrict__ y, const double* __restrict__ rf,
+                                                    double* __restrict__ b, const Ctrl* ctrl) {
+    if (gated(ctrl)) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s0 = rf[3 * (size_t)i], s1 = rf[3 * (size_t)i + 1], s2 = rf[3 * (size_t)i + 2];
+    for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
+        const size_t r = 3 * (size_t)slots[k];
+        s0 += y[r]; s1 += y[r + 1]; s2 += y[r + 2];
+    }
+    b[3 * (size_t)i] = s0; b[3 * (size_t)i + 1] = s1; b[3 * (size_t)i + 2] = s2;
+}
+
+// ------------------------------------------------------------------ control
+__global__ __launch_bounds__(kBlock) void k_geo_control(Ctrl* ctrl, const double* red, int nb, int accel,
+                                                        double* hist_comb, unsigned long long* hist_clock) {
+    if (ctrl->done) return;
+    __shared__ double sm[kBlock / 64];
+    double a = 0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) a += red[i];
+    a = block_sum(a, sm);
+    if (threadIdx.x != 0) return;
+    const double comb = a;
+    ctrl->comb = comb;
+    ctrl->iters_run += 1;
+    const bool accept = !accel || ctrl->alm_reset || comb < ctrl->prev_prim;
+    if (accept) {
+        const int k = ctrl->nrec;
+        if (k < ctrl->cap) { hist_comb[k] = comb; hist_clock[k] = wall_clock64(); }
+        ctrl->nrec = k + 1;
+        ctrl->prev_prim = comb;
+        ctrl->alm_reset = 0;
+        ctrl->reject = 0;
+        ctrl->aa_skip = 0;
+        if (ctrl->nrec >= ctrl->max_iter) ctrl->done = 1;
+    } else {
+        ctrl->reject = 1;
+        ctrl->nrej += 1;
+        ctrl->alm_reset = 1;
+        ctrl->aa_iter = 0;   // accelerator->reset (AndersonAcceleration.h:73-91)
+        ctrl->aa_col = 0;
+        ctrl->aa_skip = 1;
+    }
+}
+
+__global__ void k_geo_start(Ctrl* ctrl, unsigned long long* clock0) {
+    (void)ctrl;
+    *clock0 = wall_clock64();
+}
+
+__global__ __launch_bounds__(kBlock) void k_geo_restore(double* __restrict__ cu, double* __restrict__ cx,
+                                                        double* __restrict__ aacur, const double* __restrict__ du,
+                                                        const double* __restrict__ dx, long long nu, long long nx,
+                                                        const Ctrl* ctrl) {
+    if (ctrl->done || !ctrl->reject) return;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nu + nx; i += (long long)gridDim.x * blockDim.x) {
+        if (i < nu) { const double v = du[i]; cu[i] = v; if (aacur) aacur[i] = v; }
+        else { const double v = dx[i - nu]; cx[i - nu] = v; if (aacur) aacur[i] = v; }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_closest(SurfDev S, const double* __restrict__ p, double* __restrict__ c, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double qx, qy, qz;
+    bvh_closest(S, p[3 * (size_t)i], p[3 * (size_t)i + 1], p[3 * (size_t)i + 2], -1, qx, qy, qz);
+    c[3 * (size_t)i] = qx; c[3 * (size_t)i + 1] = qy; c[3 * (size_t)i + 2] = qz;
+}
+
+inline int grid_for(long long n) { long long b = (n + kBlock - 1) / kBlock; return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048); }
+
+}  // namespace
+
+// ============================================================================ launchers
+#define GEO_DISPATCH(KERNEL, ...)                                                                          \
+    switch (g.type) {                                                                                      \
+        case GEO_PLANE:                                                                                    \
+            switch (g.K) {                                                                                 \
+                case 3: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 3>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+                case 4: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 4>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+                case 5: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 5>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+                case 6: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 6>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+                case 7: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 7>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+                case 8: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 8>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+                default: throw Error(ERR_ARG, "plane constraint with unsupported vertex count");         \
+            }                                                                                              \
+            break;                                                                                         \
+        case GEO_ANGLE: hipLaunchKernelGGL((KERNEL<GEO_ANGLE, 3>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+        case GEO_EDGE: hipLaunchKernelGGL((KERNEL<GEO_EDGE, 2>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+        case GEO_CLOSENESS: hipLaunchKernelGGL((KERNEL<GEO_CLOSENESS, 1>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+        case GEO_POINT_TO_REF: hipLaunchKernelGGL((KERNEL<GEO_POINT_TO_REF, 1>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+        case GEO_REF_SURFACE: hipLaunchKernelGGL((KERNEL<GEO_REF_SURFACE, 1>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
+        default: throw Error(ERR_ARG, "unknown constraint type");                                        \
+    }
+
+void launch_geo_z(const GeoGroupDev& g, const double* x, const double* u, double* z, double* y, const Ctrl* ctrl,
+                  hipStream_t s) {
+    if (g.count == 0) return;
+    const dim3 grid(blocks_for(g.count));
+    GEO_DISPATCH(k_geo_z, g, x, u, z, y, ctrl)
+    AA_CHECK_LAUNCH();
+}
+
+int geo_u_blocks(int count) { return blocks_for(count); }
+
+void launch_geo_u(const GeoGroupDev& g, const double* xnew, const double* xcur, const double* z, const double* u,
+                  double* unew, const Ctrl* ctrl, double* red, int red_off, hipStream_t s) {
+    if (g.count == 0 || !g.hard) return;
+    const dim3 grid(blocks_for(g.count));
+    GEO_DISPATCH(k_geo_u, g, xnew, xcur, z, u, unew, ctrl, red, red_off)
+    AA_CHECK_LAUNCH();
+}
+
+void launch_geo_rhs(int n, const int* ptr, const int* slots, const double* y, const double* rhs_fixed, double* b,
+                    const Ctrl* ctrl, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_geo_rhs, dim3(blocks_for(n)), dim3(kBlock), 0, s, n, ptr, slots, y, rhs_fixed, b, ctrl);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_geo_control(Ctrl* ctrl, const double* red, int nb, int accel, double* hist_comb,
+                        unsigned long long* hist_clock, hipStream_t s) {
+    hipLaunchKernelGGL(k_geo_control, dim3(1), dim3(kBlock), 0, s, ctrl, red, nb, accel, hist_comb, hist_clock);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_geo_start(Ctrl* ctrl, unsigned long long* clock0, hipStream_t s) {
+    hipLaunchKernelGGL(k_geo_start, dim3(1), dim3(1), 0, s, ctrl, clock0);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_geo_restore(double* cu, double* cx, double* aacur, const double* du, const double* dx, long long nu,
+                        long long nx, const Ctrl* ctrl, hipStream_t s) {
+    hipLaunchKernelGGL(k_geo_restore, dim3(grid_for(nu + nx)), dim3(kBlock), 0, s, cu, cx, aacur, du, dx, nu, nx, ctrl);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_closest(const SurfDev& sd, const double* p, double* c, int n, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_closest, dim3(blocks_for(n)), dim3(kBlock), 0, s, sd, p, c, n);
+    AA_CHECK_LAUNCH();
+}
+
+}  // namespace aa

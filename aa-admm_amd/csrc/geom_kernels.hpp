@@ -1,0 +1,68 @@
+// Device data structures and kernel launchers of the Geometry (ALM) hot path
+// (the reference's ALMGeometrySolver<3>, Geometry/ALMGeometrySolver.h:163-461).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "elastic_kernels.hpp"   // Ctrl, Seg2, Anderson launchers
+
+namespace aa {
+
+// constraint types (Geometry/Constraint.h) -- must match include/aa_admm.h AA_CON_*
+enum GeoType { GEO_PLANE = 0, GEO_ANGLE = 1, GEO_EDGE = 2, GEO_CLOSENESS = 3, GEO_POINT_TO_REF = 4, GEO_REF_SURFACE = 5 };
+constexpr int kGeoMaxK = 8;   // largest plane supported on device (face valence)
+
+// Bounding-volume hierarchy over one reference triangle surface (closest-point queries of
+// PointToRefSurfaceConstraint / ReferenceSurfceConstraint). Nodes in depth-first order:
+// the left child of node i is i+1; `a` is the right child (inner) or the first triangle
+// (leaf), `b` = -(triangle count) for a leaf, 0 otherwise.
+struct BvhNode {
+    double lo[3], hi[3];
+    int a, b, pad[2];
+};
+struct BvhTri { double v[9]; };   // triangle corners, stored in leaf order
+struct SurfDev {
+    const BvhNode* nodes;
+    const BvhTri* tris;
+    int n_nodes, n_tris;
+};
+
+// One homogeneous block of constraints (same type / index count / weight / hard-soft).
+struct GeoGroupDev {
+    int type, K, cols, hard;
+    int count;
+    double sw;            // weight_ = sqrt(weight) (Constraint.h:64-69)
+    double yscale;        // scale of the rhs contribution: rho (hard) / weight (soft)
+    long long uoff;       // hard: u / z offset, SoA [(c*3 + d)][count]
+    long long slot0;      // first rhs slot of this group: slot(e, a) = slot0 + e*K + a
+    const int* idx;       // [K][count] internal point ids
+    const double* prm;    // [P][count]   EDGE length; ANGLE min, max; else unused
+    int* warm;            // [count] last closest triangle (closest-point groups), may be null
+    SurfDev surf;
+};
+
+// z-step of one group: Dx = T(x) (+u for hard), z = P(Dx) (x sqrt(w) for soft); writes z
+// (hard) and the rhs slot rows y[slot] = yscale * T^T (z - u)  (hard)  /  w T^T P(Dx)  (soft)
+void launch_geo_z(const GeoGroupDev& g, const double* x, const double* u, double* z, double* y, const Ctrl* ctrl,
+                  hipStream_t s);
+// b = rhs_fixed + sum of the slot rows of each point (fixed order)
+void launch_geo_rhs(int n, const int* ptr, const int* slots, const double* y, const double* rhs_fixed, double* b,
+                    const Ctrl* ctrl, hipStream_t s);
+// hard groups: Dn = T(x_new), Dp = T(x_cur); u_new = u + Dn - z; partial sums of
+// |Dn - z|^2 + |Dn - Dp|^2 (the combined residual, ALMGeometrySolver.h:452-461)
+void launch_geo_u(const GeoGroupDev& g, const double* xnew, const double* xcur, const double* z, const double* u,
+                  double* unew, const Ctrl* ctrl, double* red, int red_off, hipStream_t s);
+int geo_u_blocks(int count);
+// accept / reject (ALMGeometrySolver.h:215-263): comb from the partials; on accept record
+// (comb, device clock), nrec++, done when nrec >= max_iter; on reject reject = 1, Anderson
+// reset (aa_iter = aa_col = 0) and aa_skip = 1.
+void launch_geo_control(Ctrl* ctrl, const double* red, int nb, int accel, double* hist_comb,
+                        unsigned long long* hist_clock, hipStream_t s);
+// prologue: ctrl fields, clock origin
+void launch_geo_start(Ctrl* ctrl, unsigned long long* clock0, hipStream_t s);
+// reject restore: (cur_u, cur_x) = (def_u, def_x) and the Anderson current iterate alike (gate: reject)
+void launch_geo_restore(double* cu, double* cx, double* aacur, const double* du, const double* dx, long long nu,
+                        long long nx, const Ctrl* ctrl, hipStream_t s);
+// closest points of `n` points (test hook / soft-energy evaluation)
+void launch_closest(const SurfDev& sd, const double* p, double* c, int n, hipStream_t s);
+
+}  // namespace aa

@@ -110,6 +110,69 @@ int aa_elastic_bench_iterations(aa_elastic h, int iters, double* ms);
  * measured with HIP events on the solver's stream; and its algorithmic bytes per launch. */
 int aa_elastic_kernel_stats(aa_elastic h, const char* name, double* avg_ms, double* bytes, int* launches);
 
+/* ==== Geometry: ALMGeometrySolver<3> + Constraint<3> (bldeng/AA-ADMM Geometry/) ============= */
+typedef struct aa_geom_s* aa_geom;        /* one ALMGeometrySolver<3> instance             */
+
+/* Constraint types (Geometry/Constraint.h). Index count k per constraint and the per-constraint
+ * parameters each type takes (params is [count][P], row-major):
+ *   AA_CON_PLANE        PlaneConstraint(idI, w)                     k = 3..8  P = 0  (:396-414)
+ *   AA_CON_ANGLE        AngleConstraint<3>(tip, s1, s2, w, min, max) k = 3     P = 2  (:220-296)
+ *   AA_CON_EDGE         EdgeLengthConstraint<3>(i1, i2, w, length)   k = 2     P = 1  (:194-218)
+ *   AA_CON_CLOSENESS    ClosenessConstraint<3>(i, w, target)         k = 1     P = 3  (:299-326;
+ *                       its projection is the identity in the reference, kept as such)
+ *   AA_CON_POINT_TO_REF PointToRefSurfaceConstraint(i, w, aabb)      k = 1     P = 1 = surface id (:328-349)
+ *   AA_CON_REF_SURFACE  ReferenceSurfceConstraint(n, w, V, F): one   k = 1     P = 1 = surface id (:351-394)
+ *                       constraint over points 0..count-1 (idx may be NULL)                    */
+#define AA_CON_PLANE 0
+#define AA_CON_ANGLE 1
+#define AA_CON_EDGE 2
+#define AA_CON_CLOSENESS 3
+#define AA_CON_POINT_TO_REF 4
+#define AA_CON_REF_SURFACE 5
+
+/* SPDSolverType (Geometry/SolverCommon.h:34-38); both factorisations are a Cholesky here. */
+#define AA_SPD_LDLT 0
+#define AA_SPD_LLT 1
+
+typedef struct {
+    double setup_ms;         /* setup_ADMM: assembly of the global matrix and rhs_fixed       */
+    double factor_ms;        /* nested-dissection ordering + factorisation (first solve)     */
+    double solve_ms;         /* wall time of the last solve_ADMM (device-synchronised)       */
+    int iterations;          /* x-updates of the last solve (accepted + rejected)            */
+    int accepted;            /* accepted iterations (= function_values_.size())              */
+    int rejects;             /* Anderson rejections                                          */
+    int n_points;
+    long long nnz_factor;    /* scalar nnz(L) of the global factor                           */
+    long long hard_cols, soft_cols, n_constraints;
+} aa_geom_runtime;
+
+int aa_geom_create(aa_ctx ctx, aa_geom* out);                                  /* ALMGeometrySolver() */
+int aa_geom_destroy(aa_geom h);                                                /* ~ALMGeometrySolver  */
+/* Reference surface (TriMeshAABB / igl::AABB over V (nv x 3), F (nf x 3)); returns its id. */
+int aa_geom_add_ref_surface(aa_geom h, const double* V3, int nv, const int* F3, int nf, int* id);
+/* add_hard_constraint (hard = 1) / add_soft_constraint (hard = 0) of `count` constraints of one
+ * type: idx is [count][k] point ids, weight the constructor weight, params [count][P]. */
+int aa_geom_add_constraints(aa_geom h, int hard, int type, const int* idx, int k, int count, double weight,
+                            const double* params);
+/* add_laplacian / add_uniform_laplacian (coefs as given; ref_points3 == NULL) and
+ * add_relative_laplacian / add_relative_uniform_laplacian (ref_points3 = 3 x n points). */
+int aa_geom_add_laplacian(aa_geom h, const int* idx, const double* coefs, int k, double weight,
+                          const double* ref_points3);
+int aa_geom_add_closeness(aa_geom h, int idx, double weight, const double* target3);   /* add_closeness */
+int aa_geom_setup(aa_geom h, int n_points, double penalty, int spd_solver_type);       /* setup_ADMM    */
+/* solve_ADMM(init_x (3 x n), rel_residual_eps, max_iter, Anderson_m): max_iter accepted
+ * iterations; Anderson_m = 0 runs plain ADMM. */
+int aa_geom_solve(aa_geom h, const double* init_x3, double rel_residual_eps, int max_iter, int anderson_m);
+int aa_geom_get_solution(aa_geom h, double* x3);                               /* get_solution()      */
+/* function_values_ (combined residual per accepted iteration) and elapsed_time_ (s since the
+ * loop started, device clock). Returns the count in *n (<= cap copied). */
+int aa_geom_get_history(aa_geom h, double* comb, double* time_s, int cap, int* n);
+int aa_geom_runtime_info(aa_geom h, aa_geom_runtime* out);
+/* closest points on a reference surface (PointToRefSurfaceConstraint's projection) */
+int aa_geom_closest_points(aa_geom h, int surface, const double* p3, int n, double* out3);
+int aa_geom_bench_iterations(aa_geom h, int iters, double* ms);
+int aa_geom_kernel_stats(aa_geom h, const char* name, double* avg_ms, double* bytes, int* launches);
+
 #ifdef __cplusplus
 }
 #endif
