@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--nx", type=int, default=112)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-iters", type=int, default=40)
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c5"],
+                   help="c2: cloth (BASELINE configs[1], the headline); c3: planar-quad 317x317 (configs[2]); "
+                        "c5: wire mesh 707x707 (configs[4], single-GPU here)")
     return p.parse_args()
 
 
@@ -111,9 +114,115 @@ def cpu_baseline(scene_builder, iters):
                       f"median iters/s of steps 2-3 (step 1 = warm-up), OMP_NUM_THREADS={threads}"}
 
 
+def geom_scene(args):
+    gs = importlib.import_module("aa-admm_amd.geom_scenes")
+    if args.config == "c3":
+        n = args.nx if args.nx != 112 else 317
+        return gs.pq_heightfield(n, n, iters=args.iters, aa_m=10), f"planar-quad height field {n}x{n} quads"
+    n = args.nx if args.nx != 112 else 707
+    return gs.wire_grid(n, n, iters=args.iters, aa_m=20), f"wire mesh height field {n}x{n} quads"
+
+
+def geom_cpu_baseline(args):
+    """The REFERENCE's ALMGeometrySolver (oracle/_ref/ref_geom, compiled from its own sources) on
+    the host cores, bounded sample: the same scene with a reduced iteration count."""
+    gs = importlib.import_module("aa-admm_amd.geom_scenes")
+    sc, _ = geom_scene(argparse.Namespace(**{**vars(args), "iters": args.cpu_iters}))
+    drv = os.path.join(REPO, "oracle", "_ref", "ref_geom")
+    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    if not os.path.exists(drv):
+        return {"value": None, "error": "oracle/_ref/ref_geom not built"}
+    with tempfile.TemporaryDirectory() as tmp:
+        gs.write_geom_scene(sc, os.path.join(tmp, "s.bin"))
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+        r = subprocess.run([drv, "s.bin", "o.bin"], cwd=tmp, capture_output=True, text=True, env=env, timeout=900)
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr[-500:])
+        res = gs.read_geom_result(os.path.join(tmp, "o.bin"), sc.n_points)
+    return {"value": round(len(res["comb"]) / res["loop_s"], 3), "unit": "ADMM iters/s", "cores": threads,
+            "kind": "reference", "setup_s": round(res["setup_s"], 3),
+            "sample": f"{sc.name}: one solve_ADMM of {args.cpu_iters} accepted iterations (m={sc.aa_m}), loop time "
+                      f"(setup excluded, as ALMGeometrySolver.h:194-195), OMP_NUM_THREADS={threads}"}
+
+
+def main_geom(args, world, rank, local, dist):
+    """configs[2] / configs[4]: one bench step = one solve_ADMM of `iters` accepted ALM iterations
+    (inputs resident on the device after setup); value = accepted iterations / wall time."""
+    pkg = importlib.import_module("aa-admm_amd")
+    capi = pkg.capi
+    ctx = capi.Context(local)
+    sc, desc = geom_scene(args)
+    t0 = time.time()
+    g = capi.geom_from_scene(ctx, sc)
+    eps = 2.0 * (1e-8 * sc.avg_edge_length() * sc.hard_cols()) ** 2   # ALMGeometrySolver.h:173 (commented stop)
+    for _ in range(max(1, args.warmup)):
+        g.solve(sc.x0, 1e-8 * sc.avg_edge_length(), sc.iters, sc.aa_m)   # first solve also orders + factors
+    rt0 = g.runtime()
+    setup_ms = (time.time() - t0) * 1e3
+    barrier(dist, ctx)
+    t0 = time.perf_counter()
+    acc, xupd, tte = 0, 0, []
+    for _ in range(args.steps):
+        g.solve(sc.x0, 1e-8 * sc.avg_edge_length(), sc.iters, sc.aa_m)
+        rt = g.runtime()
+        acc += rt.accepted
+        xupd += rt.iterations
+        h = g.history()
+        hit = np.nonzero(h["comb"] <= eps)[0]
+        tte.append(float(h["time_s"][hit[0]] * 1e3) if len(hit) else None)
+    barrier(dist, ctx)
+    elapsed = time.perf_counter() - t0
+    elapsed_max = allreduce(dist, elapsed, _max_op(dist))
+    acc_all = allreduce(dist, float(acc), _sum_op(dist))
+    value = acc_all / elapsed_max
+    roof, cpu = None, None
+    if rank == 0:
+        g.bench_iterations(min(sc.iters, 50))
+        stats = {k: g.kernel_stats(k) for k in ("z", "rhs", "solve", "u", "aa")}
+        k = max(stats, key=lambda kk: stats[kk]["avg_ms"])
+        st = stats[k]
+        achieved = st["bytes"] / (st["avg_ms"] * 1e-3) / 1e9 if st["avg_ms"] > 0 else 0.0
+        names = {"z": "k_geo_z (constraint projections + rhs slot rows)", "rhs": "k_geo_rhs",
+                 "solve": "multifrontal triangular solves (3 RHS)", "u": "k_geo_u (dual update + residual)",
+                 "aa": "Anderson reduce/solve/mix + control"}
+        roof = {"kernel": names[k], "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "avg_launch_us": round(st["avg_ms"] * 1e3, 2), "bytes_per_launch": st["bytes"],
+                "phase_us_per_iter": {kk: round(v["avg_ms"] * 1e3, 2) for kk, v in stats.items()},
+                "phase_bytes_per_iter": {kk: v["bytes"] for kk, v in stats.items()}}
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = geom_cpu_baseline(args)
+            except Exception as e:
+                cpu = {"value": None, "error": str(e)[:200]}
+        tt = [t for t in tte if t is not None]
+        line = {
+            "metric": "ADMM iters/sec + time-to-eps (primal+dual residual)", "value": round(value, 2),
+            "unit": "ADMM iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic (generated height-field quad mesh)",
+            "config": {"workload": f"{desc}, ALM + Anderson m={sc.aa_m}, {sc.iters} accepted iterations per solve "
+                                   f"(BASELINE configs[{2 if args.config == 'c3' else 4}])",
+                       "points": sc.n_points, "hard_cols": sc.hard_cols(), "anderson_m": sc.aa_m,
+                       "parallelism": f"replicas{world}", "global_solve": "supernodal direct",
+                       "nnz_factor": rt0.nnz_factor, "setup_ms": round(setup_ms, 1),
+                       "factor_ms": round(rt0.factor_ms, 1)},
+            "accepted_iters": int(acc_all), "x_updates": int(xupd),
+            "time_to_eps_ms": (round(statistics.median(tt), 3) if tt else None), "eps_abs": eps,
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    g.close()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world, rank, local, dist = dist_setup(args.gpus)
+    if args.config != "c2":
+        return main_geom(args, world, rank, local, dist)
     pkg = importlib.import_module("aa-admm_amd")
     capi, scenes = pkg.capi, pkg.scenes
 

@@ -8,7 +8,7 @@ application. This script writes the scenes below, runs them, and stores inputs +
 PlanarityOpt run on its own data files (Geometry/Geometry_model/PQMeshData), which pins the
 scene recipe of geom_scenes.planarity_from_mesh. Run in the build container:
 
-    make -C oracle ref && python tests/golden/make_golden_geom.py
+    make -C oracle ref && python tests/golden/make_golden_geom.py [--full]
 """
 from __future__ import annotations
 
@@ -163,7 +163,35 @@ def element_tables(tmp):
     return out
 
 
+def scene_digest(sc):
+    """sha256 over the scene arrays: the full-size fixture stores outputs only (the scene is
+    regenerated by geom_scenes) and this digest proves the regenerated scene is the same."""
+    import hashlib
+    h = hashlib.sha256()
+    for a in [sc.x0, sc.reg_idx, sc.reg_coef] + [g.idx for g in sc.groups] + [V for V, F in sc.surfaces] + \
+             [F for V, F in sc.surfaces]:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return np.frombuffer(h.digest(), np.uint8)
+
+
+def full_size_c3(tmp):
+    """BASELINE configs[2] at full size (317 x 317 quads): the reference's residual curve and
+    sampled solution points (the 2.4 MB solution itself is not stored)."""
+    sc = gs.pq_heightfield(317, 317, iters=100, aa_m=10)
+    res = run_ref(sc, tmp)
+    rng = np.random.default_rng(3)
+    sample = np.sort(rng.choice(sc.n_points, 256, replace=False)).astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "full_c3_pq317.npz"), comb=res["comb"], sample=sample,
+                        x_sample=res["x"][sample], x_sum=res["x"].sum(0), x_norm=np.linalg.norm(res["x"]),
+                        digest=scene_digest(sc), ref_loop_s=res["loop_s"], ref_setup_s=res["setup_s"])
+    print("full_c3_pq317", len(res["comb"]), res["loop_s"])
+
+
 def main():
+    if "--full" in sys.argv:
+        with tempfile.TemporaryDirectory() as tmp:
+            full_size_c3(tmp)
+        return
     with tempfile.TemporaryDirectory() as tmp:
         for name, sc in cases().items():
             res = run_ref(sc, tmp)

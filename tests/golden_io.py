@@ -52,7 +52,8 @@ def load_case(name):
 
 def case_names():
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and f not in ("elements.npz", "geom_elements.npz") and not f.startswith("geom_"))
+                  if f.endswith(".npz") and f not in ("elements.npz", "geom_elements.npz")
+                  and not f.startswith(("geom_", "full_")))
 
 
 # ---------------------------------------------------------------------------- Geometry (ALM)

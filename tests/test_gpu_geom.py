@@ -4,6 +4,7 @@ judged relative to comb_0 -- 1e-8 over the first 40 accepted iterations and 1e-6
 curve (Anderson trajectories amplify rounding differences; the oracle meets the same bounds
 against the reference); solutions 1e-8 relative; closest points 1e-13 absolute."""
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -59,26 +60,38 @@ def test_gpu_geom_deterministic(pkg, ctx):
     ga.close(); gb.close()
 
 
-def test_gpu_geom_full_size_c3_properties(pkg, ctx):
+def test_gpu_geom_full_size_c3(pkg, ctx):
     """BASELINE configs[2] at full size (317 x 317 quads = 100 489 planarity constraints, 101 124
-    points, m = 10): finite, one record per accepted iteration, residual decreases by orders of
-    magnitude, and the faces become planar (max |n . p| over faces, normalised by edge length)."""
+    points, m = 10) against the reference's own run of the same scene (tests/golden/
+    full_c3_pq317.npz, make_golden_geom.py --full). The curve is judged relative to comb_0 over
+    the first 75 iterations (1e-8); later the reference itself enters an accept/reject cycle in
+    which comb grows 500x over comb_0, so that phase is judged per entry (1e-3 relative); the
+    solution on 256 sampled points and its sum to 1e-8 relative; plus planarity improvement."""
     gs = pkg.geom_scenes
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden_geom import scene_digest
+    ref = np.load(os.path.join(GOLDEN, "full_c3_pq317.npz"))
     sc = gs.pq_heightfield(317, 317, iters=100, aa_m=10)
+    assert np.array_equal(scene_digest(sc), ref["digest"]), "regenerated scene differs from the fixture's"
     got, g = pkg.capi.run_geom(ctx, sc)
     rt = g.runtime()
     assert rt.n_points == 101124 and rt.hard_cols == 4 * 100489 and rt.accepted == 100
-    c = got["comb"]
-    assert len(c) == 100 and np.all(np.isfinite(c)) and c[-1] < 1e-3 * c[0]
+    c, rc = got["comb"], ref["comb"]
+    assert len(c) == len(rc) == 100 and np.all(np.isfinite(c))
+    assert np.abs(c[:75] - rc[:75]).max() <= 1e-8 * rc[0]
+    assert np.all(np.abs(c - rc) <= 1e-3 * np.abs(rc))
+    x = got["x"]
+    scale = np.abs(ref["x_sample"]).max()
+    assert np.abs(x[ref["sample"]] - ref["x_sample"]).max() <= 1e-8 * scale
+    assert np.allclose(x.sum(0), ref["x_sum"], rtol=1e-8, atol=1e-8 * scale * len(x))
 
     def planarity(X):
         Q = sc.groups[1].idx
         P = X[Q] - X[Q].mean(1, keepdims=True)
-        _, _, vt = np.linalg.svd(P, full_matrices=True)
-        n = vt[:, 2, :]
+        n = np.linalg.svd(P, full_matrices=True)[2][:, 2, :]
         return np.abs(np.einsum("fkd,fd->fk", P, n)).max() / sc.avg_edge_length()
 
-    assert planarity(got["x"]) < 0.1 * planarity(sc.x0)
+    assert planarity(x) < 0.5 * planarity(sc.x0)
     g.close()
 
 
