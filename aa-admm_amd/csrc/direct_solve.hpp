@@ -1,16 +1,21 @@
 // GPU supernodal triangular solves against the host multifrontal factor (spd_direct.hpp).
 //
-// Replaces the reference's per-iteration LDLTSolver::solve (LinearSolver.hpp:87-90) with a
-// multifrontal solve over the nested-dissection supernode tree, one kernel per tree height
-// and sweep (all supernodes of equal height are independent), one workgroup per supernode:
+// Replaces the reference's per-iteration LDLTSolver::solve (LinearSolver.hpp:87-90) and
+// SPDSolver::solve (Geometry/SPDSolver.h:60-63) with a level-scheduled solve over the
+// nested-dissection supernode tree. Per supernode s (pivots P, boundary rows B, |P| = p,
+// |B| = nb) the host pre-multiplies the factor into one dense (p + nb) x p matrix
+//        G_s = [ Linv_PP ; M ],   M = L_BP Linv_PP,
+// so that both sweeps of a supernode are single matrix-vector products with no dependency
+// inside the supernode:
 //   forward   f = [b_P ; 0] + extend_add(children's update vectors)
-//             y_P = Linv_PP f_P                 (dense, inverted diagonal block)
-//             u   = f_B - L_BP y_P              (dense; this node's update vector for its parent)
-//   backward  t   = y_P - L_BP^T x_B            (x_B gathered from the ancestors' solution)
-//             x_P = Linv_PP^T t
-// Every dense product is thread-per-row over a column-major (coalesced) copy of the block,
-// with the vector operand broadcast from LDS: no cross-lane reductions, no atomics,
-// deterministic. The three coordinates (x, y, z right-hand sides) are processed together.
+//             y_P = Linv_PP f_P ,   u = f_B - M f_P        (rows of G_s . f_P)
+//   backward  x_P = Linv_PP^T y_P - M^T x_B                (columns of G_s . [y_P ; -x_B])
+// All supernodes of one tree height are independent, so a level is one launch whose work is
+// cut into row tasks: small supernodes get a workgroup (thread per row, front vector in LDS),
+// large ones are spread over many workgroups (wave per row, lanes across the row). Every
+// product reads a coalesced copy of G_s (row-major for lane-across-row, column-major for
+// thread-per-row); sums are in a fixed order (no atomics): deterministic. Three right-hand
+// sides (x, y, z coordinates) are processed together.
 #pragma once
 #include <vector>
 
@@ -22,9 +27,8 @@ namespace aa {
 
 class DirectSolver {
 public:
-    static constexpr int kMaxFront = 3200;   // p + |bnd| of a supernode kept in LDS (3 RHS fp64)
-    static constexpr int kBigP = 512;        // larger supernodes use the multi-workgroup path
     static constexpr int kTopRows = 2048;    // upper tree levels amalgamated into one dense root
+    static constexpr int kWaveP = 192;       // supernodes with p above this use wave-per-row tasks
 
     void build(const SupernodalFactor& F, hipStream_t s);
     // x (n x 3, stride 3 doubles) = A^-1 b ; b is read only. gate: skip when ctrl->done (or !reject).
@@ -34,19 +38,22 @@ public:
     double bytes_per_solve() const { return bytes_; }
     int kernels_per_solve() const { return kernels_; }
 
+    struct Task { int node, r0, nr, mode; };   // mode 0: thread per row, 1: wave per row
+
 private:
-    struct Level { int first, count, block, lds_fwd, lds_bwd; std::vector<int> big; };
-    struct Big { int node, b0, p, nb, bnd_off, pptr_off; long long loff, boff, uoff, foff, toff; };
+    struct Level {
+        int fwd_first = 0, fwd_count = 0, bwd_first = 0, bwd_count = 0;
+        int asm_first = 0, asm_count = 0;     // assembly tasks of the wave-mode supernodes
+        int block = 256, lds_fwd = 0, lds_bwd = 0;
+    };
     int n_ = 0, nn_ = 0, kernels_ = 0;
     size_t nnz_L_ = 0;
     double bytes_ = 0;
-    DevBuf<int> beg_, p_, nb_, bnd_off_, bnd_, kid_ptr_, kids_, map_off_, map_, lvl_nodes_;
-    DevBuf<long long> loff_, boff_, uoff_;
-    DevBuf<double> linv_rm_, linv_cm_, lbp_rm_, lbp_cm_, Y_, U_, Fg_, Tg_;
-    DevBuf<int> big_pptr_;
-    DevBuf<long long> big_psrc_;
+    DevBuf<int> beg_, p_, nb_, bnd_off_, bnd_, pull_off_, pptr_;
+    DevBuf<long long> goff_, uoff_, foff_, psrc_;
+    DevBuf<double> Gr_, Gc_, Y_, U_, Fg_;
+    DevBuf<Task> tasks_;
     std::vector<Level> levels_;
-    std::vector<Big> bigs_;
 };
 
 }  // namespace aa

@@ -78,6 +78,7 @@ struct BvhBuilder {
         if (e - b <= 4) {
             (*nodes)[me].a = (int)tris->size();
             (*nodes)[me].b = -(e - b);
+            (*nodes)[me].skip = me + 1;
             for (int i = b; i < e; ++i) {
                 BvhTri tr;
                 for (int a = 0; a < 3; ++a)
@@ -95,6 +96,7 @@ struct BvhBuilder {
         const int r = build(mid, e);
         (*nodes)[me].a = r;
         (*nodes)[me].b = 0;
+        (*nodes)[me].skip = (int)nodes->size();
         return me;
     }
 };

@@ -10,7 +10,7 @@
 //             Eigen JacobiSVD), normal = the row rotation of the smallest row norm;
 //   angle  -- the closed-form rotation of Constraint.h:243-291;
 //   edge   -- v |v|^-1 L;   closeness -- identity (Constraint.h:319-322 never overrides);
-//   closest point on a reference surface -- stack traversal of a depth-first BVH with exact
+//   closest point on a reference surface -- stackless traversal of a depth-first BVH with exact
 //             box pruning, warm-started from the previous iteration's triangle.
 #include "common.hpp"
 #include "geom_kernels.hpp"
@@ -235,51 +235,53 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
     return tx * tx + ty * ty + tz * tz;
 }
 
-// exact closest point on the surface; `warm` (a triangle id or -1) seeds the upper bound
+// exact closest point on the surface. Stackless depth-first traversal over escape links
+// (`skip` = the node after a subtree): no per-lane stack, so no scratch memory. The upper
+// bound comes from `warm` (the previous iteration's triangle: points move little between ALM
+// iterations) or, on a cold start, from a greedy descent to the nearest-box leaf; boxes that
+// cannot beat it are skipped whole. Strictly smaller distances replace the best, so the result
+// is the exact minimum (ties resolved toward the warm / first-found triangle).
 __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, int warm, double& cx, double& cy,
                            double& cz) {
-    constexpr int kStack = 64;
     double best = INFINITY;
     int best_t = -1;
     cx = px; cy = py; cz = pz;
-    if (warm >= 0 && warm < S.n_tris) {
+    if (S.n_nodes == 0) return -1;
+    auto test_tri = [&](int t) {
         double qx, qy, qz;
-        closest_on_tri(S.tris[warm].v, px, py, pz, qx, qy, qz);
-        best = (px - qx) * (px - qx) + (py - qy) * (py - qy) + (pz - qz) * (pz - qz);
-        best_t = warm; cx = qx; cy = qy; cz = qz;
-    }
-    if (S.n_nodes == 0) return best_t;
-    int st_node[kStack];
-    double st_d[kStack];
-    int sp = 0;
-    int node = 0;
-    double nd2 = box_d2(S.nodes[0], px, py, pz);
-    for (;;) {
-        if (nd2 < best) {
-            const BvhNode nd = S.nodes[node];
+        closest_on_tri(S.tris[t].v, px, py, pz, qx, qy, qz);
+        const double d2 = (px - qx) * (px - qx) + (py - qy) * (py - qy) + (pz - qz) * (pz - qz);
+        if (d2 < best) { best = d2; best_t = t; cx = qx; cy = qy; cz = qz; }
+    };
+    if (warm >= 0 && warm < S.n_tris) {
+        test_tri(warm);
+    } else {   // cold start: greedy descent
+        int i = 0;
+        for (;;) {
+            const BvhNode& nd = S.nodes[i];
             if (nd.b < 0) {
-                for (int t = nd.a; t < nd.a - nd.b; ++t) {
-                    if (t == warm) continue;
-                    double qx, qy, qz;
-                    closest_on_tri(S.tris[t].v, px, py, pz, qx, qy, qz);
-                    const double d2 = (px - qx) * (px - qx) + (py - qy) * (py - qy) + (pz - qz) * (pz - qz);
-                    if (d2 < best) { best = d2; best_t = t; cx = qx; cy = qy; cz = qz; }
-                }
-            } else {
-                const int l = node + 1, r = nd.a;
-                const double dl = box_d2(S.nodes[l], px, py, pz), dr = box_d2(S.nodes[r], px, py, pz);
-                const bool left_first = dl <= dr;
-                const int nn = left_first ? l : r, ff = left_first ? r : l;
-                const double dn = left_first ? dl : dr, df = left_first ? dr : dl;
-                if (df < best && sp < kStack) { st_node[sp] = ff; st_d[sp] = df; ++sp; }
-                node = nn; nd2 = dn;
-                continue;
+                for (int t = nd.a; t < nd.a - nd.b; ++t) test_tri(t);
+                break;
             }
+            const double dl = box_d2(S.nodes[i + 1], px, py, pz), dr = box_d2(S.nodes[nd.a], px, py, pz);
+            i = dl <= dr ? i + 1 : nd.a;
         }
-        if (sp == 0) break;
-        --sp;
-        node = st_node[sp];
-        nd2 = st_d[sp];
+    }
+    const int seed = best_t;
+    int i = 0;
+    while (i < S.n_nodes) {
+        const BvhNode nd = S.nodes[i];
+        if (box_d2(nd, px, py, pz) < best) {
+            if (nd.b < 0) {
+                for (int t = nd.a; t < nd.a - nd.b; ++t)
+                    if (t != seed) test_tri(t);
+                i = nd.skip;
+            } else {
+                i = i + 1;
+            }
+        } else {
+            i = nd.skip;
+        }
     }
     return best_t;
 }

@@ -14,10 +14,11 @@ constexpr int kGeoMaxK = 8;   // largest plane supported on device (face valence
 // Bounding-volume hierarchy over one reference triangle surface (closest-point queries of
 // PointToRefSurfaceConstraint / ReferenceSurfceConstraint). Nodes in depth-first order:
 // the left child of node i is i+1; `a` is the right child (inner) or the first triangle
-// (leaf), `b` = -(triangle count) for a leaf, 0 otherwise.
+// (leaf), `b` = -(triangle count) for a leaf, 0 otherwise; `skip` is the first node after
+// this node's subtree (the escape link of a stackless traversal).
 struct BvhNode {
     double lo[3], hi[3];
-    int a, b, pad[2];
+    int a, b, skip, pad;
 };
 struct BvhTri { double v[9]; };   // triangle corners, stored in leaf order
 struct SurfDev {

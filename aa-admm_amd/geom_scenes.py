@@ -269,10 +269,15 @@ def planarity_from_mesh(V, faces, refV, refF, *, iters=100, aa_m=10, penalty=1e5
     return sc
 
 
-def pq_heightfield(nx=317, ny=317, *, iters=100, aa_m=10, ref_factor=2, **kw) -> GeomScene:
+def pq_heightfield(nx=317, ny=317, *, iters=100, aa_m=10, ref_factor=2, noise=0.0, **kw) -> GeomScene:
     """configs[2]: planar-quad optimisation of a (nx x ny)-quad height-field grid (100 489
-    faces at 317 x 317), reference surface = the same field triangulated at `ref_factor`x."""
+    faces at 317 x 317), reference surface = the same field triangulated at `ref_factor`x.
+    noise > 0 displaces the initial points off the surface by noise * edge length (seeded,
+    deterministic) -- a scanned-surface start, so that closeness and planarity both act."""
     V, Q = quad_grid(nx, ny)
+    if noise > 0:
+        rng = np.random.default_rng(20191015)
+        V = V + (noise / max(nx, ny)) * rng.standard_normal(V.shape)
     RV, RF = field_trimesh(ref_factor * nx, ref_factor * ny)
     return planarity_from_mesh(V, [list(q) for q in Q], RV, RF, iters=iters, aa_m=aa_m,
                                name=f"pq{nx}x{ny}", **kw)

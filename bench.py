@@ -118,7 +118,8 @@ def geom_scene(args):
     gs = importlib.import_module("aa-admm_amd.geom_scenes")
     if args.config == "c3":
         n = args.nx if args.nx != 112 else 317
-        return gs.pq_heightfield(n, n, iters=args.iters, aa_m=10), f"planar-quad height field {n}x{n} quads"
+        return (gs.pq_heightfield(n, n, iters=args.iters, aa_m=10, noise=0.3),
+                f"planar-quad height field {n}x{n} quads, initial points scattered 0.3 h off the surface")
     n = args.nx if args.nx != 112 else 707
     return gs.wire_grid(n, n, iters=args.iters, aa_m=20), f"wire mesh height field {n}x{n} quads"
 

@@ -177,7 +177,7 @@ def scene_digest(sc):
 def full_size_c3(tmp):
     """BASELINE configs[2] at full size (317 x 317 quads): the reference's residual curve and
     sampled solution points (the 2.4 MB solution itself is not stored)."""
-    sc = gs.pq_heightfield(317, 317, iters=100, aa_m=10)
+    sc = gs.pq_heightfield(317, 317, iters=100, aa_m=10, noise=0.3)
     res = run_ref(sc, tmp)
     rng = np.random.default_rng(3)
     sample = np.sort(rng.choice(sc.n_points, 256, replace=False)).astype(np.int32)

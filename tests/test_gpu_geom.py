@@ -62,28 +62,28 @@ def test_gpu_geom_deterministic(pkg, ctx):
 
 def test_gpu_geom_full_size_c3(pkg, ctx):
     """BASELINE configs[2] at full size (317 x 317 quads = 100 489 planarity constraints, 101 124
-    points, m = 10) against the reference's own run of the same scene (tests/golden/
-    full_c3_pq317.npz, make_golden_geom.py --full). The curve is judged relative to comb_0 over
-    the first 75 iterations (1e-8); later the reference itself enters an accept/reject cycle in
-    which comb grows 500x over comb_0, so that phase is judged per entry (1e-3 relative); the
-    solution on 256 sampled points and its sum to 1e-8 relative; plus planarity improvement."""
+    points scattered 0.3 h off the surface, m = 10) against the reference's own run of the same
+    scene (tests/golden/full_c3_pq317.npz, make_golden_geom.py --full): the residual curve
+    relative to comb_0 (1e-8 over the first 40 iterations, 1e-6 over all 100), the solution on
+    256 sampled points and its column sums (1e-6 of the coordinate scale), and the faces ending
+    flatter than they started."""
     gs = pkg.geom_scenes
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
     from make_golden_geom import scene_digest
     ref = np.load(os.path.join(GOLDEN, "full_c3_pq317.npz"))
-    sc = gs.pq_heightfield(317, 317, iters=100, aa_m=10)
+    sc = gs.pq_heightfield(317, 317, iters=100, aa_m=10, noise=0.3)
     assert np.array_equal(scene_digest(sc), ref["digest"]), "regenerated scene differs from the fixture's"
     got, g = pkg.capi.run_geom(ctx, sc)
     rt = g.runtime()
     assert rt.n_points == 101124 and rt.hard_cols == 4 * 100489 and rt.accepted == 100
     c, rc = got["comb"], ref["comb"]
     assert len(c) == len(rc) == 100 and np.all(np.isfinite(c))
-    assert np.abs(c[:75] - rc[:75]).max() <= 1e-8 * rc[0]
-    assert np.all(np.abs(c - rc) <= 1e-3 * np.abs(rc))
+    assert np.abs(c[:40] - rc[:40]).max() <= 1e-8 * rc[0]
+    assert np.abs(c - rc).max() <= 1e-6 * rc[0]
     x = got["x"]
     scale = np.abs(ref["x_sample"]).max()
-    assert np.abs(x[ref["sample"]] - ref["x_sample"]).max() <= 1e-8 * scale
-    assert np.allclose(x.sum(0), ref["x_sum"], rtol=1e-8, atol=1e-8 * scale * len(x))
+    assert np.abs(x[ref["sample"]] - ref["x_sample"]).max() <= 1e-6 * scale
+    assert np.allclose(x.sum(0), ref["x_sum"], rtol=1e-6, atol=1e-6 * scale * len(x))
 
     def planarity(X):
         Q = sc.groups[1].idx
