@@ -4,6 +4,7 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 namespace aa {
@@ -16,12 +17,6 @@ __device__ __forceinline__ bool solve_gated(const Ctrl* c, int gate_reject) {
     return gate_reject && !c->reject;
 }
 
-struct Plan {  // kernel arguments shared by the solve kernels
-    const int* beg; const int* p; const int* nb; const int* bnd_off; const int* bnd;
-    const int* pull_off; const int* pptr; const long long* psrc;
-    const long long* goff; const long long* uoff; const long long* foff;
-    const double* Gr; const double* Gc;
-};
 using Task = DirectSolver::Task;
 
 __device__ __forceinline__ double wsum(double v) {
@@ -30,20 +25,22 @@ __device__ __forceinline__ double wsum(double v) {
     return v;
 }
 
-// front row q of supernode s: [b_P ; 0]_q + the children's update entries landing on it
-__device__ __forceinline__ void front_row(const Plan& P, int s, int q, const double* __restrict__ B,
-                                          const double* __restrict__ U, double& a0, double& a1, double& a2) {
+// front row q of a supernode: [b_P ; 0]_q + the children's update entries landing on it
+// (ELL pull list: t.ell_w offsets into U per row, -1 = none; fixed order -> deterministic)
+__device__ __forceinline__ void front_row(const Task& t, int q, const long long* __restrict__ ell,
+                                          const double* __restrict__ B, const double* __restrict__ U, double& a0,
+                                          double& a1, double& a2) {
     a0 = a1 = a2 = 0;
-    if (q < P.p[s]) { const size_t o = 3 * (size_t)(P.beg[s] + q); a0 = B[o]; a1 = B[o + 1]; a2 = B[o + 2]; }
-    const int r = P.pull_off[s] + q;
-    for (int e = P.pptr[r]; e < P.pptr[r + 1]; ++e) {
-        const double* u = U + P.psrc[e];
-        a0 += u[0]; a1 += u[1]; a2 += u[2];
+    if (q < t.p) { const size_t o = 3 * (size_t)(t.beg + q); a0 = B[o]; a1 = B[o + 1]; a2 = B[o + 2]; }
+    const long long* e = ell + t.ell_off + (size_t)q * t.ell_w;
+    for (int k = 0; k < t.ell_w; ++k) {
+        const long long o = e[k];
+        if (o >= 0) { a0 += U[o]; a1 += U[o + 1]; a2 += U[o + 2]; }
     }
 }
 
 // assembly of the front vectors of wave-mode supernodes into Fg
-__global__ __launch_bounds__(256) void k_asm(Plan P, const Task* __restrict__ tasks, int first,
+__global__ __launch_bounds__(256) void k_asm(const Task* __restrict__ tasks, int first, const long long* __restrict__ ell,
                                              const double* __restrict__ B, const double* __restrict__ U,
                                              double* __restrict__ Fg, const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
@@ -51,29 +48,30 @@ __global__ __launch_bounds__(256) void k_asm(Plan P, const Task* __restrict__ ta
     if ((int)threadIdx.x >= t.nr) return;
     const int q = t.r0 + threadIdx.x;
     double a0, a1, a2;
-    front_row(P, t.node, q, B, U, a0, a1, a2);
-    double* f = Fg + P.foff[t.node] + 3 * (size_t)q;
+    front_row(t, q, ell, B, U, a0, a1, a2);
+    double* f = Fg + t.foff + 3 * (size_t)q;
     f[0] = a0; f[1] = a1; f[2] = a2;
 }
 
 // forward sweep of one tree level: y_P = Linv f_P (rows r < p), u = f_B - M f_P (rows r >= p)
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_fwd(Plan P, const Task* __restrict__ tasks, int first,
+__global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, int first, const double* __restrict__ Gr,
+                                               const double* __restrict__ Gc, const long long* __restrict__ ell,
                                                const double* __restrict__ B, double* __restrict__ Y,
                                                double* __restrict__ U, const double* __restrict__ Fg,
                                                const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Task t = tasks[first + blockIdx.x];
-    const int s = t.node, p = P.p[s], R = p + P.nb[s], b0 = P.beg[s];
+    const int p = t.p, R = p + t.nb;
     const int tid = threadIdx.x;
     if (t.mode == 0) {   // thread per row, f_P in LDS, column-major G (lanes read consecutive rows)
         double* f = lds;
-        for (int c = tid; c < p; c += BLOCK) front_row(P, s, c, B, U, f[3 * c], f[3 * c + 1], f[3 * c + 2]);
+        for (int c = tid; c < p; c += BLOCK) front_row(t, c, ell, B, U, f[3 * c], f[3 * c + 1], f[3 * c + 2]);
         __syncthreads();
         if (tid >= t.nr) return;
         const int r = t.r0 + tid;
-        const double* G = P.Gc + P.goff[s] + r;
+        const double* G = Gc + t.goff + r;
         const int cmax = r < p ? r + 1 : p;
         double a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll 8
@@ -82,20 +80,20 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(Plan P, const Task* __restrict__ 
             a0 += v * f[3 * c]; a1 += v * f[3 * c + 1]; a2 += v * f[3 * c + 2];
         }
         if (r < p) {
-            const size_t o = 3 * (size_t)(b0 + r);
+            const size_t o = 3 * (size_t)(t.beg + r);
             Y[o] = a0; Y[o + 1] = a1; Y[o + 2] = a2;
         } else {
             double f0, f1, f2;
-            front_row(P, s, r, B, U, f0, f1, f2);
-            double* u = U + P.uoff[s] + 3 * (size_t)(r - p);
+            front_row(t, r, ell, B, U, f0, f1, f2);
+            double* u = U + t.uoff + 3 * (size_t)(r - p);
             u[0] = f0 - a0; u[1] = f1 - a1; u[2] = f2 - a2;
         }
     } else {             // wave per row, lanes across the row of the row-major G, f from Fg
         const int lane = tid & 63, w = tid >> 6;
-        const double* F = Fg + P.foff[s];
+        const double* F = Fg + t.foff;
         for (int rr = w; rr < t.nr; rr += BLOCK / 64) {
             const int r = t.r0 + rr;
-            const double* row = P.Gr + P.goff[s] + (size_t)r * p;
+            const double* row = Gr + t.goff + (size_t)r * p;
             const int cmax = r < p ? r + 1 : p;
             double a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll 4
@@ -106,10 +104,10 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(Plan P, const Task* __restrict__ 
             a0 = wsum(a0); a1 = wsum(a1); a2 = wsum(a2);
             if (lane == 0) {
                 if (r < p) {
-                    const size_t o = 3 * (size_t)(b0 + r);
+                    const size_t o = 3 * (size_t)(t.beg + r);
                     Y[o] = a0; Y[o + 1] = a1; Y[o + 2] = a2;
                 } else {
-                    double* u = U + P.uoff[s] + 3 * (size_t)(r - p);
+                    double* u = U + t.uoff + 3 * (size_t)(r - p);
                     u[0] = F[3 * r] - a0; u[1] = F[3 * r + 1] - a1; u[2] = F[3 * r + 2] - a2;
                 }
             }
@@ -119,19 +117,20 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(Plan P, const Task* __restrict__ 
 
 // backward sweep of one tree level: x_P = Linv^T y_P - M^T x_B (columns j of G)
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_bwd(Plan P, const Task* __restrict__ tasks, int first,
+__global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, int first, const double* __restrict__ Gr,
+                                               const double* __restrict__ Gc, const int* __restrict__ bnd,
                                                const double* __restrict__ Y, double* __restrict__ X,
                                                const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Task t = tasks[first + blockIdx.x];
-    const int s = t.node, p = P.p[s], nb = P.nb[s], R = p + nb, b0 = P.beg[s];
-    const int* bi = P.bnd + P.bnd_off[s];
+    const int p = t.p, R = p + t.nb;
+    const int* bi = bnd + t.bnd_off;
     const int tid = threadIdx.x;
-    if (t.mode == 0) {   // thread per column, [y_P ; x_B] in LDS, row-major G (lanes read consecutive columns)
+    if (t.mode == 0) {   // thread per column, [y_P ; -x_B] in LDS, row-major G (lanes read consecutive columns)
         double* v = lds;
         for (int r = tid; r < R; r += BLOCK) {
-            const size_t o = r < p ? 3 * (size_t)(b0 + r) : 3 * (size_t)bi[r - p];
+            const size_t o = r < p ? 3 * (size_t)(t.beg + r) : 3 * (size_t)bi[r - p];
             const double sg = r < p ? 1.0 : -1.0;
             const double* src = r < p ? Y : X;
             v[3 * r] = sg * src[o]; v[3 * r + 1] = sg * src[o + 1]; v[3 * r + 2] = sg * src[o + 2];
@@ -139,26 +138,26 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(Plan P, const Task* __restrict__ 
         __syncthreads();
         if (tid >= t.nr) return;
         const int j = t.r0 + tid;
-        const double* G = P.Gr + P.goff[s] + j;
+        const double* G = Gr + t.goff + j;
         double a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll 8
         for (int r = j; r < R; ++r) {
             const double g = G[(size_t)r * p];
             a0 += g * v[3 * r]; a1 += g * v[3 * r + 1]; a2 += g * v[3 * r + 2];
         }
-        const size_t o = 3 * (size_t)(b0 + j);
+        const size_t o = 3 * (size_t)(t.beg + j);
         X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
     } else {             // wave per column, lanes down the column of the column-major G
         const int lane = tid & 63, w = tid >> 6;
         for (int jj = w; jj < t.nr; jj += BLOCK / 64) {
             const int j = t.r0 + jj;
-            const double* col = P.Gc + P.goff[s] + (size_t)j * R;
+            const double* col = Gc + t.goff + (size_t)j * R;
             double a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll 4
             for (int r = j + lane; r < R; r += 64) {
                 const double g = col[r];
                 if (r < p) {
-                    const size_t o = 3 * (size_t)(b0 + r);
+                    const size_t o = 3 * (size_t)(t.beg + r);
                     a0 += g * Y[o]; a1 += g * Y[o + 1]; a2 += g * Y[o + 2];
                 } else {
                     const size_t o = 3 * (size_t)bi[r - p];
@@ -167,10 +166,115 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(Plan P, const Task* __restrict__ 
             }
             a0 = wsum(a0); a1 = wsum(a1); a2 = wsum(a2);
             if (lane == 0) {
-                const size_t o = 3 * (size_t)(b0 + j);
+                const size_t o = 3 * (size_t)(t.beg + j);
                 X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
             }
         }
+    }
+}
+
+using SubNode = DirectSolver::SubNode;
+using SubLevel = DirectSolver::SubLevel;
+using SubTree = DirectSolver::SubTree;
+
+__device__ __forceinline__ void sub_front_row(const SubNode& t, int q, const long long* __restrict__ ell,
+                                              const double* __restrict__ B, const double* __restrict__ U, double& a0,
+                                              double& a1, double& a2) {
+    a0 = a1 = a2 = 0;
+    if (q < t.p) { const size_t o = 3 * (size_t)(t.beg + q); a0 = B[o]; a1 = B[o + 1]; a2 = B[o + 2]; }
+    const long long* e = ell + t.ell_off + (size_t)q * t.ell_w;
+    for (int k = 0; k < t.ell_w; ++k) {
+        const long long o = e[k];
+        if (o >= 0) { a0 += U[o]; a1 += U[o + 1]; a2 += U[o + 2]; }
+    }
+}
+
+// forward sweep of a whole bottom subtree (one workgroup), its levels bottom-up
+__global__ __launch_bounds__(256) void k_fwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
+                                                 const SubNode* __restrict__ nodes, const int* __restrict__ items,
+                                                 const double* __restrict__ Gc, const long long* __restrict__ ell,
+                                                 const double* __restrict__ B, double* __restrict__ Y,
+                                                 double* __restrict__ U, const Ctrl* ctrl, int gate_reject) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const SubTree T = trees[blockIdx.x];
+    const int tid = threadIdx.x;
+    for (int l = 0; l < T.nlvl; ++l) {
+        const SubLevel L = lvls[T.lvl0 + l];
+        for (int i = tid; i < L.nfa; i += 256) {          // front vectors f_P of the level's supernodes
+            const int it = items[L.fa0 + i];
+            const SubNode nd = nodes[L.n0 + (it >> 16)];
+            const int c = it & 0xffff;
+            double* f = lds + nd.lds + 3 * c;
+            sub_front_row(nd, c, ell, B, U, f[0], f[1], f[2]);
+        }
+        __syncthreads();
+        for (int i = tid; i < L.nfr; i += 256) {          // rows of G . f_P
+            const int it = items[L.fr0 + i];
+            const SubNode nd = nodes[L.n0 + (it >> 16)];
+            const int r = it & 0xffff, p = nd.p, R = p + nd.nb;
+            const double* f = lds + nd.lds;
+            const double* G = Gc + nd.goff + r;
+            const int cmax = r < p ? r + 1 : p;
+            double a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll 8
+            for (int c = 0; c < cmax; ++c) {
+                const double v = G[(size_t)c * R];
+                a0 += v * f[3 * c]; a1 += v * f[3 * c + 1]; a2 += v * f[3 * c + 2];
+            }
+            if (r < p) {
+                const size_t o = 3 * (size_t)(nd.beg + r);
+                Y[o] = a0; Y[o + 1] = a1; Y[o + 2] = a2;
+            } else {
+                double f0, f1, f2;
+                sub_front_row(nd, r, ell, B, U, f0, f1, f2);
+                double* u = U + nd.uoff + 3 * (size_t)(r - p);
+                u[0] = f0 - a0; u[1] = f1 - a1; u[2] = f2 - a2;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// backward sweep of a whole bottom subtree (one workgroup), its levels top-down
+__global__ __launch_bounds__(256) void k_bwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
+                                                 const SubNode* __restrict__ nodes, const int* __restrict__ items,
+                                                 const double* __restrict__ Gr, const int* __restrict__ bnd,
+                                                 const double* __restrict__ Y, double* __restrict__ X,
+                                                 const Ctrl* ctrl, int gate_reject) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const SubTree T = trees[blockIdx.x];
+    const int tid = threadIdx.x;
+    for (int l = T.nlvl - 1; l >= 0; --l) {
+        const SubLevel L = lvls[T.lvl0 + l];
+        for (int i = tid; i < L.nbv; i += 256) {          // [y_P ; -x_B] of the level's supernodes
+            const int it = items[L.bv0 + i];
+            const SubNode nd = nodes[L.n0 + (it >> 16)];
+            const int r = it & 0xffff;
+            const size_t o = r < nd.p ? 3 * (size_t)(nd.beg + r) : 3 * (size_t)bnd[nd.bnd_off + r - nd.p];
+            const double sg = r < nd.p ? 1.0 : -1.0;
+            const double* src = r < nd.p ? Y : X;
+            double* v = lds + nd.lds + 3 * r;
+            v[0] = sg * src[o]; v[1] = sg * src[o + 1]; v[2] = sg * src[o + 2];
+        }
+        __syncthreads();
+        for (int i = tid; i < L.nbc; i += 256) {          // columns of G^T . v
+            const int it = items[L.bc0 + i];
+            const SubNode nd = nodes[L.n0 + (it >> 16)];
+            const int j = it & 0xffff, p = nd.p, R = p + nd.nb;
+            const double* v = lds + nd.lds;
+            const double* G = Gr + nd.goff + j;
+            double a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll 8
+            for (int r = j; r < R; ++r) {
+                const double g = G[(size_t)r * p];
+                a0 += g * v[3 * r]; a1 += g * v[3 * r + 1]; a2 += g * v[3 * r + 2];
+            }
+            const size_t o = 3 * (size_t)(nd.beg + j);
+            X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
+        }
+        __syncthreads();
     }
 }
 
@@ -226,7 +330,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
         for (int r = 0; r < R; ++r)
             for (int c = 0; c < ps; ++c) gc[(size_t)c * R + r] = gr[(size_t)r * ps + c];
     }
-    // children lists and pull lists (front row q of a parent <- child update entries, fixed order)
+    // children lists and ELL pull lists (front row q of a parent <- child update entries, fixed order)
     std::vector<std::vector<int>> kl(nn_);
     for (int sn = 0; sn < nn_; ++sn) if (F.parent[sn] >= 0) kl[F.parent[sn]].push_back(sn);
     std::vector<std::vector<long long>> pull(rows_total);
@@ -246,57 +350,178 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
             }
         }
     }
-    std::vector<int> pptr(rows_total + 1, 0);
-    std::vector<long long> psrc;
-    for (int r = 0; r < rows_total; ++r) {
-        psrc.insert(psrc.end(), pull[r].begin(), pull[r].end());
-        pptr[r + 1] = (int)psrc.size();
+    std::vector<int> ell_w(nn_, 0);
+    std::vector<long long> ell_off(nn_, 0), ell;
+    for (int sn = 0; sn < nn_; ++sn) {
+        const int R = p[sn] + nb[sn];
+        int w = 0;
+        for (int q = 0; q < R; ++q) w = std::max(w, (int)pull[pull_off[sn] + q].size());
+        ell_w[sn] = w;
+        ell_off[sn] = (long long)ell.size();
+        for (int q = 0; q < R; ++q) {
+            const auto& l = pull[pull_off[sn] + q];
+            for (int k = 0; k < w; ++k) ell.push_back(k < (int)l.size() ? l[k] : -1);
+        }
+    }
+    // ---- fused bottom subtrees: the largest cut height H such that at least `min_sub`
+    // subtrees root at height <= H (enough workgroups to fill the chip) and every subtree level
+    // fits the LDS budget; supernodes above H are solved level by level.
+    std::vector<std::vector<int>> kids(nn_);
+    for (int sn = 0; sn < nn_; ++sn) if (F.parent[sn] >= 0) kids[F.parent[sn]].push_back(sn);
+    const char* ms = std::getenv("AA_SOLVE_MIN_SUBTREES");
+    const int min_sub = ms ? std::atoi(ms) : 96;
+    constexpr int kSubLds = 64 * 1024, kMaxItemRow = 0xffff;
+    auto roots_at = [&](int H) {
+        std::vector<int> r;
+        for (int sn = 0; sn < nn_; ++sn)
+            if (F.height[sn] <= H && (F.parent[sn] < 0 || F.height[F.parent[sn]] > H)) r.push_back(sn);
+        return r;
+    };
+    auto collect = [&](int root) {
+        std::vector<int> out, st{root};
+        while (!st.empty()) { int v = st.back(); st.pop_back(); out.push_back(v); for (int c : kids[v]) st.push_back(c); }
+        return out;
+    };
+    cut_height_ = -1;
+    for (int H = F.max_height - 1; H >= 1; --H) {
+        std::vector<int> r = roots_at(H);
+        if ((int)r.size() < min_sub) continue;
+        bool ok = true;
+        for (int rt : r) {
+            std::vector<long long> lf(H + 1, 0), lb(H + 1, 0), nodes_at(H + 1, 0);
+            for (int v : collect(rt)) {
+                lf[F.height[v]] += 24LL * p[v];
+                lb[F.height[v]] += 24LL * (p[v] + nb[v]);
+                nodes_at[F.height[v]] += 1;
+                if (p[v] + nb[v] > kMaxItemRow) ok = false;
+            }
+            for (int h = 0; h <= H; ++h) if (lf[h] > kSubLds || lb[h] > kSubLds || nodes_at[h] > kMaxItemRow) ok = false;
+            if (!ok) break;
+        }
+        if (ok) { cut_height_ = H; break; }
+    }
+    std::vector<char> fused(nn_, 0);
+    {
+        std::vector<SubNode> snodes;
+        std::vector<SubLevel> slevels;
+        std::vector<SubTree> strees;
+        std::vector<int> items;
+        sub_lds_f_ = sub_lds_b_ = 0;
+        if (cut_height_ >= 0) {
+            for (int rt : roots_at(cut_height_)) {
+                std::vector<int> all = collect(rt);
+                const int H = F.height[rt];
+                SubTree T{(int)slevels.size(), H + 1};
+                for (int h = 0; h <= H; ++h) {
+                    SubLevel L{};
+                    L.n0 = (int)snodes.size();
+                    int lf = 0, lb = 0;
+                    std::vector<int> lv;
+                    for (int v : all) if (F.height[v] == h) lv.push_back(v);
+                    std::sort(lv.begin(), lv.end());
+                    for (int v : lv) {
+                        fused[v] = 1;
+                        SubNode nd{};
+                        nd.p = p[v]; nd.nb = nb[v]; nd.beg = beg[v]; nd.bnd_off = bnd_off[v]; nd.ell_w = ell_w[v];
+                        nd.lds = 0; nd.goff = goff[v]; nd.uoff = uoff[v]; nd.ell_off = ell_off[v];
+                        snodes.push_back(nd);
+                    }
+                    // forward: f_P offsets, assembly items, row items
+                    L.fa0 = (int)items.size();
+                    for (size_t k = 0; k < lv.size(); ++k) {
+                        snodes[L.n0 + k].lds = lf / 8;
+                        for (int c = 0; c < p[lv[k]]; ++c) items.push_back(((int)k << 16) | c);
+                        lf += 24 * p[lv[k]];
+                    }
+                    L.nfa = (int)items.size() - L.fa0;
+                    L.fr0 = (int)items.size();
+                    for (size_t k = 0; k < lv.size(); ++k)
+                        for (int r = 0; r < p[lv[k]] + nb[lv[k]]; ++r) items.push_back(((int)k << 16) | r);
+                    L.nfr = (int)items.size() - L.fr0;
+                    // backward: the same supernodes with their [y_P ; -x_B] vectors; the LDS
+                    // offsets differ, so the backward items address a second copy of the nodes
+                    const int n1 = (int)snodes.size();
+                    for (size_t k = 0; k < lv.size(); ++k) {
+                        SubNode nd = snodes[L.n0 + k];
+                        nd.lds = lb / 8;
+                        lb += 24 * (p[lv[k]] + nb[lv[k]]);
+                        snodes.push_back(nd);
+                    }
+                    L.bv0 = (int)items.size();
+                    for (size_t k = 0; k < lv.size(); ++k)
+                        for (int r = 0; r < p[lv[k]] + nb[lv[k]]; ++r) items.push_back(((int)(k + (n1 - L.n0)) << 16) | r);
+                    L.nbv = (int)items.size() - L.bv0;
+                    L.bc0 = (int)items.size();
+                    for (size_t k = 0; k < lv.size(); ++k)
+                        for (int j = 0; j < p[lv[k]]; ++j) items.push_back(((int)(k + (n1 - L.n0)) << 16) | j);
+                    L.nbc = (int)items.size() - L.bc0;
+                    sub_lds_f_ = std::max(sub_lds_f_, lf);
+                    sub_lds_b_ = std::max(sub_lds_b_, lb);
+                    slevels.push_back(L);
+                }
+                strees.push_back(T);
+            }
+        }
+        n_sub_ = (int)strees.size();
+        sub_nodes_.upload(snodes, s);
+        sub_levels_.upload(slevels, s);
+        sub_trees_.upload(strees, s);
+        sub_items_.upload(items, s);
     }
     // levels by height and their row tasks
     std::vector<std::vector<int>> hl(F.max_height + 1);
-    for (int sn = 0; sn < nn_; ++sn) hl[F.height[sn]].push_back(sn);
+    for (int sn = 0; sn < nn_; ++sn) if (!fused[sn]) hl[F.height[sn]].push_back(sn);
     std::vector<Task> tasks;
+    auto mk = [&](int sn, int r0, int nr, int mode) {
+        Task t{};
+        t.node = sn; t.r0 = r0; t.nr = nr; t.mode = mode;
+        t.p = p[sn]; t.nb = nb[sn]; t.beg = beg[sn]; t.bnd_off = bnd_off[sn];
+        t.ell_w = ell_w[sn];
+        t.goff = goff[sn]; t.uoff = uoff[sn]; t.foff = foff[sn]; t.ell_off = ell_off[sn];
+        return t;
+    };
     levels_.clear();
     kernels_ = 0;
     int max_lds = 0;
     for (auto& l : hl) {
         if (l.empty()) continue;
         Level L;
-        int max_rows0 = 0;
-        bool any_wave = false;
-        std::vector<int> wave;
+        int fr = 0, br = 0;
+        bool fwave = false, bwave = false;
         for (int sn : l) {
-            const bool m0 = p[sn] <= kWaveP && 24 * (p[sn] + nb[sn]) <= kMaxLdsMode0;
-            if (m0) max_rows0 = std::max(max_rows0, std::max(p[sn] + nb[sn], p[sn]));
-            else { any_wave = true; wave.push_back(sn); }
+            const int R = p[sn] + nb[sn];
+            if (p[sn] <= kWaveP) fr = std::max(fr, R); else fwave = true;
+            if (R <= kWaveR) br = std::max(br, p[sn]); else bwave = true;
         }
-        L.block = (any_wave || max_rows0 > 128) ? 256 : (max_rows0 > 64 ? 128 : 64);
-        // assembly tasks of wave-mode supernodes
+        L.fblock = (fwave || fr > 128) ? 256 : (fr > 64 ? 128 : 64);
+        L.bblock = (bwave || br > 128) ? 256 : (br > 64 ? 128 : 64);
         L.asm_first = (int)tasks.size();
-        for (int sn : wave) {
+        for (int sn : l) {
+            if (p[sn] <= kWaveP) continue;
             foff[sn] = fo;
             fo += 3LL * (p[sn] + nb[sn]);
-            for (int r0 = 0; r0 < p[sn] + nb[sn]; r0 += 256) tasks.push_back({sn, r0, std::min(256, p[sn] + nb[sn] - r0), 1});
+            for (int r0 = 0; r0 < p[sn] + nb[sn]; r0 += 256) tasks.push_back(mk(sn, r0, std::min(256, p[sn] + nb[sn] - r0), 1));
         }
         L.asm_count = (int)tasks.size() - L.asm_first;
         L.fwd_first = (int)tasks.size();
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
-            if (foff[sn] < 0) {
-                for (int r0 = 0; r0 < R; r0 += L.block) tasks.push_back({sn, r0, std::min(L.block, R - r0), 0});
+            if (p[sn] <= kWaveP) {
+                for (int r0 = 0; r0 < R; r0 += L.fblock) tasks.push_back(mk(sn, r0, std::min(L.fblock, R - r0), 0));
                 L.lds_fwd = std::max(L.lds_fwd, 24 * p[sn]);
             } else {
-                for (int r0 = 0; r0 < R; r0 += kWaveRowsPerTask) tasks.push_back({sn, r0, std::min(kWaveRowsPerTask, R - r0), 1});
+                for (int r0 = 0; r0 < R; r0 += kWaveRowsPerTask) tasks.push_back(mk(sn, r0, std::min(kWaveRowsPerTask, R - r0), 1));
             }
         }
         L.fwd_count = (int)tasks.size() - L.fwd_first;
         L.bwd_first = (int)tasks.size();
         for (int sn : l) {
-            if (foff[sn] < 0) {
-                for (int j0 = 0; j0 < p[sn]; j0 += L.block) tasks.push_back({sn, j0, std::min(L.block, p[sn] - j0), 0});
-                L.lds_bwd = std::max(L.lds_bwd, 24 * (p[sn] + nb[sn]));
+            const int R = p[sn] + nb[sn];
+            if (R <= kWaveR) {
+                for (int j0 = 0; j0 < p[sn]; j0 += L.bblock) tasks.push_back(mk(sn, j0, std::min(L.bblock, p[sn] - j0), 0));
+                L.lds_bwd = std::max(L.lds_bwd, 24 * R);
             } else {
-                for (int j0 = 0; j0 < p[sn]; j0 += kWaveRowsPerTask) tasks.push_back({sn, j0, std::min(kWaveRowsPerTask, p[sn] - j0), 1});
+                for (int j0 = 0; j0 < p[sn]; j0 += kWaveRowsPerTask) tasks.push_back(mk(sn, j0, std::min(kWaveRowsPerTask, p[sn] - j0), 1));
             }
         }
         L.bwd_count = (int)tasks.size() - L.bwd_first;
@@ -304,9 +529,9 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
         kernels_ += 2 + (L.asm_count ? 1 : 0);
         levels_.push_back(L);
     }
-    beg_.upload(beg, s); p_.upload(p, s); nb_.upload(nb, s);
-    bnd_off_.upload(bnd_off, s); bnd_.upload(bnd, s); pull_off_.upload(pull_off, s); pptr_.upload(pptr, s);
-    goff_.upload(goff, s); uoff_.upload(uoff, s); foff_.upload(foff, s); psrc_.upload(psrc, s);
+    if (n_sub_) kernels_ += 2;
+    bnd_.upload(bnd, s);
+    ell_.upload(ell, s);
     Gr_.upload(Gr, s); Gc_.upload(Gc, s);
     tasks_.upload(tasks, s);
     Y_.alloc(3 * (size_t)n_);
@@ -324,26 +549,26 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
 }
 
 void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
-    Plan P{beg_.p, p_.p, nb_.p, bnd_off_.p, bnd_.p, pull_off_.p, pptr_.p, psrc_.p,
-           goff_.p, uoff_.p, foff_.p, Gr_.p, Gc_.p};
     const Task* T = tasks_.p;
+    if (n_sub_)
+        hipLaunchKernelGGL(k_fwd_sub, dim3(n_sub_), dim3(256), sub_lds_f_, s, sub_trees_.p, sub_levels_.p, sub_nodes_.p,
+                           sub_items_.p, Gc_.p, ell_.p, b, Y_.p, U_.p, ctrl, gate_reject);
     for (auto& L : levels_) {
         if (L.asm_count)
-            hipLaunchKernelGGL(k_asm, dim3(L.asm_count), dim3(256), 0, s, P, T, L.asm_first, b, U_.p, Fg_.p, ctrl, gate_reject);
-        switch (L.block) {
-            case 64: hipLaunchKernelGGL(k_fwd<64>, dim3(L.fwd_count), dim3(64), L.lds_fwd, s, P, T, L.fwd_first, b, Y_.p, U_.p, Fg_.p, ctrl, gate_reject); break;
-            case 128: hipLaunchKernelGGL(k_fwd<128>, dim3(L.fwd_count), dim3(128), L.lds_fwd, s, P, T, L.fwd_first, b, Y_.p, U_.p, Fg_.p, ctrl, gate_reject); break;
-            default: hipLaunchKernelGGL(k_fwd<256>, dim3(L.fwd_count), dim3(256), L.lds_fwd, s, P, T, L.fwd_first, b, Y_.p, U_.p, Fg_.p, ctrl, gate_reject); break;
-        }
+            hipLaunchKernelGGL(k_asm, dim3(L.asm_count), dim3(256), 0, s, T, L.asm_first, ell_.p, b, U_.p, Fg_.p, ctrl, gate_reject);
+#define FWD(BL) hipLaunchKernelGGL(k_fwd<BL>, dim3(L.fwd_count), dim3(BL), L.lds_fwd, s, T, L.fwd_first, Gr_.p, Gc_.p, ell_.p, b, Y_.p, U_.p, Fg_.p, ctrl, gate_reject)
+        switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
+#undef FWD
     }
     for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
         const Level& L = *it;
-        switch (L.block) {
-            case 64: hipLaunchKernelGGL(k_bwd<64>, dim3(L.bwd_count), dim3(64), L.lds_bwd, s, P, T, L.bwd_first, Y_.p, x, ctrl, gate_reject); break;
-            case 128: hipLaunchKernelGGL(k_bwd<128>, dim3(L.bwd_count), dim3(128), L.lds_bwd, s, P, T, L.bwd_first, Y_.p, x, ctrl, gate_reject); break;
-            default: hipLaunchKernelGGL(k_bwd<256>, dim3(L.bwd_count), dim3(256), L.lds_bwd, s, P, T, L.bwd_first, Y_.p, x, ctrl, gate_reject); break;
-        }
+#define BWD(BL) hipLaunchKernelGGL(k_bwd<BL>, dim3(L.bwd_count), dim3(BL), L.lds_bwd, s, T, L.bwd_first, Gr_.p, Gc_.p, bnd_.p, Y_.p, x, ctrl, gate_reject)
+        switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
+#undef BWD
     }
+    if (n_sub_)
+        hipLaunchKernelGGL(k_bwd_sub, dim3(n_sub_), dim3(256), sub_lds_b_, s, sub_trees_.p, sub_levels_.p, sub_nodes_.p,
+                           sub_items_.p, Gr_.p, bnd_.p, Y_.p, x, ctrl, gate_reject);
     AA_CHECK_LAUNCH();
 }
 

@@ -28,7 +28,8 @@ namespace aa {
 class DirectSolver {
 public:
     static constexpr int kTopRows = 2048;    // upper tree levels amalgamated into one dense root
-    static constexpr int kWaveP = 192;       // supernodes with p above this use wave-per-row tasks
+    static constexpr int kWaveP = 192;       // forward rows longer than this: wave per row
+    static constexpr int kWaveR = 384;       // backward columns longer than this: wave per column
 
     void build(const SupernodalFactor& F, hipStream_t s);
     // x (n x 3, stride 3 doubles) = A^-1 b ; b is read only. gate: skip when ctrl->done (or !reject).
@@ -38,22 +39,45 @@ public:
     double bytes_per_solve() const { return bytes_; }
     int kernels_per_solve() const { return kernels_; }
 
-    struct Task { int node, r0, nr, mode; };   // mode 0: thread per row, 1: wave per row
+    // One workgroup's share of a level: rows [r0, r0 + nr) of supernode `node` (forward) or
+    // its columns (backward). mode 0: thread per row, 1: wave per row. The supernode's
+    // metadata rides along so a workgroup needs one (scalar) load before its first product.
+    struct Task {
+        int node, r0, nr, mode;
+        int p, nb, beg, bnd_off;
+        int ell_w, pad0, pad1, pad2;
+        long long goff, uoff, foff, ell_off;
+    };
+
+    // Bottom subtrees (all supernodes up to a cut height) are solved whole by one workgroup
+    // each: their levels are separated by workgroup barriers instead of kernel boundaries.
+    struct SubNode {   // a supernode inside a fused subtree; lds = its vector's offset in LDS
+        int p, nb, beg, bnd_off, ell_w, lds, pad0, pad1;
+        long long goff, uoff, ell_off;
+    };
+    struct SubLevel { int n0, fa0, nfa, fr0, nfr, bv0, nbv, bc0, nbc, pad; };   // item ranges
+    struct SubTree { int lvl0, nlvl; };
 
 private:
     struct Level {
         int fwd_first = 0, fwd_count = 0, bwd_first = 0, bwd_count = 0;
         int asm_first = 0, asm_count = 0;     // assembly tasks of the wave-mode supernodes
-        int block = 256, lds_fwd = 0, lds_bwd = 0;
+        int fblock = 256, bblock = 256, lds_fwd = 0, lds_bwd = 0;
     };
     int n_ = 0, nn_ = 0, kernels_ = 0;
     size_t nnz_L_ = 0;
     double bytes_ = 0;
-    DevBuf<int> beg_, p_, nb_, bnd_off_, bnd_, pull_off_, pptr_;
-    DevBuf<long long> goff_, uoff_, foff_, psrc_;
+    DevBuf<int> bnd_;
+    DevBuf<long long> ell_;   // per front row, ell_w pull offsets into U (-1 = none)
     DevBuf<double> Gr_, Gc_, Y_, U_, Fg_;
     DevBuf<Task> tasks_;
     std::vector<Level> levels_;
+    // fused bottom subtrees
+    int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1;
+    DevBuf<SubNode> sub_nodes_;
+    DevBuf<SubLevel> sub_levels_;
+    DevBuf<SubTree> sub_trees_;
+    DevBuf<int> sub_items_;   // (local node << 16 | row) per item
 };
 
 }  // namespace aa

@@ -1,0 +1,20 @@
+"""Per-launch durations of the last global solve in a rocprofv3 kernel trace (NO_GRAPH runs)."""
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+names = [r["Kernel_Name"] for r in rows]
+idx = set(i for i, n in enumerate(names) if "k_fwd" in n or "k_bwd" in n or "k_asm" in n)
+end = max(idx)
+start = end
+while start - 1 in idx:
+    start -= 1
+tot = 0
+for r in rows[start:end + 1]:
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
+    tot += d
+    nm = r["Kernel_Name"].split("::")[-1].split("(")[0]
+    print("  %-14s grid %8d wg %4s lds %6s vgpr %3s %7.2f us" % (nm, int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]),
+          r["Workgroup_Size_X"], r["LDS_Block_Size"], r["VGPR_Count"], d))
+print(" kernels", end - start + 1, "sum %.1f us, wall %.1f us" % (tot, (int(rows[end]["End_Timestamp"]) - int(rows[start]["Start_Timestamp"])) / 1000))
