@@ -218,9 +218,9 @@ def solver_from_scene(ctx: Context, scene) -> Solver:
     for g in scene.groups:
         lame = Lame.from_young(g.E, g.nu, g.limit_min, g.limit_max)
         if g.kind == 0:
-            s.add_tets(scene.x, g.idx, g.material, lame)
+            s.add_tets(scene.rest_x, g.idx, g.material, lame)
         else:
-            s.add_tris(scene.x, g.idx, lame)
+            s.add_tris(scene.rest_x, g.idx, lame)
     s.set_pins(scene.pin_idx, scene.pin_pts)
     return s
 

@@ -351,6 +351,20 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     kstats_["resid"].bytes = rs + 48.0 * n;
     kstats_["solve"].bytes = solver_.bytes_per_solve();
     kstats_["rhs"].bytes = 12.0 * (double)dt_row_.n + 8.0 * Z_ + 48.0 * nf_;
+    // Z variant: u = W^-1 grad E(z) and y rows (reads idx, G, w, z; writes u, y), prim (reads
+    // idx, G, w, z, u; writes block partials)
+    double gy = 0, pr = 0;
+    for (auto& g : groups_) {
+        const double per = 4.0 * g.d.nv + 8.0 * g.d.ncol * g.d.nv + 8.0;
+        gy += g.d.count * (per + 8.0 * 3 * g.d.dim);
+        pr += g.d.count * (per + 8.0 * 2 * g.d.dim);
+    }
+    kstats_["grad"].bytes = gy + 24.0 * n;
+    kstats_["prim"].bytes = pr + 24.0 * n;
+    if (accel) {   // Anderson: ~ 8 d (2m + 8) bytes per iteration (history read/write + vectors)
+        const double d = st_.variant == AA_VARIANT_UX ? (double)Z_ + 3.0 * nf_ : (double)Z_;
+        kstats_["aa"].bytes = 8.0 * d * (2.0 * st_.anderson_m + 8.0);
+    }
 }
 
 void ElasticSolver::upload_pins() {
@@ -474,8 +488,12 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
 void ElasticSolver::enqueue_iteration_z(bool accel) {
     const long long nx = 3LL * nf_;
     Ctrl* c = ctrl_.p;
+    ev_begin("grad");
     for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, accel ? 1 : 0, 0, c, s());
+    ev_end("grad");
+    ev_begin("rhs");
     launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+    ev_end("rhs");
     ev_begin("solve");
     solver_.solve(b_.p, xfull_.p, c, 0, s());
     ev_end("solve");
@@ -486,9 +504,11 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
             off += blocks_for(g.d.count);
         }
     };
+    ev_begin("prim");
     prim_all(xfull_.p, z_.p, nullptr, 0);
+    ev_end("prim");
     launch_control(CTL_PRIM_CHECK_Z, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
-    if (accel) {
+    if (accel) {   // reject branch (gated on the device; a no-op unless prim increased)
         launch_copy(u_.p, du_.p, Z_, c, 1, s());
         launch_copy(xfull_.p, dx_.p, nx, c, 1, s());
         launch_copy(z_.p, dz_.p, Z_, c, 1, s());
@@ -503,7 +523,9 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         const int m = st_.anderson_m;
         launch_copy(dx_.p, xfull_.p, nx, c, 0, s());
         launch_copy(du_.p, u_.p, Z_, c, 0, s());
+        ev_begin("local_z");
         local_z_all(xfull_.p, u_.p, dz_.p, nullptr, LZ_NORMAL, false);
+        ev_end("local_z");
         Seg2 G{dz_.p, Z_, nullptr, 0};
         Seg2 out{z_.p, Z_, nullptr, 0};
         Seg2 none{nullptr, 0, nullptr, 0};
@@ -513,14 +535,18 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         launch_aa_mix(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, out, m, s());
         ev_end("aa");
         // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
+        ev_begin("comb");
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, dz_.p, u_.p, y_.p, nf_, 2, 0, c, s());
         launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
         solver_.solve(b_.p, cxfull_.p, c, 0, s());
         local_z_all(cxfull_.p, u_.p, cz_.p, nullptr, LZ_NORMAL, false);
         prim_all(cxfull_.p, cz_.p, dz_.p, 0);
+        ev_end("comb");
     } else {
         launch_copy(lastz_.p, z_.p, Z_, c, 0, s());
+        ev_begin("local_z");
         local_z_all(xfull_.p, u_.p, z_.p, nullptr, LZ_NORMAL, false);
+        ev_end("local_z");
         prim_all(xfull_.p, z_.p, lastz_.p, 0);
     }
     launch_control(CTL_COMB_Z, c, red_a_.p, red_b_.p, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());

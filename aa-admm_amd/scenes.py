@@ -26,7 +26,7 @@ from __future__ import annotations
 
 import dataclasses
 import struct
-from typing import List
+from typing import List, Optional
 
 import numpy as np
 
@@ -70,6 +70,11 @@ class Scene:
     aa_m: int = 6
     n_steps: int = 1
     name: str = "scene"
+    rest: Optional[np.ndarray] = None   # (n, 3) rest positions of the elements; None = x
+
+    @property
+    def rest_x(self) -> np.ndarray:
+        return self.x if self.rest is None else self.rest
 
     @property
     def n_nodes(self) -> int:
@@ -182,6 +187,25 @@ def cantilever(cx=20, cy=4, cz=5, material=NEOHOOKEAN, *, variant=VARIANT_X, aa_
                  iters=iters, aa_m=aa_m, n_steps=n_steps, accel=accel, name=f"cantilever{cx}x{cy}x{cz}")
 
 
+def tet_drop(cx=100, cy=40, cz=50, material=NEOHOOKEAN, *, squash=0.9, variant=VARIANT_X, aa_m=6, iters=100,
+             n_steps=1, accel=1, E=1e7, nu=0.399) -> Scene:
+    """C4: elastic block free fall, `make_tet_blocks(cx, cy, cz)` (5 tets per cube; 100x40x50 =
+    1 000 000 tets, 211 191 nodes) scaled by 1/cy, density 1522, NeoHookean Lame(1e7, 0.399).
+    No pins, no collisions; the initial pose is the rest shape squashed to `squash` in y so that
+    the elastic prox has work (a rigid free fall converges trivially) -- SURVEY.md §8d C4.
+    The z-AA (X) order, as BASELINE.json asks (the (u,x) order goes NaN on large-deformation
+    NeoHookean scenes)."""
+    v, t = tet_blocks(cx, cy, cz)
+    v = v / float(cy)
+    m = tet_masses(v, t, 1522.0)
+    x = v.copy()
+    c = 0.5 * (v[:, 1].min() + v[:, 1].max())
+    x[:, 1] = c + squash * (v[:, 1] - c)
+    return Scene(x=x, masses=m, groups=[ElementGroup(TET, material, E, nu, t)], pin_idx=np.zeros(0, np.int32),
+                 pin_pts=np.zeros((0, 3)), pin_vel=np.zeros((0, 3)), variant=variant, iters=iters, aa_m=aa_m,
+                 n_steps=n_steps, accel=accel, name=f"drop{cx}x{cy}x{cz}", rest=v)
+
+
 def beams(dim=3, *, variant=VARIANT_X, aa_m=6, iters=100, n_steps=1, accel=1, materials=(LINEAR, NEOHOOKEAN, STVK)) -> Scene:
     """C1 beams: three make_tet_blocks(4*dim, dim, dim) beams, 1 m tall, at y = +1.75 / 0 / -1.75,
     Lame(1e7, 0.399), x-extreme faces pinned and pulled apart by dt per step
@@ -216,9 +240,11 @@ def beams(dim=3, *, variant=VARIANT_X, aa_m=6, iters=100, n_steps=1, accel=1, ma
 
 def write_scene(scene: Scene, path: str) -> None:
     with open(path, "wb") as f:
-        f.write(b"AASCENE1")
+        f.write(b"AASCENE1" if scene.rest is None else b"AASCENE2")
         f.write(struct.pack("<ii", scene.variant, scene.n_nodes))
         f.write(np.ascontiguousarray(scene.x, dtype="<f8").tobytes())
+        if scene.rest is not None:
+            f.write(np.ascontiguousarray(scene.rest, dtype="<f8").tobytes())
         f.write(np.repeat(np.asarray(scene.masses, dtype="<f8"), 3).tobytes())
         f.write(struct.pack("<i", len(scene.groups)))
         for g in scene.groups:

@@ -43,9 +43,10 @@ def parse():
     p.add_argument("--nx", type=int, default=112)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-iters", type=int, default=40)
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c5"],
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
                    help="c2: cloth (BASELINE configs[1], the headline); c3: planar-quad 317x317 (configs[2]); "
-                        "c5: wire mesh 707x707 (configs[4], single-GPU here)")
+                        "c4: 1M-tet NeoHookean block drop (configs[3]); c5: wire mesh 707x707 (configs[4])")
+    p.add_argument("--tets", type=str, default="100,40,50", help="c4 block size in cubes (5 tets per cube)")
     return p.parse_args()
 
 
@@ -86,19 +87,21 @@ def time_to_eps(comb, step_ms, iters_run):
     return (hit[0] + 1) * step_ms / iters_run
 
 
-def cpu_baseline(scene_builder, iters):
-    """The REFERENCE (oracle/_ref/ref_elastic_h, compiled from the reference's own sources)
-    on the host cores, bounded sample: 3 time steps x `iters` ADMM iterations of the same scene;
-    the first step (OpenMP spin-up, Anderson allocation) is excluded."""
+def cpu_baseline(sc, scale=1.0, what=""):
+    """The REFERENCE (oracle/_ref/ref_elastic_{h,x}, compiled from the reference's own sources)
+    on the host cores, bounded sample `sc` (3 time steps); the first step (OpenMP spin-up,
+    Anderson allocation) is excluded. `scale` converts the sample's iters/s to the bench
+    workload (element ratio, for samples smaller than the workload)."""
     scenes = importlib.import_module("aa-admm_amd.scenes")
-    sc = scene_builder(iters=iters, n_steps=3)
-    drv = os.path.join(REPO, "oracle", "_ref", "ref_elastic_h")
+    drv = os.path.join(REPO, "oracle", "_ref", "ref_elastic_h" if sc.variant == scenes.VARIANT_H else "ref_elastic_x")
     threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
     with tempfile.TemporaryDirectory() as tmp:
         scenes.write_scene(sc, os.path.join(tmp, "s.bin"))
         if os.path.exists(drv):
             env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-            r = subprocess.run([drv, "s.bin", "o.bin"], cwd=tmp, capture_output=True, text=True, env=env, timeout=600)
+            t0 = time.time()
+            r = subprocess.run([drv, "s.bin", "o.bin"], cwd=tmp, capture_output=True, text=True, env=env, timeout=900)
+            wall = time.time() - t0
             if r.returncode != 0:
                 raise RuntimeError(r.stderr[-500:])
             steps = scenes.read_ref_result(os.path.join(tmp, "o.bin"), sc.n_nodes)
@@ -106,12 +109,19 @@ def cpu_baseline(scene_builder, iters):
         else:  # reference binary absent: time our own C++ restatement instead
             sys.path.insert(0, os.path.join(REPO, "oracle"))
             import pyoracle
+            t0 = time.time()
             steps = pyoracle.run_elastic(sc)
+            wall = time.time() - t0
             kind, threads = "port", 1
     per = [len(s["prim"]) / (s["step_ms"] / 1000.0) for s in steps[1:]]
-    return {"value": round(statistics.median(per), 3), "unit": "ADMM iters/s", "cores": threads, "kind": kind,
-            "sample": f"cloth {sc.name} (50176 tris at 112x112), 3 steps x {iters} ADMM iters, (u,x)-AA m=6; "
-                      f"median iters/s of steps 2-3 (step 1 = warm-up), OMP_NUM_THREADS={threads}"}
+    raw = statistics.median(per)
+    out = {"value": round(raw * scale, 3), "unit": "ADMM iters/s", "cores": threads, "kind": kind,
+           "sample": f"{sc.name} ({sc.n_elements()} elements), {sc.n_steps} steps x {sc.iters} ADMM iters, "
+                     f"m={sc.aa_m}; median iters/s of steps 2-{sc.n_steps} (step 1 = warm-up), "
+                     f"OMP_NUM_THREADS={threads}; total wall incl. setup {wall:.1f} s{what}"}
+    if scale != 1.0:
+        out["sample_value"] = round(raw, 3)
+    return out
 
 
 def geom_scene(args):
@@ -219,19 +229,45 @@ def main_geom(args, world, rank, local, dist):
         dist.destroy_process_group()
 
 
+def elastic_scene(args, iters=None, n_steps=1):
+    scenes = importlib.import_module("aa-admm_amd.scenes")
+    it = args.iters if iters is None else iters
+    if args.config == "c4":
+        cx, cy, cz = (int(v) for v in args.tets.split(","))
+        sc = scenes.tet_drop(cx, cy, cz, iters=it, n_steps=n_steps)
+        return sc, (f"NeoHookean block free fall make_tet_blocks({cx},{cy},{cz}) {sc.n_elements()} tets, "
+                    f"{sc.n_nodes} nodes, squashed 0.9 in y, z-AA (X order) m=6, {it} ADMM iters/step, dt=1/30 "
+                    f"(BASELINE configs[3])")
+    sc = scenes.cloth(args.nx, args.nx, iters=it, n_steps=n_steps)
+    return sc, (f"cloth drop make_tri_blocks({args.nx},{args.nx}) {sc.n_elements()} tris, (u,x)-AA m=6, "
+                f"{it} ADMM iters/step, dt=1/30 (BASELINE configs[1])")
+
+
+def elastic_cpu_baseline(args):
+    scenes = importlib.import_module("aa-admm_amd.scenes")
+    if args.config == "c4":
+        # the reference cannot factor the 1M-tet system within a bench run (Eigen SimplicialLDLT
+        # of ~633k dof: tens of minutes): a 64k-tet block of the same recipe,
+        # its iters/s scaled by the element ratio (linear extrapolation -- favours the CPU, whose
+        # LDLT solve grows faster than linearly)
+        cx, cy, cz = (int(v) for v in args.tets.split(","))
+        sc = scenes.tet_drop(40, 16, 20, iters=10, n_steps=3)
+        return cpu_baseline(sc, scale=sc.n_elements() / (5.0 * cx * cy * cz),
+                            what="; value = sample iters/s x (sample tets / workload tets)")
+    sc = scenes.cloth(args.nx, args.nx, iters=args.cpu_iters, n_steps=3)
+    return cpu_baseline(sc)
+
+
 def main():
     args = parse()
     world, rank, local, dist = dist_setup(args.gpus)
-    if args.config != "c2":
+    if args.config in ("c3", "c5"):
         return main_geom(args, world, rank, local, dist)
     pkg = importlib.import_module("aa-admm_amd")
-    capi, scenes = pkg.capi, pkg.scenes
-
-    def builder(iters=args.iters, n_steps=1):
-        return scenes.cloth(args.nx, args.nx, iters=iters, n_steps=n_steps)
+    capi = pkg.capi
 
     ctx = capi.Context(local)
-    sc = builder()
+    sc, desc = elastic_scene(args)
     solver = capi.solver_from_scene(ctx, sc)
     t0 = time.time()
     solver.initialize(capi.settings_from_scene(sc))
@@ -254,24 +290,29 @@ def main():
     iters_all = allreduce(dist, float(iters_run), _sum_op(dist))
     value = iters_all / elapsed_max
 
-    # roofline of the dominant kernel, timed live with HIP events on the solver's stream
+    # roofline of the dominant kernel class, timed live with HIP events on the solver's stream
     # (separate instrumented pass of the same iteration loop, after the timed region)
     roof = None
     if rank == 0:
-        solver.bench_iterations(args.iters)
-        stats = {k: solver.kernel_stats(k) for k in ("local_z", "solve", "resid", "rhs", "aa")}
-        k = "local_z"
+        solver.bench_iterations(min(args.iters, 50))
+        names = ("local_z", "solve", "resid", "rhs", "aa") if sc.variant == 1 else \
+                ("grad", "rhs", "solve", "prim", "local_z", "aa", "comb")
+        stats = {k: solver.kernel_stats(k) for k in names}
+        per_iter = {k: v["avg_ms"] * v["launches"] for k, v in stats.items()}
+        k = "solve"   # the global solve: the dominant HBM-bound phase (north_star roofline)
         st = stats[k]
         achieved = st["bytes"] / (st["avg_ms"] * 1e-3) / 1e9 if st["avg_ms"] > 0 else 0.0
-        roof = {"kernel": "k_local_z<3> (fused update_z: tri prox + prim residual + rhs row terms)",
+        roof = {"kernel": "global solve: multifrontal triangular solves, 3 RHS (k_fwd*/k_bwd*/k_asm per solve)",
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "avg_launch_us": round(st["avg_ms"] * 1e3, 2), "bytes_per_launch": st["bytes"],
-                "phase_us_per_iter": {kk: round(v["avg_ms"] * 1e3, 2) for kk, v in stats.items()}}
+                "phase_us_per_launch": {kk: round(v["avg_ms"] * 1e3, 2) for kk, v in stats.items()},
+                "phase_bytes_per_launch": {kk: v["bytes"] for kk, v in stats.items()},
+                "dominant_phase": max(per_iter, key=per_iter.get)}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(builder, args.cpu_iters)
+            cpu = elastic_cpu_baseline(args)
         except Exception as e:  # report, never fail the GPU number on the baseline leg
             cpu = {"value": None, "error": str(e)[:200]}
 
@@ -282,12 +323,13 @@ def main():
             "metric": "ADMM iters/sec + time-to-eps (primal+dual residual)", "value": round(value, 2),
             "unit": "ADMM iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed_max * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64", "data": "synthetic (generated make_tri_blocks mesh)",
-            "config": {"workload": f"cloth drop make_tri_blocks({args.nx},{args.nx}) 50176 tris, (u,x)-AA m=6, "
-                                   f"{args.iters} ADMM iters/step, dt=1/30 (BASELINE configs[1])",
-                       "nodes": sc.n_nodes, "elements": sc.n_elements(), "admm_iters_per_step": args.iters,
-                       "anderson_m": 6, "parallelism": f"replicas{world}", "global_solve": "supernodal direct",
-                       "nnz_factor": rt.nnz_factor, "setup_ms": round(setup_ms, 1)},
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (generated make_tet_blocks mesh)" if args.config == "c4"
+                    else "synthetic (generated make_tri_blocks mesh)",
+            "config": {"workload": desc, "nodes": sc.n_nodes, "elements": sc.n_elements(),
+                       "admm_iters_per_step": args.iters, "anderson_m": sc.aa_m, "parallelism": f"replicas{world}",
+                       "global_solve": "supernodal direct", "nnz_factor": rt.nnz_factor,
+                       "setup_ms": round(setup_ms, 1)},
             "iters_executed": int(iters_all),
             "time_to_eps_ms": (round(statistics.median(tt), 3) if tt else None), "eps_rel": EPS_ELASTIC,
             "roofline": roof, "cpu_baseline": cpu,

@@ -20,10 +20,11 @@ typedef struct {
 } oracle_settings;
 
 /* Runs n_steps time steps of Solver::step on the scene; returns 0 on success.
+ * x3: initial node positions; rest3: rest positions of the elements (NULL = x3).
  * groups: kind (0 tet / 1 tri), material (0 linear / 1 NH / 2 StVK), E, nu, limit_min/max,
  * count and offset into idx (int32, 4 per tet / 3 per tri).
  * Per-step records are written to rec_* at [step*cap + i]; nrec[step] = count. */
-int oracle_elastic_run(int n_nodes, const double* x3, const double* masses,
+int oracle_elastic_run(int n_nodes, const double* x3, const double* rest3, const double* masses,
                        int n_groups, const int* g_kind, const int* g_mat, const double* g_E, const double* g_nu,
                        const double* g_lmin, const double* g_lmax, const int* g_count, const int* g_off,
                        const int* idx, int n_pins, const int* pin_idx, const double* pin_pts,

@@ -113,10 +113,13 @@ struct Elastic {
     Envelope chol;
     double pdt2 = 0;
 
-    void build(int n_nodes, const double* x3, const double* masses, int n_groups, const int* g_kind, const int* g_mat,
-               const double* g_E, const double* g_nu, const double* g_lmin, const double* g_lmax, const int* g_count,
-               const int* g_off, const int* idx, int n_pins, const int* pin_idx) {
+    // rest3: rest positions the element reductions are built from (create_tets_from_mesh takes
+    // the mesh vertices, TetEnergyTerm.hpp:36-51); x3: initial node positions (add_nodes).
+    void build(int n_nodes, const double* x3, const double* rest3, const double* masses, int n_groups, const int* g_kind,
+               const int* g_mat, const double* g_E, const double* g_nu, const double* g_lmin, const double* g_lmax,
+               const int* g_count, const int* g_off, const int* idx, int n_pins, const int* pin_idx) {
         n = n_nodes;
+        if (!rest3) rest3 = x3;
         x.assign(x3, x3 + 3 * n);
         v.assign(3 * n, 0.0);
         mass.assign(masses, masses + n);
@@ -170,7 +173,7 @@ struct Elastic {
                 e.kind = g_kind[g]; e.mat = g_mat[g]; e.nv = nv; e.ncol = nv - 1; e.dim = 3 * (nv - 1);
                 e.mu = mu; e.lambda = lam; e.k = k; e.lmin = g_lmin[g]; e.lmax = g_lmax[g];
                 const double* P[4];
-                for (int a = 0; a < nv; ++a) { e.v[a] = node2int[id[a]]; P[a] = x3 + 3 * (size_t)id[a]; }
+                for (int a = 0; a < nv; ++a) { e.v[a] = node2int[id[a]]; P[a] = rest3 + 3 * (size_t)id[a]; }
                 if (e.kind == 0) {
                     double B[9];  // row-major, columns = edges
                     for (int r = 0; r < 3; ++r) for (int cc = 0; cc < 3; ++cc) B[r * 3 + cc] = P[cc + 1][r] - P[0][r];
@@ -490,7 +493,8 @@ struct Elastic {
 
 using namespace oracle;
 
-extern "C" int oracle_elastic_run(int n_nodes, const double* x3, const double* masses, int n_groups, const int* g_kind,
+extern "C" int oracle_elastic_run(int n_nodes, const double* x3, const double* rest3, const double* masses, int n_groups,
+                                  const int* g_kind,
                                   const int* g_mat, const double* g_E, const double* g_nu, const double* g_lmin,
                                   const double* g_lmax, const int* g_count, const int* g_off, const int* idx, int n_pins,
                                   const int* pin_idx, const double* pin_pts, const double* pin_vel,
@@ -499,7 +503,7 @@ extern "C" int oracle_elastic_run(int n_nodes, const double* x3, const double* m
                                   char* err, int err_cap) {
     try {
         Elastic s;
-        s.build(n_nodes, x3, masses, n_groups, g_kind, g_mat, g_E, g_nu, g_lmin, g_lmax, g_count, g_off, idx, n_pins, pin_idx);
+        s.build(n_nodes, x3, rest3, masses, n_groups, g_kind, g_mat, g_E, g_nu, g_lmin, g_lmax, g_count, g_off, idx, n_pins, pin_idx);
         std::vector<double> pts(pin_pts, pin_pts + 3 * (size_t)n_pins);
         s.set_pins(n_pins, pin_idx, pts.data());
         s.initialize(*st);

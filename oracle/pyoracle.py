@@ -58,6 +58,7 @@ def run_elastic(scene, n_steps=None, cap=None):
         off[i] = acc
         acc += g.idx.size
     x = np.ascontiguousarray(scene.x, np.float64)
+    rest = None if getattr(scene, "rest", None) is None else np.ascontiguousarray(scene.rest, np.float64)
     m = np.ascontiguousarray(scene.masses, np.float64)
     pins = np.ascontiguousarray(scene.pin_idx, np.int32)
     pts = np.ascontiguousarray(scene.pin_pts, np.float64)
@@ -72,7 +73,7 @@ def run_elastic(scene, n_steps=None, cap=None):
     ms = np.zeros(n_steps)
     err = C.create_string_buffer(512)
     rc = L.oracle_elastic_run(
-        C.c_int(scene.n_nodes), _p(x, C.c_double), _p(m, C.c_double), C.c_int(len(groups)), _p(kind, C.c_int),
+        C.c_int(scene.n_nodes), _p(x, C.c_double), None if rest is None else _p(rest, C.c_double), _p(m, C.c_double), C.c_int(len(groups)), _p(kind, C.c_int),
         _p(mat, C.c_int), _p(E, C.c_double), _p(nu, C.c_double), _p(lmin, C.c_double), _p(lmax, C.c_double),
         _p(cnt, C.c_int), _p(off, C.c_int), _p(idx, C.c_int), C.c_int(len(pins)), _p(pins, C.c_int),
         _p(pts, C.c_double), _p(vel, C.c_double), C.byref(st), C.c_int(n_steps), C.c_int(cap), _p(nrec, C.c_int),

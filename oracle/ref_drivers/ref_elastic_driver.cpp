@@ -7,7 +7,8 @@
 // windyflag.cpp:63-183, beams.cpp) with a file-driven loop:
 //
 //   scene file (written by aa-admm_amd/scenes.py: write_scene) -> admm::Solver
-//     add_nodes (Solver.hpp:265-279), create_tets_from_mesh / create_tris_from_mesh
+//     add_nodes (Solver.hpp:265-279) with the initial positions, create_tets_from_mesh /
+//     create_tris_from_mesh on the rest positions (AASCENE2; AASCENE1: rest = initial)
 //     (TetEnergyTerm.hpp:36-51, TriEnergyTerm.hpp:33-47), set_pins (Solver.cpp:280-315),
 //     initialize (Solver.cpp:361-491), step() x n_steps (Solver.cpp:34-234)
 //   -> result file: per time step the per-iteration (prim, comb, reject) rows that
@@ -58,11 +59,17 @@ int main(int argc, char** argv) {
     if (!f) { perror("scene"); return 2; }
     Reader r{f};
     char magic[8];
-    if (fread(magic, 1, 8, f) != 8 || memcmp(magic, "AASCENE1", 8) != 0) { fprintf(stderr, "bad magic\n"); return 2; }
+    if (fread(magic, 1, 8, f) != 8 || (memcmp(magic, "AASCENE1", 8) != 0 && memcmp(magic, "AASCENE2", 8) != 0)) {
+        fprintf(stderr, "bad magic\n");
+        return 2;
+    }
+    const bool has_rest = magic[7] == '2';   // AASCENE2: rest positions follow the node positions
     const int variant = r.get<int>();
     const int n = r.get<int>();
-    std::vector<double> x, m;
+    std::vector<double> x, rest, m;
     r.arr(x, 3 * (size_t)n);
+    if (has_rest) r.arr(rest, 3 * (size_t)n);
+    else rest = x;
     r.arr(m, 3 * (size_t)n);
     const int n_groups = r.get<int>();
     std::vector<Group> groups(n_groups);
@@ -96,13 +103,13 @@ int main(int argc, char** argv) {
         lame.limit_max = g.lmax;
         if (g.kind == 0) {
             if (g.material == 0)
-                admm::create_tets_from_mesh<double, admm::TetEnergyTerm>(solver.energyterms, x.data(), g.idx.data(), g.count, lame, 0);
+                admm::create_tets_from_mesh<double, admm::TetEnergyTerm>(solver.energyterms, rest.data(), g.idx.data(), g.count, lame, 0);
             else if (g.material == 1)
-                admm::create_tets_from_mesh<double, admm::NeoHookeanTet>(solver.energyterms, x.data(), g.idx.data(), g.count, lame, 0);
+                admm::create_tets_from_mesh<double, admm::NeoHookeanTet>(solver.energyterms, rest.data(), g.idx.data(), g.count, lame, 0);
             else
-                admm::create_tets_from_mesh<double, admm::StVKTet>(solver.energyterms, x.data(), g.idx.data(), g.count, lame, 0);
+                admm::create_tets_from_mesh<double, admm::StVKTet>(solver.energyterms, rest.data(), g.idx.data(), g.count, lame, 0);
         } else {
-            admm::create_tris_from_mesh<double, admm::TriEnergyTerm>(solver.energyterms, x.data(), g.idx.data(), g.count, lame, 0);
+            admm::create_tris_from_mesh<double, admm::TriEnergyTerm>(solver.energyterms, rest.data(), g.idx.data(), g.count, lame, 0);
         }
     }
     auto pins_at = [&](int k) {

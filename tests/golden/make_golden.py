@@ -43,6 +43,8 @@ def cases():
         "cloth12_ux_aa1": S.cloth(12, 12, iters=30, n_steps=2, aa_m=1),
         "cant8_ux_lin_aa3_pen": _with(S.cantilever(8, 2, 2, S.LINEAR, iters=30, n_steps=1, variant=S.VARIANT_H, aa_m=3),
                                       penalty=4.0),
+        # C4 recipe at small size: NeoHookean block free fall from a squashed pose (rest != initial)
+        "drop6_z_nh_aa6": S.tet_drop(6, 2, 3, iters=40, n_steps=2),
     }
 
 
@@ -117,12 +119,16 @@ def _run_elem(buf, tmp, width, count):
     return np.fromfile(pout, dtype="<f8").reshape(count, width)
 
 
-def main():
+def main(only=None):
     with tempfile.TemporaryDirectory() as tmp:
         for name, sc in cases().items():
+            if only and name not in only:
+                continue
             steps = run_ref(sc, tmp)
             save_case(os.path.join(HERE, name + ".npz"), sc, steps)
             print(name, [len(s["prim"]) for s in steps])
+        if only:
+            return
         et = element_tables(tmp)
         arrays = {}
         for name in ("tet_linear", "tet_nh", "tet_stvk", "tri_h_limits", "tri_h_free"):
@@ -136,4 +142,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])   # optional case names: regenerate only those trajectory fixtures

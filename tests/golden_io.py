@@ -29,6 +29,8 @@ def save_case(path, sc, steps):
     )
     for i, g in enumerate(sc.groups):
         d[f"g{i}_idx"] = g.idx
+    if sc.rest is not None:
+        d["rest"] = sc.rest
     np.savez_compressed(path, **d)
 
 
@@ -41,7 +43,8 @@ def load_case(name):
     sc = scenes.Scene(x=d["x"], masses=d["masses"], groups=groups, pin_idx=d["pin_idx"].astype(np.int32),
                       pin_pts=d["pin_pts"], pin_vel=d["pin_vel"], variant=int(st[0]), dt=float(st[1]),
                       gravity=float(st[2]), penalty=float(st[3]), iters=int(st[4]), accel=int(st[5]),
-                      aa_m=int(st[6]), n_steps=int(st[7]), name=name)
+                      aa_m=int(st[6]), n_steps=int(st[7]), name=name,
+                      rest=d["rest"] if "rest" in d.files else None)
     steps, o = [], 0
     for k, n in enumerate(d["nrec"]):
         steps.append(dict(prim=d["prim"][o:o + n], comb=d["comb"][o:o + n], reject=d["reject"][o:o + n],
