@@ -25,6 +25,8 @@ EXPORTS = [
     "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats",
+    "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_destroy", "aa_comm_info",
+    "aa_comm_allreduce_host", "aa_elastic_set_comm",
     "aa_geom_create", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
     "aa_geom_add_closeness", "aa_geom_setup", "aa_geom_solve", "aa_geom_get_solution", "aa_geom_get_history",
     "aa_geom_runtime_info", "aa_geom_closest_points", "aa_geom_bench_iterations", "aa_geom_kernel_stats",
@@ -119,6 +121,69 @@ class Context:
             pass
 
 
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_longlong, C.c_void_p)
+
+
+class Comm:
+    """Communicator of the partitioned multi-GPU solver (aa_comm_*).
+
+    Comm.rccl(ctx, rank, size, unique_id): RCCL over xGMI, one process per GPU.
+    Comm.host(fn, rank, size): host-staged transport; fn(np.ndarray) sums the array in place
+    over the ranks (e.g. torch.distributed over gloo) -- lets several ranks share one GPU.
+    """
+
+    def __init__(self, h, keep=None):
+        self.h = h
+        self._keep = keep
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_ubyte * 128)()
+        _chk(lib().aa_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, ctx: Context, rank: int, size: int, unique_id: bytes):
+        h = C.c_void_p()
+        uid = (C.c_ubyte * 128).from_buffer_copy(unique_id)
+        _chk(lib().aa_comm_create_rccl(ctx.h, uid, C.c_int(rank), C.c_int(size), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def host(cls, fn, rank: int, size: int):
+        def cb(buf, n, _user):
+            try:
+                fn(np.ctypeslib.as_array(buf, shape=(int(n),)))
+                return 0
+            except Exception:   # noqa: BLE001 -- reported to C as a failed reduction
+                return 1
+        cfn = HOST_ALLREDUCE_FN(cb)
+        h = C.c_void_p()
+        _chk(lib().aa_comm_create_host(cfn, None, C.c_int(rank), C.c_int(size), C.byref(h)))
+        return cls(h, keep=cfn)
+
+    def info(self):
+        r, n = C.c_int(), C.c_int()
+        _chk(lib().aa_comm_info(self.h, C.byref(r), C.byref(n)))
+        return r.value, n.value
+
+    def allreduce_host(self, a):
+        a = np.ascontiguousarray(a, np.float64)
+        _chk(lib().aa_comm_allreduce_host(self.h, _dp(a), C.c_longlong(a.size)))
+        return a
+
+    def close(self):
+        if self.h:
+            lib().aa_comm_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Solver:
     """Mirror of admm::Solver: add_nodes / create_*_from_mesh / set_pins / initialize / step."""
 
@@ -164,6 +229,11 @@ class Solver:
         else:
             p = np.ascontiguousarray(points, np.float64).reshape(-1)
             _chk(lib().aa_elastic_set_pins(self.h, _ip(i), _dp(p), C.c_int(len(i))))
+
+    def set_comm(self, comm):
+        """Partition over comm's ranks at initialize() (every rank binds the same scene)."""
+        self.comm = comm   # the communicator must outlive the solver
+        _chk(lib().aa_elastic_set_comm(self.h, comm.h if comm is not None else None))
 
     def initialize(self, settings: Settings):
         _chk(lib().aa_elastic_initialize(self.h, C.byref(settings)))
@@ -211,9 +281,11 @@ class Solver:
         return dict(avg_ms=a.value, bytes=b.value, launches=n.value)
 
 
-def solver_from_scene(ctx: Context, scene) -> Solver:
+def solver_from_scene(ctx: Context, scene, comm=None) -> Solver:
     """Binds a scenes.Scene the way binding::add_trimesh/add_tetmesh + the samples do."""
     s = Solver(ctx)
+    if comm is not None:
+        s.set_comm(comm)
     s.add_nodes(scene.x, np.repeat(np.asarray(scene.masses, np.float64), 3))
     for g in scene.groups:
         lame = Lame.from_young(g.E, g.nu, g.limit_min, g.limit_max)
@@ -231,9 +303,9 @@ def settings_from_scene(scene) -> Settings:
                     variant=scene.variant, verbose=0)
 
 
-def run_scene(ctx: Context, scene, n_steps=None):
+def run_scene(ctx: Context, scene, n_steps=None, comm=None):
     """Runs the scene like the reference driver; returns per-step dicts (prim, comb, reject, x, v)."""
-    s = solver_from_scene(ctx, scene)
+    s = solver_from_scene(ctx, scene, comm)
     s.initialize(settings_from_scene(scene))
     out = []
     n_steps = scene.n_steps if n_steps is None else n_steps

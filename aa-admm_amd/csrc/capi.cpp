@@ -2,15 +2,18 @@
 // status codes; the message is kept per thread for aa_last_error().
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <string>
 
 #include "../../include/aa_admm.h"
+#include "comm.hpp"
 #include "elastic.hpp"
 #include "geom.hpp"
 
 struct aa_ctx_s { aa::Context c; };
 struct aa_elastic_s { aa::ElasticSolver* s; aa_ctx_s* ctx; };
 struct aa_geom_s { aa::GeomSolver* s; aa_ctx_s* ctx; };
+struct aa_comm_s { std::unique_ptr<aa::Comm> c; };
 
 namespace {
 thread_local std::string g_err;
@@ -182,6 +185,54 @@ int aa_elastic_get_history(aa_elastic h, double* prim, double* comb, int* reject
 
 int aa_elastic_runtime(aa_elastic h, aa_runtime* out) {
     return guarded([&] { NEED(h && out, "null argument"); *out = h->s->runtime(); });
+}
+
+int aa_comm_unique_id(unsigned char id[128]) {
+    return guarded([&] { NEED(id, "null argument"); aa::rccl_unique_id(id); });
+}
+
+int aa_comm_create_rccl(aa_ctx ctx, const unsigned char id[128], int rank, int size, aa_comm* out) {
+    return guarded([&] {
+        NEED(ctx && id && out, "null argument");
+        NEED(size >= 1 && rank >= 0 && rank < size, "aa_comm_create_rccl: bad rank/size");
+        AA_HIP(hipSetDevice(ctx->c.device));
+        auto* c = new aa_comm_s;
+        try { c->c = aa::make_rccl_comm(id, rank, size); } catch (...) { delete c; throw; }
+        *out = c;
+    });
+}
+
+int aa_comm_create_host(aa_host_allreduce_fn fn, void* user, int rank, int size, aa_comm* out) {
+    return guarded([&] {
+        NEED(fn && out, "null argument");
+        NEED(size >= 1 && rank >= 0 && rank < size, "aa_comm_create_host: bad rank/size");
+        auto* c = new aa_comm_s;
+        c->c = aa::make_host_comm(fn, user, rank, size);
+        *out = c;
+    });
+}
+
+int aa_comm_destroy(aa_comm c) {
+    return guarded([&] { delete c; });
+}
+
+int aa_comm_info(aa_comm c, int* rank, int* size) {
+    return guarded([&] {
+        NEED(c, "null handle");
+        if (rank) *rank = c->c->rank();
+        if (size) *size = c->c->size();
+    });
+}
+
+int aa_comm_allreduce_host(aa_comm c, double* buf, long long n) {
+    return guarded([&] {
+        NEED(c && (n == 0 || buf) && n >= 0, "bad argument");
+        c->c->allreduce_sum_host(buf, (size_t)n);
+    });
+}
+
+int aa_elastic_set_comm(aa_elastic h, aa_comm c) {
+    return guarded([&] { NEED(h, "null handle"); h->s->set_comm(c ? c->c.get() : nullptr); });
 }
 
 int aa_elastic_bench_iterations(aa_elastic h, int iters, double* ms) {

@@ -1,0 +1,131 @@
+// RCCL and host-callback transports of aa::Comm (see comm.hpp).
+#include "comm.hpp"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "common.hpp"
+
+namespace aa {
+
+namespace {
+
+// librccl entry points, resolved once (types from the header, symbols at run time)
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    static std::string err;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+            if (h) break;
+        }
+        if (!h) { err = std::string("cannot load librccl: ") + dlerror(); return; }
+        r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+        r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
+        r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+        if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string) {
+            err = "librccl: missing symbols";
+            r = Rccl{};
+        }
+    });
+    if (!r.all_reduce) throw Error(ERR_DEVICE, err.empty() ? "librccl unavailable" : err);
+    return r;
+}
+
+void nccl_check(ncclResult_t rc, const char* what) {
+    if (rc != ncclSuccess) throw Error(ERR_DEVICE, std::string(what) + ": " + rccl().error_string(rc));
+}
+
+class RcclComm final : public Comm {
+public:
+    RcclComm(const unsigned char id[128], int rank, int size) {
+        rank_ = rank; size_ = size;
+        ncclUniqueId uid;
+        static_assert(sizeof(uid) == 128, "ncclUniqueId must be 128 bytes");
+        std::memcpy(&uid, id, 128);
+        nccl_check(rccl().comm_init_rank(&comm_, size, uid, rank), "ncclCommInitRank");
+    }
+    ~RcclComm() override {
+        if (comm_) (void)rccl().comm_destroy(comm_);
+    }
+    void allreduce_sum(const double* src, double* dst, size_t n, hipStream_t s) override {
+        if (n == 0) return;
+        nccl_check(rccl().all_reduce(src, dst, n, ncclDouble, ncclSum, comm_, s), "ncclAllReduce");
+    }
+    void allreduce_sum_host(double* buf, size_t n) override {
+        if (n == 0) return;
+        double* d = nullptr;
+        AA_HIP(hipMalloc(&d, n * sizeof(double)));
+        hipError_t e = hipMemcpy(d, buf, n * sizeof(double), hipMemcpyHostToDevice);
+        if (e == hipSuccess) {
+            const ncclResult_t rc = rccl().all_reduce(d, d, n, ncclDouble, ncclSum, comm_, nullptr);
+            if (rc != ncclSuccess) { (void)hipFree(d); nccl_check(rc, "ncclAllReduce"); }
+            e = hipMemcpy(buf, d, n * sizeof(double), hipMemcpyDeviceToHost);
+        }
+        (void)hipFree(d);
+        AA_HIP(e);
+    }
+    bool capturable() const override { return false; }   // eager launches
+
+private:
+    ncclComm_t comm_ = nullptr;
+};
+
+class HostComm final : public Comm {
+public:
+    HostComm(HostAllreduceFn fn, void* user, int rank, int size) : fn_(fn), user_(user) { rank_ = rank; size_ = size; }
+    void allreduce_sum(const double* src, double* dst, size_t n, hipStream_t s) override {
+        if (n == 0) return;
+        buf_.resize(n);
+        AA_HIP(hipMemcpyAsync(buf_.data(), src, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        AA_HIP(hipStreamSynchronize(s));
+        allreduce_sum_host(buf_.data(), n);
+        AA_HIP(hipMemcpyAsync(dst, buf_.data(), n * sizeof(double), hipMemcpyHostToDevice, s));
+        AA_HIP(hipStreamSynchronize(s));
+    }
+    void allreduce_sum_host(double* buf, size_t n) override {
+        if (n == 0) return;
+        if (fn_(buf, (long long)n, user_) != 0) throw Error(ERR_DEVICE, "host all-reduce callback failed");
+    }
+    bool capturable() const override { return false; }
+
+private:
+    HostAllreduceFn fn_;
+    void* user_;
+    std::vector<double> buf_;
+};
+
+}  // namespace
+
+void rccl_unique_id(unsigned char out[128]) {
+    ncclUniqueId uid;
+    nccl_check(rccl().get_unique_id(&uid), "ncclGetUniqueId");
+    std::memcpy(out, &uid, 128);
+}
+
+std::unique_ptr<Comm> make_rccl_comm(const unsigned char id[128], int rank, int size) {
+    return std::unique_ptr<Comm>(new RcclComm(id, rank, size));
+}
+
+std::unique_ptr<Comm> make_host_comm(HostAllreduceFn fn, void* user, int rank, int size) {
+    if (!fn) throw Error(ERR_ARG, "host all-reduce: null callback");
+    return std::unique_ptr<Comm>(new HostComm(fn, user, rank, size));
+}
+
+}  // namespace aa

@@ -283,33 +283,44 @@ constexpr int kMaxLdsMode0 = 96 * 1024;
 
 }  // namespace
 
-void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
+void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part, int my_part,
+                         int top_beg, Comm* comm) {
     n_ = F.n;
     nn_ = F.n_nodes;
-    nnz_L_ = F.nnz_L;
+    comm_ = (node_part && comm && comm->size() > 1) ? comm : nullptr;
+    top_beg_ = comm_ ? top_beg : n_;
+    // partitioned: this GPU holds the supernodes of its own part and the shared top only
+    std::vector<char> inc(nn_, 1);
+    if (comm_)
+        for (int sn = 0; sn < nn_; ++sn) inc[sn] = (*node_part)[sn] == my_part || (*node_part)[sn] == -1;
     std::vector<int> beg(nn_), p(nn_), nb(nn_), bnd_off(nn_), bnd, pull_off(nn_);
     std::vector<long long> goff(nn_), uoff(nn_), foff(nn_, -1);
     long long go = 0, uo = 0, fo = 0;
-    double dense = 0, offd = 0, bsum = 0;
+    double dense = 0, offd = 0, bsum = 0, piv = 0;
     int rows_total = 0;
+    nnz_L_ = 0;
     for (int sn = 0; sn < nn_; ++sn) {
         const int ps = F.end[sn] - F.beg[sn], nbs = (int)F.bnd[sn].size();
         beg[sn] = F.beg[sn]; p[sn] = ps; nb[sn] = nbs;
         goff[sn] = go; uoff[sn] = uo;
         bnd_off[sn] = (int)bnd.size();
-        bnd.insert(bnd.end(), F.bnd[sn].begin(), F.bnd[sn].end());
         pull_off[sn] = rows_total;
+        if (!inc[sn]) continue;
+        bnd.insert(bnd.end(), F.bnd[sn].begin(), F.bnd[sn].end());
         rows_total += ps + nbs;
+        nnz_L_ += (size_t)ps * (ps + 1) / 2 + (size_t)ps * nbs;
         go += (long long)(ps + nbs) * ps;
         uo += 3LL * nbs;
         dense += 0.5 * ps * (ps + 1.0);
         offd += (double)ps * nbs;
+        piv += ps;
         bsum += nbs;
     }
     // G_s = [Linv ; M], M = L_BP Linv (row-major copy Gr and column-major copy Gc)
     std::vector<double> Gr(go), Gc(go);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int sn = 0; sn < nn_; ++sn) {
+        if (!inc[sn]) continue;
         const int ps = p[sn], nbs = nb[sn], R = ps + nbs;
         double* gr = Gr.data() + goff[sn];
         const std::vector<double>& Li = F.Linv[sn];
@@ -331,8 +342,10 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
             for (int c = 0; c < ps; ++c) gc[(size_t)c * R + r] = gr[(size_t)r * ps + c];
     }
     // children lists and ELL pull lists (front row q of a parent <- child update entries, fixed order)
+    // (partitioned: the children of the top that belong to other GPUs' parts contribute nothing
+    // here -- their update vectors arrive through the all-reduce of the top rows)
     std::vector<std::vector<int>> kl(nn_);
-    for (int sn = 0; sn < nn_; ++sn) if (F.parent[sn] >= 0) kl[F.parent[sn]].push_back(sn);
+    for (int sn = 0; sn < nn_; ++sn) if (F.parent[sn] >= 0 && inc[sn]) kl[F.parent[sn]].push_back(sn);
     std::vector<std::vector<long long>> pull(rows_total);
     for (int par = 0; par < nn_; ++par) {
         const std::vector<int>& pb = F.bnd[par];
@@ -353,7 +366,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
     std::vector<int> ell_w(nn_, 0);
     std::vector<long long> ell_off(nn_, 0), ell;
     for (int sn = 0; sn < nn_; ++sn) {
-        const int R = p[sn] + nb[sn];
+        const int R = inc[sn] ? p[sn] + nb[sn] : 0;
         int w = 0;
         for (int q = 0; q < R; ++q) w = std::max(w, (int)pull[pull_off[sn] + q].size());
         ell_w[sn] = w;
@@ -367,14 +380,14 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
     // subtrees root at height <= H (enough workgroups to fill the chip) and every subtree level
     // fits the LDS budget; supernodes above H are solved level by level.
     std::vector<std::vector<int>> kids(nn_);
-    for (int sn = 0; sn < nn_; ++sn) if (F.parent[sn] >= 0) kids[F.parent[sn]].push_back(sn);
+    for (int sn = 0; sn < nn_; ++sn) if (F.parent[sn] >= 0 && inc[sn]) kids[F.parent[sn]].push_back(sn);
     const char* ms = std::getenv("AA_SOLVE_MIN_SUBTREES");
     const int min_sub = ms ? std::atoi(ms) : 96;
     constexpr int kSubLds = 64 * 1024, kMaxItemRow = 0xffff;
     auto roots_at = [&](int H) {
         std::vector<int> r;
         for (int sn = 0; sn < nn_; ++sn)
-            if (F.height[sn] <= H && (F.parent[sn] < 0 || F.height[F.parent[sn]] > H)) r.push_back(sn);
+            if (inc[sn] && F.height[sn] <= H && (F.parent[sn] < 0 || F.height[F.parent[sn]] > H)) r.push_back(sn);
         return r;
     };
     auto collect = [&](int root) {
@@ -470,7 +483,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
     }
     // levels by height and their row tasks
     std::vector<std::vector<int>> hl(F.max_height + 1);
-    for (int sn = 0; sn < nn_; ++sn) if (!fused[sn]) hl[F.height[sn]].push_back(sn);
+    for (int sn = 0; sn < nn_; ++sn) if (!fused[sn] && inc[sn]) hl[F.height[sn]].push_back(sn);
     std::vector<Task> tasks;
     auto mk = [&](int sn, int r0, int nr, int mode) {
         Task t{};
@@ -544,7 +557,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s) {
     }
     // algorithmic bytes of one solve: the factor once per sweep (dense triangles + boundary
     // blocks, fp64), b/y/x (24 B per node each way) and the update vectors (write + read)
-    bytes_ = 2.0 * 8.0 * (dense + offd) + 4.0 * 24.0 * n_ + 3.0 * 24.0 * bsum;
+    bytes_ = 2.0 * 8.0 * (dense + offd) + 4.0 * 24.0 * piv + 3.0 * 24.0 * bsum;
     AA_HIP(hipStreamSynchronize(s));
 }
 
@@ -560,6 +573,12 @@ void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject
         switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
     }
+    // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
+    // and in the update vectors); their sum over the GPUs is the full forward result. When the
+    // solve is gated off the stale rows are summed too -- harmless, the next forward rewrites
+    // them and the backward sweep is gated alike on every GPU.
+    if (comm_ && top_beg_ < n_)
+        comm_->allreduce_sum(Y_.p + 3 * (size_t)top_beg_, Y_.p + 3 * (size_t)top_beg_, 3 * (size_t)(n_ - top_beg_), s);
     for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
         const Level& L = *it;
 #define BWD(BL) hipLaunchKernelGGL(k_bwd<BL>, dim3(L.bwd_count), dim3(BL), L.lds_bwd, s, T, L.bwd_first, Gr_.p, Gc_.p, bnd_.p, Y_.p, x, ctrl, gate_reject)

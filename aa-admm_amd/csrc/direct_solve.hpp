@@ -19,6 +19,7 @@
 #pragma once
 #include <vector>
 
+#include "comm.hpp"
 #include "common.hpp"
 #include "elastic_kernels.hpp"
 #include "spd_direct.hpp"
@@ -31,7 +32,12 @@ public:
     static constexpr int kWaveP = 192;       // forward rows longer than this: wave per row
     static constexpr int kWaveR = 384;       // backward columns longer than this: wave per column
 
-    void build(const SupernodalFactor& F, hipStream_t s);
+    // Partitioned (comm with size > 1): node_part[s] is the part of supernode s
+    // (-1 = shared top separator, rows [top_beg, n)); only the supernodes of `my_part` and of
+    // the top are stored and solved here, and the top rows of the forward result are summed
+    // over the GPUs between the two sweeps.
+    void build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part = nullptr, int my_part = -1,
+               int top_beg = -1, Comm* comm = nullptr);
     // x (n x 3, stride 3 doubles) = A^-1 b ; b is read only. gate: skip when ctrl->done (or !reject).
     void solve(double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s);
     int n() const { return n_; }
@@ -64,7 +70,8 @@ private:
         int asm_first = 0, asm_count = 0;     // assembly tasks of the wave-mode supernodes
         int fblock = 256, bblock = 256, lds_fwd = 0, lds_bwd = 0;
     };
-    int n_ = 0, nn_ = 0, kernels_ = 0;
+    int n_ = 0, nn_ = 0, kernels_ = 0, top_beg_ = 0;
+    Comm* comm_ = nullptr;
     size_t nnz_L_ = 0;
     double bytes_ = 0;
     DevBuf<int> bnd_;

@@ -147,6 +147,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     auto t0 = std::chrono::steady_clock::now();
     drop_graph();
     if (const char* g = std::getenv("AA_ADMM_NO_GRAPH")) use_graph_ = !(g[0] == '1');
+    if (comm_ && !comm_->capturable()) use_graph_ = false;
     st_ = s_in;
     if (st_.timestep_s <= 0.0) st_.timestep_s = 1.0 / 24.0;  // Solver.cpp:369-373
     const int n = num_nodes();
@@ -195,13 +196,34 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     std::vector<double> coords(3 * (size_t)nf_);
     for (int k = 0; k < nf_; ++k)
         for (int j = 0; j < 3; ++j) coords[3 * k + j] = x_[3 * (size_t)free_nodes[k] + j];
-    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32, DirectSolver::kTopRows);
+    // partitioned: the first log2(P) bisections of the nested dissection are
+    // forced; part r (a contiguous range of free nodes) belongs to rank r, the separators of
+    // those bisections (the "top") are shared by all ranks
+    const int P = comm_ ? comm_->size() : 1;
+    int levels = 0;
+    while ((1 << levels) < P) ++levels;
+    if ((1 << levels) != P) throw Error(ERR_ARG, "initialize: the number of ranks must be a power of two");
+    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, levels);
     node2int_.assign(n, -1);
     int2node_.assign(n, -1);
     for (int q = 0; q < nf_; ++q) { node2int_[free_nodes[tree.perm[q]]] = q; int2node_[q] = free_nodes[tree.perm[q]]; }
     {
         int q = nf_;
         for (auto& kv : pins_) { node2int_[kv.first] = q; int2node_[q] = kv.first; ++q; }
+    }
+    top_beg_ = P > 1 ? tree.top_beg : nf_;
+    own_beg_ = P > 1 ? tree.part_beg[rank_] : 0;
+    own_end_ = P > 1 ? tree.part_end[rank_] : nf_;
+    if (P > 1) {   // every rank must have been handed the same scene
+        double h[5] = {(double)n, (double)nf_, 0, 0, 0};
+        for (auto& g : hgroups_) h[2] += (double)g.idx.size();
+        for (size_t i = 0; i < x_.size(); ++i) { h[3] += x_[i]; h[4] += m3_[i]; }
+        double r[5];
+        std::copy(h, h + 5, r);
+        comm_->allreduce_sum_host(r, 5);
+        for (int i = 0; i < 5; ++i)
+            if (std::fabs(r[i] - P * h[i]) > 1e-12 * std::fabs(P * h[i]))
+                throw Error(ERR_ARG, "initialize: the ranks were given different scenes (nodes, elements or pins differ)");
     }
     // ---- global matrix A_s = M + pdt2 * sum_e w^2 G^T G  (Solver.cpp:466-467)
     const double dt2 = st_.timestep_s * st_.timestep_s;
@@ -249,16 +271,50 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     } catch (const std::runtime_error& e) {
         throw Error(ERR_NUMERIC, e.what());
     }
-    solver_.build(F, s());
+    solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_);
 
+    // ---- element ownership (partitioned): an element touching a node of part r belongs to
+    // rank r (it cannot touch another part: the separators split the mesh); elements whose free
+    // nodes are all separator nodes go round-robin. Every rank computes the same assignment.
+    std::vector<HostGroup> owned;
+    nbg_ = 0;
+    long long zmax = 0;
+    if (P > 1) {
+        std::vector<int> qpart(n, -1);
+        for (int r = 0; r < P; ++r) for (int q = tree.part_beg[r]; q < tree.part_end[r]; ++q) qpart[q] = r;
+        std::vector<long long> zr(P, 0);
+        std::vector<int> br(P, 0);
+        long long rr = 0;
+        for (auto& hg : hgroups_) {
+            const int cnt = (int)(hg.idx.size() / hg.nv);
+            std::vector<int> c(P, 0);
+            HostGroup lg;
+            lg.kind = hg.kind; lg.material = hg.material; lg.nv = hg.nv; lg.ncol = hg.ncol; lg.lame = hg.lame;
+            for (int t = 0; t < cnt; ++t) {
+                int o = -1;
+                for (int a = 0; a < hg.nv && o < 0; ++a) o = qpart[node2int_[hg.idx[(size_t)t * hg.nv + a]]];
+                if (o < 0) o = (int)(rr++ % P);
+                ++c[o];
+                if (o != rank_) continue;
+                lg.idx.insert(lg.idx.end(), hg.idx.begin() + (size_t)t * hg.nv, hg.idx.begin() + (size_t)(t + 1) * hg.nv);
+                lg.G.insert(lg.G.end(), hg.G.begin() + (size_t)t * hg.ncol * hg.nv, hg.G.begin() + (size_t)(t + 1) * hg.ncol * hg.nv);
+                lg.vol.push_back(hg.vol[t]);
+                lg.w.push_back(hg.w[t]);
+            }
+            for (int r = 0; r < P; ++r) { br[r] += blocks_for(c[r]); zr[r] += 3LL * hg.ncol * c[r]; }
+            owned.push_back(std::move(lg));
+        }
+        for (int r = 0; r < P; ++r) { nbg_ = std::max(nbg_, br[r]); zmax = std::max(zmax, zr[r]); }
+    }
+    const std::vector<HostGroup>& dgroups = P > 1 ? owned : hgroups_;
     // ---- device element groups (internal node ids), z/u offsets, D^T gather rows
     groups_.clear();
-    groups_.resize(hgroups_.size());
+    groups_.resize(dgroups.size());
     long long zoff = 0, yrow = 0;
     red_blocks_ = 0;
     std::vector<std::vector<std::pair<long long, double>>> dtr(nf_);
-    for (size_t gi = 0; gi < hgroups_.size(); ++gi) {
-        auto& hg = hgroups_[gi];
+    for (size_t gi = 0; gi < dgroups.size(); ++gi) {
+        auto& hg = dgroups[gi];
         auto& dg = groups_[gi];
         const int cnt = (int)(hg.idx.size() / hg.nv);
         std::vector<int> idx((size_t)hg.nv * cnt);
@@ -290,6 +346,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
         red_blocks_ += blocks_for(cnt);
     }
     Z_ = zoff;
+    if (P == 1) { nbg_ = red_blocks_; zmax = Z_; }
     {
         std::vector<int> ptr(nf_ + 1, 0), row;
         std::vector<double> val;
@@ -315,7 +372,13 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     xbar_.alloc(3 * (size_t)nf_); Mxbar_.alloc(3 * (size_t)nf_); b_.alloc(3 * (size_t)nf_); dx_.alloc(3 * (size_t)nf_);
     z_.alloc(Z_); u_.alloc(Z_); y_.alloc(Z_); du_.alloc(Z_);
     if (st_.variant == AA_VARIANT_Z) { dz_.alloc(Z_); lastz_.alloc(Z_); cz_.alloc(Z_); }
-    red_a_.alloc(std::max(1, red_blocks_)); red_b_.alloc(std::max(1, red_blocks_));
+    // residual block partials [a | b], padded to the largest rank's block count (zeros beyond
+    // this rank's blocks), and their all-rank sums (the same buffer on one GPU)
+    nbg_ = std::max(1, nbg_);
+    red_ab_.alloc(2 * (size_t)nbg_); red_ab_.zero(s());
+    pa_ = red_ab_.p; pb_ = red_ab_.p + nbg_;
+    if (comm_) { red_gab_.alloc(2 * (size_t)nbg_); red_gab_.zero(s()); ga_ = red_gab_.p; gb_ = red_gab_.p + nbg_; }
+    else { ga_ = pa_; gb_ = pb_; }
     ctrl_.alloc(1);
     hist_cap_ = std::max(1, st_.admm_iters);
     hist_prim_.alloc(hist_cap_); hist_comb_.alloc(hist_cap_); hist_rej_.alloc(hist_cap_);
@@ -325,9 +388,13 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
         aa_cur_.alloc(dim);
         aa_dF_.alloc((size_t)m * Z_); aa_dF_.zero(s());
         aa_dG_.alloc((size_t)m * dim); aa_dG_.zero(s());
-        aa_blocks_ = aa_reduce_blocks(dim);
+        // same grid on every rank (the largest rank's) so the partial layouts line up
+        aa_blocks_ = aa_reduce_blocks(st_.variant == AA_VARIANT_UX ? zmax + 3LL * nf_ : zmax);
+        (void)dim;
         const int mm = m <= 8 ? 8 : (m <= 16 ? 16 : 32);
-        aa_red_.alloc((size_t)aa_blocks_ * (2 + 2 * mm));
+        aa_red_.alloc((size_t)aa_blocks_ * (2 + 2 * mm)); aa_red_.zero(s());
+        if (comm_) { aa_red_g_.alloc(aa_red_.n); aa_red_g_.zero(s()); aag_ = aa_red_g_.p; }
+        else aag_ = aa_red_.p;
     }
     AA_HIP(hipStreamSynchronize(s()));
     initialized_ = true;
@@ -367,6 +434,35 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     }
 }
 
+void ElasticSolver::set_comm(Comm* c) {
+    if (initialized_) throw Error(ERR_STATE, "set_comm after initialize is not supported");
+    comm_ = c;   // size 1 runs the reductions through the transport too (plumbing checks)
+    rank_ = comm_ ? comm_->rank() : 0;
+}
+
+// all-rank sums of the residual block partials (no-op on one GPU: ga_/gb_ alias pa_/pb_)
+void ElasticSolver::reduce_partials() {
+    if (comm_) comm_->allreduce_sum(red_ab_.p, red_gab_.p, 2 * (size_t)nbg_, s());
+}
+
+void ElasticSolver::reduce_aa() {
+    if (comm_) comm_->allreduce_sum(aa_red_.p, aa_red_g_.p, aa_red_.n, s());
+}
+
+// Partitioned: after a step each rank holds valid positions/velocities for its own part, the
+// shared top and the pins. Zero everything else (the top and pins on ranks > 0) and sum over
+// the ranks, so every rank ends the step with the full state (Solver::m_x / m_v).
+void ElasticSolver::gather_state(DevBuf<double>& v) {
+    if (!comm_) return;
+    auto zero = [&](int q0, int q1) {
+        if (q1 > q0) AA_HIP(hipMemsetAsync(v.p + 3 * (size_t)q0, 0, 3 * sizeof(double) * (size_t)(q1 - q0), s()));
+    };
+    zero(0, own_beg_);
+    zero(own_end_, top_beg_);
+    if (rank_ != 0) zero(top_beg_, n_);
+    comm_->allreduce_sum(v.p, v.p, 3 * (size_t)n_, s());
+}
+
 void ElasticSolver::upload_pins() {
     if (!pins_dirty_) return;
     std::vector<double> p(3 * (size_t)np_);
@@ -396,7 +492,7 @@ void ElasticSolver::local_z_all(const double* xfull, const double* u, double* z,
     const bool timed = mode == LZ_NORMAL && red;
     if (timed) ev_begin("local_z");
     for (auto& g : groups_) {
-        launch_local_z(g.d, xfull, u, z, y, nf_, st_.variant, mode, ctrl_.p, red ? red_a_.p : nullptr, off, s());
+        launch_local_z(g.d, xfull, u, z, y, nf_, st_.variant, mode, ctrl_.p, red ? pa_ : nullptr, off, s());
         off += blocks_for(g.d.count);
     }
     if (timed) ev_end("local_z");
@@ -413,6 +509,10 @@ void ElasticSolver::prologue() {
     c.aa_active = accel ? 1 : 0;
     AA_HIP(hipMemcpyAsync(ctrl_.p, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s()));
     launch_predict(n_, nf_, xs_.p, vs_.p, mass_.p, st_.timestep_s, st_.gravity, xbar_.p, Mxbar_.p, xfull_.p, s());
+    // partitioned: the mass term of a shared separator row enters the right-hand side once
+    // (rank 0); the other ranks contribute only their elements' D^T rows to it
+    if (comm_ && rank_ != 0 && top_beg_ < nf_)
+        AA_HIP(hipMemsetAsync(Mxbar_.p + 3 * (size_t)top_beg_, 0, 3 * sizeof(double) * (size_t)(nf_ - top_beg_), s()));
     for (auto& g : groups_) launch_init_z(g.d, xfull_.p, z_.p, s());
     u_.zero(s());
     const long long nx = 3LL * nf_;
@@ -423,7 +523,7 @@ void ElasticSolver::prologue() {
         {
             int off = 0;
             for (auto& g : groups_) {
-                launch_resid_update_u(g.d, xfull_.p, xlast_.p, z_.p, u_.p, nf_, ctrl_.p, red_a_.p, red_b_.p, off, s());
+                launch_resid_update_u(g.d, xfull_.p, xlast_.p, z_.p, u_.p, nf_, ctrl_.p, pa_, pb_, off, s());
                 off += blocks_for(g.d.count);
             }
         }
@@ -450,12 +550,16 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
     const long long nx = 3LL * nf_;
     Ctrl* c = ctrl_.p;
     local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_NORMAL, true);
-    launch_check_restore_ux(c, red_a_.p, red_blocks_, accel, u_.p, xfull_.p, accel ? aa_cur_.p : nullptr, du_.p, dx_.p,
+    reduce_partials();
+    launch_check_restore_ux(c, ga_, nbg_, accel, u_.p, xfull_.p, accel ? aa_cur_.p : nullptr, du_.p, dx_.p,
                             Z_, nx, s());
-    if (accel) local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_REDO, true);
+    if (accel) {
+        local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_REDO, true);
+        reduce_partials();
+    }
     ev_begin("rhs");
     launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s(), xfull_.p, xlast_.p,
-               red_a_.p, red_blocks_);
+               ga_, nbg_);
     ev_end("rhs");
     ev_begin("solve");
     solver_.solve(b_.p, xfull_.p, c, 0, s());
@@ -464,23 +568,25 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
     {
         int off = 0;
         for (auto& g : groups_) {
-            launch_resid_update_u(g.d, xfull_.p, xlast_.p, z_.p, u_.p, nf_, c, red_a_.p, red_b_.p, off, s());
+            launch_resid_update_u(g.d, xfull_.p, xlast_.p, z_.p, u_.p, nf_, c, pa_, pb_, off, s());
             off += blocks_for(g.d.count);
         }
     }
     ev_end("resid");
+    reduce_partials();
     if (accel) {
         const int m = st_.anderson_m;
         Seg2 G{u_.p, Z_, xfull_.p, nx};
         Seg2 cp{du_.p, Z_, dx_.p, nx};
         ev_begin("aa");
-        launch_aa_reduce(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, cp, m, s(), red_a_.p, red_b_.p,
-                         red_blocks_, hist_prim_.p, hist_comb_.p, hist_rej_.p);
-        launch_aa_solve(c, aa_red_.p, aa_blocks_, m, s());
+        launch_aa_reduce(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, cp, m, s(), ga_, gb_, nbg_,
+                         hist_prim_.p, hist_comb_.p, hist_rej_.p);
+        reduce_aa();
+        launch_aa_solve(c, aag_, aa_blocks_, m, s());
         launch_aa_mix(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, G, m, s());
         ev_end("aa");
     } else {
-        launch_control(CTL_COMB_UX, c, red_a_.p, red_b_.p, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+        launch_control(CTL_COMB_UX, c, ga_, gb_, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     }
 }
 
@@ -500,14 +606,15 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
     auto prim_all = [&](const double* xf, const double* z, const double* zref, int redo) {
         int off = 0;
         for (auto& g : groups_) {
-            launch_prim_z(g.d, xf, z, zref, nf_, redo, c, red_a_.p, zref ? red_b_.p : nullptr, off, s());
+            launch_prim_z(g.d, xf, z, zref, nf_, redo, c, pa_, zref ? pb_ : nullptr, off, s());
             off += blocks_for(g.d.count);
         }
     };
     ev_begin("prim");
     prim_all(xfull_.p, z_.p, nullptr, 0);
     ev_end("prim");
-    launch_control(CTL_PRIM_CHECK_Z, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    reduce_partials();
+    launch_control(CTL_PRIM_CHECK_Z, c, ga_, nullptr, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     if (accel) {   // reject branch (gated on the device; a no-op unless prim increased)
         launch_copy(u_.p, du_.p, Z_, c, 1, s());
         launch_copy(xfull_.p, dx_.p, nx, c, 1, s());
@@ -517,8 +624,9 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());
         solver_.solve(b_.p, xfull_.p, c, 1, s());
         prim_all(xfull_.p, z_.p, nullptr, 1);
+        reduce_partials();
     }
-    launch_control(CTL_PRIM_FINAL_Z, c, red_a_.p, nullptr, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    launch_control(CTL_PRIM_FINAL_Z, c, ga_, nullptr, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     if (accel) {
         const int m = st_.anderson_m;
         launch_copy(dx_.p, xfull_.p, nx, c, 0, s());
@@ -531,7 +639,8 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         Seg2 none{nullptr, 0, nullptr, 0};
         ev_begin("aa");
         launch_aa_reduce(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, none, m, s());
-        launch_aa_solve(c, aa_red_.p, aa_blocks_, m, s());
+        reduce_aa();
+        launch_aa_solve(c, aag_, aa_blocks_, m, s());
         launch_aa_mix(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, out, m, s());
         ev_end("aa");
         // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
@@ -549,7 +658,8 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         ev_end("local_z");
         prim_all(xfull_.p, z_.p, lastz_.p, 0);
     }
-    launch_control(CTL_COMB_Z, c, red_a_.p, red_b_.p, red_blocks_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    reduce_partials();
+    launch_control(CTL_COMB_Z, c, ga_, gb_, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
 }
 
 void ElasticSolver::epilogue_enqueue(bool accel) {
@@ -570,6 +680,11 @@ void ElasticSolver::fetch_results() {
     }
     rt_.iterations = c.iters_run;
     rt_.rejects = c.nrej;
+    if (comm_) {   // a failing element prox lives on one rank: agree before throwing
+        double f[2] = {c.fail == 1 ? 1.0 : 0.0, c.fail == 2 ? 1.0 : 0.0};
+        comm_->allreduce_sum_host(f, 2);
+        c.fail = f[0] > 0 ? 1 : (f[1] > 0 ? 2 : 0);
+    }
     if (c.fail == 1) throw Error(ERR_NUMERIC, "the line search step became smaller than the minimum value allowed");
     if (c.fail == 2) throw Error(ERR_NUMERIC, "**TriEnergyTerm TODO: gradient function");
 }
@@ -597,6 +712,8 @@ void ElasticSolver::step() {
         }
     }
     epilogue_enqueue(accel);
+    gather_state(xs_);
+    gather_state(vs_);
     fetch_results();
     // host mirrors of m_x / m_v
     std::vector<double> xs(3 * (size_t)n_), vs(3 * (size_t)n_);

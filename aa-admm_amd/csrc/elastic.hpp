@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/aa_admm.h"
+#include "comm.hpp"
 #include "common.hpp"
 #include "direct_solve.hpp"
 #include "elastic_kernels.hpp"
@@ -28,6 +29,9 @@ public:
     void add_elements(int kind, int material, const double* verts3, const int* idx, int count, const aa_lame& lame,
                       int vertex_offset);
     void set_pins(const int* inds, const double* pts3, int n);
+    // multi-GPU: partition the mesh over comm's ranks at initialize(); every
+    // rank passes the same scene. Not owned; must outlive the solver.
+    void set_comm(Comm* c);
     void initialize(const aa_settings& s);
     void step();
 
@@ -80,12 +84,22 @@ private:
     DevBuf<double> dt_val_;
     DevBuf<double> xs_, vs_, mass_, xfull_, xlast_, xbar_, Mxbar_, b_, cxfull_;
     DevBuf<double> z_, u_, y_, du_, dz_, dx_, lastz_, cz_;
-    DevBuf<double> aa_cur_, aa_dF_, aa_dG_, aa_red_;
-    DevBuf<double> red_a_, red_b_;
+    DevBuf<double> aa_cur_, aa_dF_, aa_dG_, aa_red_, aa_red_g_;
+    // residual block partials: this rank's [a | b] (pa_, pb_) and their sums over the ranks
+    // (ga_, gb_; aliases of pa_, pb_ on one GPU); nbg_ = the largest rank's block count
+    DevBuf<double> red_ab_, red_gab_;
+    double *pa_ = nullptr, *pb_ = nullptr, *ga_ = nullptr, *gb_ = nullptr, *aag_ = nullptr;
+    int nbg_ = 0;
     DevBuf<Ctrl> ctrl_;
     DevBuf<double> hist_prim_, hist_comb_;
     DevBuf<int> hist_rej_;
     int red_blocks_ = 0, aa_blocks_ = 0, hist_cap_ = 0;
+    // partition: own free nodes [own_beg_, own_end_), shared top [top_beg_, nf_)
+    Comm* comm_ = nullptr;
+    int rank_ = 0, own_beg_ = 0, own_end_ = 0, top_beg_ = 0;
+    void reduce_partials();
+    void reduce_aa();
+    void gather_state(DevBuf<double>& v);
     std::vector<double> h_prim_, h_comb_;
     std::vector<int> h_rej_;
     int nrec_ = 0;

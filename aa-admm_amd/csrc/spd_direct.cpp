@@ -28,15 +28,9 @@ struct NdBuilder {
     NdBuilder(int n_, const double* x_, const std::vector<int>& p_, const std::vector<int>& j_, int l_)
         : n(n_), xyz(x_), ap(p_), aj(j_), leaf(l_), mark(n_, 0), side(n_, 0) {}
 
-    // returns the list of root node ids of the forest built over `verts`
-    std::vector<int> build(std::vector<int> verts) {
-        if (verts.empty()) return {};
-        if ((int)verts.size() <= leaf) {
-            std::sort(verts.begin(), verts.end());
-            piv.push_back(verts);
-            kids.push_back({});
-            return {(int)piv.size() - 1};
-        }
+    // one bisection step: median split along the longest bounding-box axis, then the vertices of
+    // the lower half adjacent to the upper half form the (one-sided) vertex separator
+    void split(std::vector<int>& verts, std::vector<int>& left, std::vector<int>& right, std::vector<int>& sep) {
         double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
         for (int v : verts)
             for (int d = 0; d < 3; ++d) { lo[d] = std::min(lo[d], xyz[3 * v + d]); hi[d] = std::max(hi[d], xyz[3 * v + d]); }
@@ -50,7 +44,6 @@ struct NdBuilder {
         });
         const int st = ++stamp;
         for (size_t i = 0; i < verts.size(); ++i) { mark[verts[i]] = st; side[verts[i]] = i < half ? 0 : 1; }
-        std::vector<int> left, right, sep;
         for (size_t i = 0; i < verts.size(); ++i) {
             int v = verts[i];
             if (i >= half) { right.push_back(v); continue; }
@@ -61,31 +54,66 @@ struct NdBuilder {
             }
             (touches ? sep : left).push_back(v);
         }
-        if (left.empty() && right.empty()) {  // degenerate: everything is separator
-            std::sort(sep.begin(), sep.end());
-            piv.push_back(sep);
-            kids.push_back({});
-            return {(int)piv.size() - 1};
-        }
+    }
+
+    int add_node(std::vector<int> p, std::vector<int> k) {
+        std::sort(p.begin(), p.end());
+        piv.push_back(std::move(p));
+        kids.push_back(std::move(k));
+        return (int)piv.size() - 1;
+    }
+
+    // returns the list of root node ids of the forest built over `verts`
+    std::vector<int> build(std::vector<int> verts) {
+        if (verts.empty()) return {};
+        if ((int)verts.size() <= leaf) return {add_node(std::move(verts), {})};
+        std::vector<int> left, right, sep;
+        split(verts, left, right, sep);
+        if (left.empty() && right.empty()) return {add_node(std::move(sep), {})};  // degenerate
         std::vector<int> roots = build(std::move(left));
         std::vector<int> r2 = build(std::move(right));
         roots.insert(roots.end(), r2.begin(), r2.end());
         if (sep.empty()) return roots;
-        std::sort(sep.begin(), sep.end());
-        piv.push_back(sep);
-        kids.push_back(roots);
-        return {(int)piv.size() - 1};
+        return {add_node(std::move(sep), roots)};
+    }
+
+    // the top `levels` bisections are forced (one part per leaf of the top, in left-to-right
+    // order); each part is then dissected by build(). part_of[node] = part id, -1 = top separator
+    std::vector<int> part_of;
+    std::vector<int> build_parts(std::vector<int> verts, int levels, int& next_part) {
+        if (levels == 0) {
+            const int id = next_part++;
+            const size_t first = piv.size();
+            std::vector<int> r = build(std::move(verts));
+            part_of.resize(piv.size(), -1);
+            for (size_t k = first; k < piv.size(); ++k) part_of[k] = id;
+            return r;
+        }
+        std::vector<int> left, right, sep;
+        if (!verts.empty()) split(verts, left, right, sep);
+        if (left.empty() && right.empty() && !sep.empty()) std::swap(left, sep);   // tiny: keep it in a part
+        std::vector<int> roots = build_parts(std::move(left), levels - 1, next_part);
+        std::vector<int> r2 = build_parts(std::move(right), levels - 1, next_part);
+        roots.insert(roots.end(), r2.begin(), r2.end());
+        if (sep.empty()) return roots;
+        const int s = add_node(std::move(sep), roots);
+        part_of.resize(piv.size(), -1);
+        return {s};
     }
 };
 }  // namespace
 
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                         int leaf_size, int top_rows) {
+                         int leaf_size, int top_rows, int part_levels) {
     NdBuilder b(n, xyz, adj_ptr, adj, std::max(1, leaf_size));
     std::vector<int> all(n);
     std::iota(all.begin(), all.end(), 0);
-    std::vector<int> roots = b.build(all);
+    int nparts = 0;
+    std::vector<int> roots = part_levels > 0 ? b.build_parts(all, part_levels, nparts) : b.build(all);
     std::vector<std::vector<int>> piv = std::move(b.piv), kids = std::move(b.kids);
+    std::vector<int> part_of = std::move(b.part_of);
+    part_of.resize(piv.size(), part_levels > 0 ? -1 : 0);
+    if (part_levels > 0) top_rows = 0;   // the partition roots must stay separate supernodes
     // ---- amalgamate the top of the tree into one dense supernode: the upper levels have few,
     // mid-sized supernodes whose level-by-level solve is pure latency; as one dense block they
     // are a single wide GEMV per sweep.
@@ -123,18 +151,37 @@ NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_p
             roots = {(int)piv.size() - 1};
         }
     }
-    // ---- postorder numbering from the roots (children first)
+    // ---- postorder numbering from the roots (children first). Partitioned: the subtrees of
+    // part 0, 1, ... first (each a contiguous pivot range), then the top separators in
+    // postorder -- every GPU's own rows and the shared separator rows are then contiguous.
     NdTree t;
     std::vector<int> order;
     std::function<void(int)> dfs = [&](int s) {
         for (int c : kids[s]) dfs(c);
         order.push_back(s);
     };
-    for (int r : roots) dfs(r);
+    if (part_levels > 0) {
+        std::vector<std::vector<int>> part_roots(nparts);
+        std::function<void(int)> find = [&](int s) {
+            if (part_of[s] >= 0) { part_roots[part_of[s]].push_back(s); return; }
+            for (int c : kids[s]) find(c);
+        };
+        for (int r : roots) find(r);
+        for (auto& pr : part_roots) for (int r : pr) dfs(r);
+        std::function<void(int)> dfs_top = [&](int s) {
+            for (int c : kids[s]) if (part_of[c] < 0) dfs_top(c);
+            order.push_back(s);
+        };
+        for (int r : roots) if (part_of[r] < 0) dfs_top(r);
+    } else {
+        for (int r : roots) dfs(r);
+    }
     const int nn = (int)order.size();
     std::vector<int> newid(piv.size(), -1);
     for (int i = 0; i < nn; ++i) newid[order[i]] = i;
     t.beg.resize(nn); t.end.resize(nn); t.parent.assign(nn, -1); t.children.resize(nn);
+    t.part.assign(nn, 0);
+    t.n_parts = part_levels > 0 ? nparts : 1;
     int c = 0;
     for (int i = 0; i < nn; ++i) {
         const int s = order[i];
@@ -142,9 +189,28 @@ NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_p
         for (int v : piv[s]) t.perm.push_back(v);
         c += (int)piv[s].size();
         t.end[i] = c;
+        t.part[i] = s < (int)part_of.size() ? part_of[s] : (part_levels > 0 ? -1 : 0);
         for (int k : kids[s]) { t.children[i].push_back(newid[k]); t.parent[newid[k]] = i; }
     }
     if (c != n) throw std::runtime_error("nested_dissection: lost vertices");
+    // pivot ranges of the parts and of the shared top (partitioned ordering only)
+    t.part_beg.assign(t.n_parts, 0);
+    t.part_end.assign(t.n_parts, 0);
+    t.top_beg = part_levels > 0 ? n : 0;
+    if (part_levels > 0) {
+        int cur = 0;
+        for (int pp = 0; pp < t.n_parts; ++pp) {
+            t.part_beg[pp] = cur;
+            for (int i = 0; i < nn; ++i) if (t.part[i] == pp) cur = std::max(cur, t.end[i]);
+            t.part_end[pp] = cur;
+        }
+        t.top_beg = cur;
+        for (int i = 0; i < nn; ++i)
+            if ((t.part[i] < 0) != (t.beg[i] >= t.top_beg) && t.end[i] > t.beg[i])
+                throw std::runtime_error("nested_dissection: partitioned ordering is not contiguous");
+    } else {
+        t.part_end[0] = n;
+    }
     return t;
 }
 
@@ -245,9 +311,16 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree) {
 }
 
 void factor_solve_host(const SupernodalFactor& F, std::vector<double>& b) {
+    factor_solve_host_part(F, nullptr, -1, b, nullptr);
+}
+
+void factor_solve_host_part(const SupernodalFactor& F, const NdTree* T, int part, std::vector<double>& b,
+                            const std::function<void(double*, size_t)>& reduce_top) {
     const int nn = F.n_nodes;
+    auto skip = [&](int s) { return T && T->part[s] != part && T->part[s] != -1; };
     std::vector<double> t;
     for (int s = 0; s < nn; ++s) {  // forward (postorder)
+        if (skip(s)) continue;
         const int b0 = F.beg[s], p = F.end[s] - b0, nb = (int)F.bnd[s].size();
         t.assign((size_t)p * 3, 0.0);
         for (int i = 0; i < p; ++i)
@@ -258,7 +331,11 @@ void factor_solve_host(const SupernodalFactor& F, std::vector<double>& b) {
             for (int j = 0; j < p; ++j)
                 for (int c = 0; c < 3; ++c) b[3 * (size_t)F.bnd[s][a] + c] -= F.LBP[s][(size_t)a * p + j] * t[3 * j + c];
     }
+    // partitioned: the top rows now hold this rank's share of the forward result (linear in
+    // the right-hand side and in the children's update vectors) -- their sum is the full one
+    if (T && reduce_top && T->top_beg < F.n) reduce_top(b.data() + 3 * (size_t)T->top_beg, 3 * (size_t)(F.n - T->top_beg));
     for (int s = nn - 1; s >= 0; --s) {  // backward
+        if (skip(s)) continue;
         const int b0 = F.beg[s], p = F.end[s] - b0, nb = (int)F.bnd[s].size();
         t.assign((size_t)p * 3, 0.0);
         for (int j = 0; j < p; ++j)

@@ -11,6 +11,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 namespace aa {
@@ -28,11 +29,19 @@ struct NdTree {
     std::vector<int> beg, end;      // pivot range of node s in new indexing
     std::vector<int> parent;        // -1 for roots
     std::vector<std::vector<int>> children;
+    std::vector<int> part;          // partition of node s (part_levels > 0), -1 = top separator
+    int n_parts = 1;
+    // partitioned ordering: part q owns pivots [part_beg[q], part_end[q]) (contiguous, in
+    // part order), the shared top separators are [top_beg, n)
+    std::vector<int> part_beg, part_end;
+    int top_beg = 0;
 };
 // top_rows > 0: the upper levels of the tree (up to top_rows pivots) are amalgamated into
-// one dense root supernode.
+// one dense root supernode. part_levels = L > 0: the first L bisections are forced and give
+// 2^L parts (one per GPU of the partitioned solver); their separators form the "top" of the
+// tree (part -1) and no amalgamation is done.
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                         int leaf_size, int top_rows = 0);
+                         int leaf_size, int top_rows = 0, int part_levels = 0);
 
 struct SupernodalFactor {
     int n = 0;
@@ -52,5 +61,13 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree);
 
 // Host reference solve with the factor (used by self-checks): x = A^-1 b, b is n x 3.
 void factor_solve_host(const SupernodalFactor& F, std::vector<double>& b3);
+
+// Host reference of ONE rank's share of the partitioned solve (tests/cpp/part_solve.cpp):
+// forward over the supernodes of `part` and of the top with b3 holding this rank's PARTIAL
+// right-hand side (its own rows complete, top rows partial), `reduce_top` sums the top rows
+// [top_beg, n) x 3 over the ranks, then backward over the same supernodes. On return the rows
+// of the part and of the top hold x; other rows are untouched.
+void factor_solve_host_part(const SupernodalFactor& F, const NdTree* T, int part, std::vector<double>& b3,
+                            const std::function<void(double*, size_t)>& reduce_top);
 
 }  // namespace aa

@@ -102,6 +102,31 @@ int aa_elastic_set_v(aa_elastic h, const double* v3);
 int aa_elastic_get_history(aa_elastic h, double* prim, double* comb, int* reject, int cap, int* n);
 int aa_elastic_runtime(aa_elastic h, aa_runtime* out);                   /* runtime_data()    */
 
+/* ---- multi-GPU: mesh partitioned over the GPUs of one node -----------
+ * The reference is one OpenMP process (no MPI/NCCL); this is new surface. One process per GPU;
+ * every rank builds the SAME scene through the calls above, attaches a communicator, then
+ * initialize() partitions the free nodes by nested dissection into `size` parts (a power of
+ * two) plus the shared separator rows, and each rank keeps the elements of its part. step()
+ * runs the identical reference iteration on all ranks (all-reduced residuals, Anderson dot
+ * products and separator rows of the global solve); afterwards every rank holds the full
+ * x and v. */
+typedef struct aa_comm_s* aa_comm;
+/* Host transport callback: in-place SUM of n doubles over all ranks; return 0 on success. */
+typedef int (*aa_host_allreduce_fn)(double* buf, long long n, void* user);
+/* ncclGetUniqueId: called on rank 0, the 128 bytes are broadcast by the caller. */
+int aa_comm_unique_id(unsigned char id[128]);
+/* RCCL communicator over xGMI on ctx's GPU (ncclCommInitRank; collective over all ranks). */
+int aa_comm_create_rccl(aa_ctx ctx, const unsigned char id[128], int rank, int size, aa_comm* out);
+/* Host-staged transport through a caller callback (e.g. torch.distributed/gloo); lets several
+ * ranks share one GPU (tests). Never captured into a hipGraph. */
+int aa_comm_create_host(aa_host_allreduce_fn fn, void* user, int rank, int size, aa_comm* out);
+int aa_comm_destroy(aa_comm c);
+int aa_comm_info(aa_comm c, int* rank, int* size);
+/* In-place SUM of a host array over the ranks (blocking; setup-time agreements, tests). */
+int aa_comm_allreduce_host(aa_comm c, double* buf, long long n);
+/* Attach before aa_elastic_initialize; the communicator must outlive the solver. */
+int aa_elastic_set_comm(aa_elastic h, aa_comm c);
+
 /* ---- benchmarking hooks (device-resident inputs, no host traffic) ------------------ */
 /* Enqueue `iters` iterations of the ADMM loop of the current time step without the
  * per-step prologue/epilogue; used by bench.py to time the hot loop alone. */

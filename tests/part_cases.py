@@ -1,0 +1,26 @@
+"""Scenes of the partitioned-solver GPU tests: (builder, tolerance relative to comb_0 / |x|).
+Closed-form element paths 1e-9, L-BFGS (NeoHookean) paths 1e-6 -- the same bars as the
+single-GPU parity tests; the partitioned run only reorders floating-point sums."""
+import importlib
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+scenes = importlib.import_module("aa-admm_amd.scenes")
+
+CASES = {
+    # (u,x)-AA cloth with two pinned corners (C2 recipe, 3 200 tris)
+    "cloth_ux": (lambda: scenes.cloth(40, 40, iters=60, n_steps=3), 1e-9),
+    # (u,x)-AA linear cantilever, x=0 face pinned
+    "cant_ux": (lambda: scenes.cantilever(12, 3, 3, scenes.LINEAR, iters=40, n_steps=2,
+                                          variant=scenes.VARIANT_H), 1e-9),
+    # z-AA NeoHookean block drop (C4 recipe, 1 440 tets), no pins
+    "drop_z": (lambda: scenes.tet_drop(12, 4, 6, iters=40, n_steps=2), 1e-6),
+    # z-AA beams with moving pins (C1 recipe)
+    "beams_z": (lambda: scenes.beams(3, iters=50, n_steps=2, variant=scenes.VARIANT_X), 1e-6),
+    # no Anderson, z order, linear tets
+    "cant_z_noaa": (lambda: scenes.cantilever(10, 3, 3, scenes.LINEAR, iters=30, n_steps=2,
+                                              variant=scenes.VARIANT_X, accel=0), 1e-9),
+}

@@ -1,0 +1,48 @@
+"""One rank of a partitioned elastic run (launched by torch.distributed.run from
+tests/test_gpu_partition.py). Every rank binds the same scene, attaches a communicator and
+runs the time steps; rank r writes its per-step history and final state to OUT/rank{r}.npz.
+
+    AA_CASE=<name> AA_TRANSPORT=host|rccl AA_OUT=<dir> python -m torch.distributed.run ... part_worker.py
+"""
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+from part_cases import CASES  # noqa: E402
+
+
+def main():
+    pkg = importlib.import_module("aa-admm_amd")
+    dist.init_process_group("gloo")
+    rank, size = dist.get_rank(), dist.get_world_size()
+    sc = CASES[os.environ["AA_CASE"]][0]()
+    device = int(os.environ.get("AA_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    ctx = pkg.capi.Context(device)
+    if os.environ.get("AA_TRANSPORT", "host") == "rccl":
+        comm = pkg.dist.rccl_comm(ctx, rank, size)
+    else:
+        comm = pkg.dist.host_comm(rank, size)
+    steps, s = pkg.capi.run_scene(ctx, sc, comm=comm)
+    out = {}
+    for k, st in enumerate(steps):
+        for key in ("prim", "comb", "reject", "x", "v"):
+            out[f"{key}{k}"] = st[key]
+    rt = s.runtime()
+    out["n_elements"] = np.array([rt.n_elements])
+    out["iterations"] = np.array([rt.iterations])
+    np.savez(os.path.join(os.environ["AA_OUT"], f"rank{rank}.npz"), **out)
+    s.close()
+    comm.close()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
