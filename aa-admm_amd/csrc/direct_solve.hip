@@ -4,6 +4,7 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 
@@ -382,6 +383,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     std::vector<std::vector<int>> kids(nn_);
     for (int sn = 0; sn < nn_; ++sn) if (F.parent[sn] >= 0 && inc[sn]) kids[F.parent[sn]].push_back(sn);
     const char* ms = std::getenv("AA_SOLVE_MIN_SUBTREES");
+    const bool stats = std::getenv("AA_SOLVE_STATS") != nullptr;
     const int min_sub = ms ? std::atoi(ms) : 96;
     constexpr int kSubLds = 64 * 1024, kMaxItemRow = 0xffff;
     auto roots_at = [&](int H) {
@@ -476,6 +478,14 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             }
         }
         n_sub_ = (int)strees.size();
+        if (stats) {
+            double by = 0;
+            int nsn = 0;
+            for (int sn = 0; sn < nn_; ++sn)
+                if (fused[sn]) { by += 8.0 * (0.5 * p[sn] * (p[sn] + 1.0) + (double)p[sn] * nb[sn]); ++nsn; }
+            std::fprintf(stderr, "[solve] fused subtrees: %d (cut height %d), %d supernodes, %.2f MB/sweep, lds f %d b %d\n",
+                         n_sub_, cut_height_, nsn, by / 1e6, sub_lds_f_, sub_lds_b_);
+        }
         sub_nodes_.upload(snodes, s);
         sub_levels_.upload(slevels, s);
         sub_trees_.upload(strees, s);
@@ -541,6 +551,18 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         max_lds = std::max(max_lds, std::max(L.lds_fwd, L.lds_bwd));
         kernels_ += 2 + (L.asm_count ? 1 : 0);
         levels_.push_back(L);
+        if (stats) {
+            double by = 0;
+            int maxp = 0, maxnb = 0, nw = 0;
+            for (int sn : l) {
+                by += 8.0 * (0.5 * p[sn] * (p[sn] + 1.0) + (double)p[sn] * nb[sn]);
+                maxp = std::max(maxp, p[sn]); maxnb = std::max(maxnb, nb[sn]);
+                nw += p[sn] > kWaveP;
+            }
+            std::fprintf(stderr, "[solve] level %zu: %zu supernodes (%d wave), max p %d, max nb %d, %.2f MB/sweep, "
+                         "fwd tasks %d (blk %d) bwd tasks %d (blk %d)\n", levels_.size() - 1, l.size(), nw, maxp, maxnb,
+                         by / 1e6, L.fwd_count, L.fblock, L.bwd_count, L.bblock);
+        }
     }
     if (n_sub_) kernels_ += 2;
     bnd_.upload(bnd, s);

@@ -13,6 +13,8 @@ from . import capi
 
 def rccl_comm(ctx: capi.Context, rank: int, size: int, group=None) -> capi.Comm:
     """RCCL communicator over xGMI: rank 0 creates the unique id, torch.distributed broadcasts it."""
+    if size == 1:
+        return capi.Comm.rccl(ctx, 0, 1, capi.Comm.unique_id())
     import torch.distributed as dist
     obj = [capi.Comm.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0, group=group)
@@ -22,6 +24,8 @@ def rccl_comm(ctx: capi.Context, rank: int, size: int, group=None) -> capi.Comm:
 def host_comm(rank: int, size: int, group=None) -> capi.Comm:
     """Host-staged transport over torch.distributed (gloo): SUM then a broadcast from rank 0,
     so every rank receives bit-identical values whatever the backend's reduction order."""
+    if size == 1:
+        return capi.Comm.host(lambda a: None, 0, 1)
     import torch
     import torch.distributed as dist
 

@@ -2,14 +2,18 @@
 """Benchmark of the admm-elastic hot path on MI355X (BASELINE.json metric: ADMM iterations/s
 and time-to-epsilon).
 
-Workload (BASELINE.json configs[1]): cloth drop, make_tri_blocks(112,112) = 50 176 triangles,
-25 313 nodes, Lame(50, 0.1) with strain limits [0.95, 1.05], (u,x)-Anderson m=6
-(admm_anderson_hard_zxu), dt = 1/30, 100 ADMM iterations per time step (windyflag settings).
-A bench "step" is one Solver::step() time step; `value` = ADMM iterations executed by all
-ranks / max-over-ranks wall time. Synthetic input (generated mesh, no datasets).
+Default workload (BASELINE.json configs[3], the 1M-tet elastic drop that north_star's target
+names for 1/2/4/8 GPUs): make_tet_blocks(100,40,50) = 1 000 000 NeoHookean tets, 211 191 nodes,
+initial pose squashed 0.9 in y, free fall, z-Anderson m=6 (admm_anderson_xzu order), dt = 1/30,
+100 ADMM iterations per time step. --config c2: cloth drop make_tri_blocks(112,112) = 50 176
+triangles, (u,x)-Anderson m=6 (configs[1]); c3 / c5: the Geometry ALM configs.
+A bench "step" is one Solver::step() time step; `value` = ADMM iterations executed / max-over-
+ranks wall time. Synthetic input (generated mesh, no datasets).
 
-Multi-GPU: one process per GPU (torchrun); each rank runs an independent replica of the
-scene ("replicas only" until mesh partitioning lands), weak scaling.
+Multi-GPU: one process per GPU (torchrun). Elastic configs partition ONE mesh over the ranks
+(--partition rccl, the default for N>1: nested-dissection parts, separator rows of the global
+solve and all residual/Anderson partials all-reduced on RCCL over xGMI; strong scaling);
+--partition none runs independent replicas (weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--iters 100] [--no-cpu-baseline]
 """
@@ -43,10 +47,16 @@ def parse():
     p.add_argument("--nx", type=int, default=112)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-iters", type=int, default=40)
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
-                   help="c2: cloth (BASELINE configs[1], the headline); c3: planar-quad 317x317 (configs[2]); "
-                        "c4: 1M-tet NeoHookean block drop (configs[3]); c5: wire mesh 707x707 (configs[4])")
+    p.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5"],
+                   help="c4 (default): 1M-tet NeoHookean block drop (configs[3]) -- the workload north_star's "
+                        "target names for 1/2/4/8 GPUs; c2: cloth 50k tris (configs[1]); c3: planar-quad 317x317 "
+                        "(configs[2]); c5: wire mesh 707x707 (configs[4])")
     p.add_argument("--tets", type=str, default="100,40,50", help="c4 block size in cubes (5 tets per cube)")
+    p.add_argument("--partition", default="auto", choices=["auto", "none", "rccl", "host"],
+                   help="elastic configs with N>1: partition ONE mesh over the ranks (rccl: RCCL over xGMI, one "
+                        "GPU per rank; host: host-staged gloo transport, for rehearsals with several ranks on one "
+                        "GPU) or run independent replicas (none). auto = rccl when N>1")
+    p.add_argument("--same-device", action="store_true", help="all ranks on GPU 0 (rehearsal with --partition host)")
     return p.parse_args()
 
 
@@ -266,9 +276,20 @@ def main():
     pkg = importlib.import_module("aa-admm_amd")
     capi = pkg.capi
 
-    ctx = capi.Context(local)
+    ctx = capi.Context(0 if args.same_device else local)
     sc, desc = elastic_scene(args)
-    solver = capi.solver_from_scene(ctx, sc)
+    part = args.partition if args.partition != "auto" else ("rccl" if world > 1 else "none")
+    comm = None
+    if part == "rccl":
+        try:
+            comm = pkg.dist.rccl_comm(ctx, rank, world)
+        except Exception as e:   # transport only: the compute stays on the GPUs either way
+            print(f"[bench] RCCL communicator failed ({e}); using the host-staged transport", file=sys.stderr)
+            part = "host (rccl init failed)"
+            comm = pkg.dist.host_comm(rank, world)
+    elif part == "host":
+        comm = pkg.dist.host_comm(rank, world)
+    solver = capi.solver_from_scene(ctx, sc, comm)
     t0 = time.time()
     solver.initialize(capi.settings_from_scene(sc))
     setup_ms = (time.time() - t0) * 1e3
@@ -287,14 +308,20 @@ def main():
     barrier(dist, ctx)
     elapsed = time.perf_counter() - t0
     elapsed_max = allreduce(dist, elapsed, _max_op(dist))
-    iters_all = allreduce(dist, float(iters_run), _sum_op(dist))
+    # replicas: every rank ran its own copy of the scene (weak scaling); partitioned: all ranks
+    # ran ONE scene together (strong scaling), its iterations count once
+    iters_all = float(iters_run) if comm is not None else allreduce(dist, float(iters_run), _sum_op(dist))
     value = iters_all / elapsed_max
 
     # roofline of the dominant kernel class, timed live with HIP events on the solver's stream
-    # (separate instrumented pass of the same iteration loop, after the timed region)
+    # (separate instrumented pass of the same iteration loop, after the timed region; every
+    # rank of a partitioned run takes part -- the loop has collectives)
     roof = None
-    if rank == 0:
+    if comm is not None:
         solver.bench_iterations(min(args.iters, 50))
+    if rank == 0:
+        if comm is None:
+            solver.bench_iterations(min(args.iters, 50))
         names = ("local_z", "solve", "resid", "rhs", "aa") if sc.variant == 1 else \
                 ("grad", "rhs", "solve", "prim", "local_z", "aa", "comb")
         stats = {k: solver.kernel_stats(k) for k in names}
@@ -322,20 +349,26 @@ def main():
         line = {
             "metric": "ADMM iters/sec + time-to-eps (primal+dual residual)", "value": round(value, 2),
             "unit": "ADMM iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed_max * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(elapsed_max * 1e3 / args.steps, 3), "higher_is_better": True,
+            "scaling": "strong" if comm is not None else "weak",
             "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (generated make_tet_blocks mesh)" if args.config == "c4"
                     else "synthetic (generated make_tri_blocks mesh)",
             "config": {"workload": desc, "nodes": sc.n_nodes, "elements": sc.n_elements(),
-                       "admm_iters_per_step": args.iters, "anderson_m": sc.aa_m, "parallelism": f"replicas{world}",
+                       "admm_iters_per_step": args.iters, "anderson_m": sc.aa_m,
+                       "parallelism": (f"mesh-partitioned{world} ({part})" if comm is not None else f"replicas{world}"),
                        "global_solve": "supernodal direct", "nnz_factor": rt.nnz_factor,
                        "setup_ms": round(setup_ms, 1)},
             "iters_executed": int(iters_all),
             "time_to_eps_ms": (round(statistics.median(tt), 3) if tt else None), "eps_rel": EPS_ELASTIC,
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if comm is not None:
+            line["config"]["partition"] = {"elements_rank0": rt.n_elements, "z_dim_rank0": rt.z_dim}
         print(json.dumps(line))
     solver.close()
+    if comm is not None:
+        comm.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
