@@ -174,6 +174,133 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
     }
 }
 
+// Backward sweep of the large supernodes (R > kWaveR) as a split-K GEMV: tile = 64 columns
+// (lanes) x kBwdTileRows rows (4 waves x 32 rows) of the row-major G, the tile's slice of
+// [y_P ; -x_B] staged in LDS, one 64 x 3 partial per tile; k_bwd_red sums the partials of each
+// column block in tile order (deterministic). Gives (columns/64) x (rows/128) workgroups per
+// supernode instead of one wave per column with a serial loop over all R rows.
+using BTile = DirectSolver::BTile;
+using BRed = DirectSolver::BRed;
+constexpr int kBwdTileRows = 128;
+
+__global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tiles, int first, const double* __restrict__ Gr,
+                                                  const int* __restrict__ bnd, const double* __restrict__ Y,
+                                                  const double* __restrict__ X, double* __restrict__ part,
+                                                  const Ctrl* ctrl, int gate_reject) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    __shared__ double v[3 * kBwdTileRows];
+    __shared__ double red[3][3 * 64];
+    const BTile t = tiles[first + blockIdx.x];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < t.nr; i += 256) {
+        const int r = t.r0 + i;
+        if (r < t.p) {
+            const size_t o = 3 * (size_t)(t.beg + r);
+            v[3 * i] = Y[o]; v[3 * i + 1] = Y[o + 1]; v[3 * i + 2] = Y[o + 2];
+        } else {
+            const size_t o = 3 * (size_t)bnd[t.bnd_off + r - t.p];
+            v[3 * i] = -X[o]; v[3 * i + 1] = -X[o + 1]; v[3 * i + 2] = -X[o + 2];
+        }
+    }
+    __syncthreads();
+    const int lane = tid & 63, w = tid >> 6;
+    const int c = t.c0 + lane;
+    constexpr int per = kBwdTileRows / 4;
+    const int i0 = w * per, i1 = min(i0 + per, t.nr);
+    double a0 = 0, a1 = 0, a2 = 0;
+    if (c < t.p) {
+        const double* G = Gr + t.goff + (size_t)t.r0 * t.p + c;
+#pragma unroll 8
+        for (int i = i0; i < i1; ++i) {
+            const double g = G[(size_t)i * t.p];
+            a0 += g * v[3 * i]; a1 += g * v[3 * i + 1]; a2 += g * v[3 * i + 2];
+        }
+    }
+    if (w > 0) { red[w - 1][3 * lane] = a0; red[w - 1][3 * lane + 1] = a1; red[w - 1][3 * lane + 2] = a2; }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { a0 += red[k][3 * lane]; a1 += red[k][3 * lane + 1]; a2 += red[k][3 * lane + 2]; }
+        double* o = part + t.poff + 3 * lane;
+        o[0] = a0; o[1] = a1; o[2] = a2;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_bwd_red(const BRed* __restrict__ reds, int first, const double* __restrict__ part,
+                                                double* __restrict__ X, const Ctrl* ctrl, int gate_reject) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    const BRed t = reds[first + blockIdx.x];
+    const int lane = threadIdx.x;
+    if (lane >= t.nc) return;
+    double a0 = 0, a1 = 0, a2 = 0;
+    const double* q = part + t.poff + 3 * lane;
+    for (int k = 0; k < t.nt; ++k, q += 3 * 64) { a0 += q[0]; a1 += q[1]; a2 += q[2]; }
+    const size_t o = 3 * (size_t)(t.beg + t.c0 + lane);
+    X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
+}
+
+// Forward sweep of the large supernodes (p > kWaveP) as a split-K GEMV on the column-major G:
+// tile = 64 rows (lanes) x kFwdTileCols columns (4 waves x 32), the tile's slice of the
+// assembled front f_P staged in LDS, one 64 x 3 partial per tile; k_fwd_red sums a row block's
+// partials in tile order and writes y_P (rows < p) or the update vector u = f_B - M f_P.
+using FTile = DirectSolver::FTile;
+using FRed = DirectSolver::FRed;
+constexpr int kFwdTileCols = 128;
+
+__global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tiles, int first, const double* __restrict__ Gc,
+                                                  const double* __restrict__ Fg, double* __restrict__ part,
+                                                  const Ctrl* ctrl, int gate_reject) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    __shared__ double f[3 * kFwdTileCols];
+    __shared__ double red[3][3 * 64];
+    const FTile t = tiles[first + blockIdx.x];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 3 * t.nc; i += 256) f[i] = Fg[t.foff + 3 * (size_t)t.c0 + i];
+    __syncthreads();
+    const int lane = tid & 63, w = tid >> 6;
+    const int r = t.r0 + lane;
+    constexpr int per = kFwdTileCols / 4;
+    const int i0 = w * per, i1 = min(i0 + per, t.nc);
+    double a0 = 0, a1 = 0, a2 = 0;
+    if (r < t.R) {
+        const double* G = Gc + t.goff + (size_t)t.c0 * t.R + r;
+#pragma unroll 8
+        for (int i = i0; i < i1; ++i) {
+            const double g = G[(size_t)i * t.R];
+            a0 += g * f[3 * i]; a1 += g * f[3 * i + 1]; a2 += g * f[3 * i + 2];
+        }
+    }
+    if (w > 0) { red[w - 1][3 * lane] = a0; red[w - 1][3 * lane + 1] = a1; red[w - 1][3 * lane + 2] = a2; }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { a0 += red[k][3 * lane]; a1 += red[k][3 * lane + 1]; a2 += red[k][3 * lane + 2]; }
+        double* o = part + t.poff + 3 * lane;
+        o[0] = a0; o[1] = a1; o[2] = a2;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_fwd_red(const FRed* __restrict__ reds, int first, const double* __restrict__ part,
+                                                const double* __restrict__ Fg, double* __restrict__ Y,
+                                                double* __restrict__ U, const Ctrl* ctrl, int gate_reject) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    const FRed t = reds[first + blockIdx.x];
+    const int lane = threadIdx.x;
+    if (lane >= t.nr) return;
+    double a0 = 0, a1 = 0, a2 = 0;
+    const double* q = part + t.poff + 3 * lane;
+    for (int k = 0; k < t.nt; ++k, q += 3 * 64) { a0 += q[0]; a1 += q[1]; a2 += q[2]; }
+    const int r = t.r0 + lane;
+    if (r < t.p) {
+        const size_t o = 3 * (size_t)(t.beg + r);
+        Y[o] = a0; Y[o + 1] = a1; Y[o + 2] = a2;
+    } else {
+        const double* fb = Fg + t.foff + 3 * (size_t)r;
+        double* u = U + t.uoff + 3 * (size_t)(r - t.p);
+        u[0] = fb[0] - a0; u[1] = fb[1] - a1; u[2] = fb[2] - a2;
+    }
+}
+
 using SubNode = DirectSolver::SubNode;
 using SubLevel = DirectSolver::SubLevel;
 using SubTree = DirectSolver::SubTree;
@@ -191,7 +318,8 @@ __device__ __forceinline__ void sub_front_row(const SubNode& t, int q, const lon
 }
 
 // forward sweep of a whole bottom subtree (one workgroup), its levels bottom-up
-__global__ __launch_bounds__(256) void k_fwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
                                                  const SubNode* __restrict__ nodes, const int* __restrict__ items,
                                                  const double* __restrict__ Gc, const long long* __restrict__ ell,
                                                  const double* __restrict__ B, double* __restrict__ Y,
@@ -202,7 +330,7 @@ __global__ __launch_bounds__(256) void k_fwd_sub(const SubTree* __restrict__ tre
     const int tid = threadIdx.x;
     for (int l = 0; l < T.nlvl; ++l) {
         const SubLevel L = lvls[T.lvl0 + l];
-        for (int i = tid; i < L.nfa; i += 256) {          // front vectors f_P of the level's supernodes
+        for (int i = tid; i < L.nfa; i += BLOCK) {          // front vectors f_P of the level's supernodes
             const int it = items[L.fa0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
             const int c = it & 0xffff;
@@ -210,7 +338,7 @@ __global__ __launch_bounds__(256) void k_fwd_sub(const SubTree* __restrict__ tre
             sub_front_row(nd, c, ell, B, U, f[0], f[1], f[2]);
         }
         __syncthreads();
-        for (int i = tid; i < L.nfr; i += 256) {          // rows of G . f_P
+        for (int i = tid; i < L.nfr; i += BLOCK) {          // rows of G . f_P
             const int it = items[L.fr0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
             const int r = it & 0xffff, p = nd.p, R = p + nd.nb;
@@ -238,7 +366,8 @@ __global__ __launch_bounds__(256) void k_fwd_sub(const SubTree* __restrict__ tre
 }
 
 // backward sweep of a whole bottom subtree (one workgroup), its levels top-down
-__global__ __launch_bounds__(256) void k_bwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
                                                  const SubNode* __restrict__ nodes, const int* __restrict__ items,
                                                  const double* __restrict__ Gr, const int* __restrict__ bnd,
                                                  const double* __restrict__ Y, double* __restrict__ X,
@@ -249,7 +378,7 @@ __global__ __launch_bounds__(256) void k_bwd_sub(const SubTree* __restrict__ tre
     const int tid = threadIdx.x;
     for (int l = T.nlvl - 1; l >= 0; --l) {
         const SubLevel L = lvls[T.lvl0 + l];
-        for (int i = tid; i < L.nbv; i += 256) {          // [y_P ; -x_B] of the level's supernodes
+        for (int i = tid; i < L.nbv; i += BLOCK) {          // [y_P ; -x_B] of the level's supernodes
             const int it = items[L.bv0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
             const int r = it & 0xffff;
@@ -260,7 +389,7 @@ __global__ __launch_bounds__(256) void k_bwd_sub(const SubTree* __restrict__ tre
             v[0] = sg * src[o]; v[1] = sg * src[o + 1]; v[2] = sg * src[o + 2];
         }
         __syncthreads();
-        for (int i = tid; i < L.nbc; i += 256) {          // columns of G^T . v
+        for (int i = tid; i < L.nbc; i += BLOCK) {          // columns of G^T . v
             const int it = items[L.bc0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
             const int j = it & 0xffff, p = nd.p, R = p + nd.nb;
@@ -384,6 +513,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     for (int sn = 0; sn < nn_; ++sn) if (F.parent[sn] >= 0 && inc[sn]) kids[F.parent[sn]].push_back(sn);
     const char* ms = std::getenv("AA_SOLVE_MIN_SUBTREES");
     const bool stats = std::getenv("AA_SOLVE_STATS") != nullptr;
+    const char* sb = std::getenv("AA_SUB_BLOCK");
+    sub_block_ = sb ? std::atoi(sb) : 1024;
     const int min_sub = ms ? std::atoi(ms) : 96;
     constexpr int kSubLds = 64 * 1024, kMaxItemRow = 0xffff;
     auto roots_at = [&](int H) {
@@ -495,6 +626,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     std::vector<std::vector<int>> hl(F.max_height + 1);
     for (int sn = 0; sn < nn_; ++sn) if (!fused[sn] && inc[sn]) hl[F.height[sn]].push_back(sn);
     std::vector<Task> tasks;
+    std::vector<BTile> btiles;
+    std::vector<BRed> breds;
+    std::vector<FTile> ftiles;
+    std::vector<FRed> freds;
+    long long poff = 0;
     auto mk = [&](int sn, int r0, int nr, int mode) {
         Task t{};
         t.node = sn; t.r0 = r0; t.nr = nr; t.mode = mode;
@@ -513,11 +649,13 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         bool fwave = false, bwave = false;
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
-            if (p[sn] <= kWaveP) fr = std::max(fr, R); else fwave = true;
-            if (R <= kWaveR) br = std::max(br, p[sn]); else bwave = true;
+            if (p[sn] <= kWaveP) fr = std::max(fr, R);
+            if (R <= kWaveR) br = std::max(br, p[sn]);
         }
-        L.fblock = (fwave || fr > 128) ? 256 : (fr > 64 ? 128 : 64);
-        L.bblock = (bwave || br > 128) ? 256 : (br > 64 ? 128 : 64);
+        (void)fwave;
+        L.fblock = fr > 128 ? 256 : (fr > 64 ? 128 : 64);
+        (void)bwave;
+        L.bblock = br > 128 ? 256 : (br > 64 ? 128 : 64);
         L.asm_first = (int)tasks.size();
         for (int sn : l) {
             if (p[sn] <= kWaveP) continue;
@@ -532,24 +670,71 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             if (p[sn] <= kWaveP) {
                 for (int r0 = 0; r0 < R; r0 += L.fblock) tasks.push_back(mk(sn, r0, std::min(L.fblock, R - r0), 0));
                 L.lds_fwd = std::max(L.lds_fwd, 24 * p[sn]);
-            } else {
-                for (int r0 = 0; r0 < R; r0 += kWaveRowsPerTask) tasks.push_back(mk(sn, r0, std::min(kWaveRowsPerTask, R - r0), 1));
             }
         }
         L.fwd_count = (int)tasks.size() - L.fwd_first;
+        // large supernodes: split-K forward tiles (64 rows x kFwdTileCols columns; tiles entirely
+        // above the diagonal of L_PP^-1 are zero and skipped), one reduction task per row block
+        L.ft_first = (int)ftiles.size();
+        L.fr_first = (int)freds.size();
+        for (int sn : l) {
+            if (p[sn] <= kWaveP) continue;
+            const int R = p[sn] + nb[sn];
+            for (int r0 = 0; r0 < R; r0 += 64) {
+                FRed rd{};
+                rd.beg = beg[sn]; rd.p = p[sn]; rd.r0 = r0; rd.nr = std::min(64, R - r0);
+                rd.uoff = uoff[sn]; rd.foff = foff[sn]; rd.poff = poff;
+                for (int c0 = 0; c0 < p[sn]; c0 += kFwdTileCols) {
+                    if (r0 + 63 < c0) break;
+                    FTile ft{};
+                    ft.beg = beg[sn]; ft.p = p[sn]; ft.R = R; ft.c0 = c0; ft.r0 = r0;
+                    ft.nc = std::min(kFwdTileCols, p[sn] - c0);
+                    ft.goff = goff[sn]; ft.foff = foff[sn]; ft.poff = poff;
+                    poff += 3 * 64;
+                    ftiles.push_back(ft);
+                    ++rd.nt;
+                }
+                freds.push_back(rd);
+            }
+        }
+        L.ft_count = (int)ftiles.size() - L.ft_first;
+        L.frd_count = (int)freds.size() - L.fr_first;
         L.bwd_first = (int)tasks.size();
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
             if (R <= kWaveR) {
                 for (int j0 = 0; j0 < p[sn]; j0 += L.bblock) tasks.push_back(mk(sn, j0, std::min(L.bblock, p[sn] - j0), 0));
                 L.lds_bwd = std::max(L.lds_bwd, 24 * R);
-            } else {
-                for (int j0 = 0; j0 < p[sn]; j0 += kWaveRowsPerTask) tasks.push_back(mk(sn, j0, std::min(kWaveRowsPerTask, p[sn] - j0), 1));
             }
         }
         L.bwd_count = (int)tasks.size() - L.bwd_first;
+        // large supernodes: split-K tiles (64 columns x kBwdTileRows rows; the tiles above the
+        // diagonal of L_PP^-1 are all zero and skipped) and one reduction task per column block
+        L.bt_first = (int)btiles.size();
+        L.br_first = (int)breds.size();
+        for (int sn : l) {
+            const int R = p[sn] + nb[sn];
+            if (R <= kWaveR) continue;
+            for (int c0 = 0; c0 < p[sn]; c0 += 64) {
+                BRed rd{};
+                rd.beg = beg[sn]; rd.c0 = c0; rd.nc = std::min(64, p[sn] - c0); rd.poff = poff;
+                for (int r0 = c0; r0 < R; r0 += kBwdTileRows) {
+                    BTile bt{};
+                    bt.beg = beg[sn]; bt.p = p[sn]; bt.nb = nb[sn]; bt.bnd_off = bnd_off[sn];
+                    bt.c0 = c0; bt.r0 = r0; bt.nr = std::min(kBwdTileRows, R - r0);
+                    bt.goff = goff[sn]; bt.poff = poff;
+                    poff += 3 * 64;
+                    btiles.push_back(bt);
+                    ++rd.nt;
+                }
+                breds.push_back(rd);
+            }
+        }
+        L.bt_count = (int)btiles.size() - L.bt_first;
+        L.br_count = (int)breds.size() - L.br_first;
         max_lds = std::max(max_lds, std::max(L.lds_fwd, L.lds_bwd));
-        kernels_ += 2 + (L.asm_count ? 1 : 0);
+        kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.asm_count ? 1 : 0) + (L.bt_count ? 2 : 0) +
+                    (L.ft_count ? 2 : 0);
         levels_.push_back(L);
         if (stats) {
             double by = 0;
@@ -560,8 +745,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 nw += p[sn] > kWaveP;
             }
             std::fprintf(stderr, "[solve] level %zu: %zu supernodes (%d wave), max p %d, max nb %d, %.2f MB/sweep, "
-                         "fwd tasks %d (blk %d) bwd tasks %d (blk %d)\n", levels_.size() - 1, l.size(), nw, maxp, maxnb,
-                         by / 1e6, L.fwd_count, L.fblock, L.bwd_count, L.bblock);
+                         "fwd tasks %d (blk %d) bwd tasks %d (blk %d) bwd tiles %d\n", levels_.size() - 1, l.size(), nw, maxp,
+                         maxnb, by / 1e6, L.fwd_count, L.fblock, L.bwd_count, L.bblock, L.bt_count);
         }
     }
     if (n_sub_) kernels_ += 2;
@@ -569,6 +754,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     ell_.upload(ell, s);
     Gr_.upload(Gr, s); Gc_.upload(Gc, s);
     tasks_.upload(tasks, s);
+    btiles_.upload(btiles, s);
+    ftiles_.upload(ftiles, s);
+    freds_.upload(freds, s);
+    breds_.upload(breds, s);
+    bpart_.alloc(std::max<long long>(poff, 3));
     Y_.alloc(3 * (size_t)n_);
     U_.alloc(std::max<long long>(uo, 3));
     Fg_.alloc(std::max<long long>(fo, 3));
@@ -585,14 +775,21 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
 
 void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
     const Task* T = tasks_.p;
-    if (n_sub_)
-        hipLaunchKernelGGL(k_fwd_sub, dim3(n_sub_), dim3(256), sub_lds_f_, s, sub_trees_.p, sub_levels_.p, sub_nodes_.p,
-                           sub_items_.p, Gc_.p, ell_.p, b, Y_.p, U_.p, ctrl, gate_reject);
+#define SUBF(BL) hipLaunchKernelGGL(k_fwd_sub<BL>, dim3(n_sub_), dim3(BL), sub_lds_f_, s, sub_trees_.p, sub_levels_.p, \
+                                    sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b, Y_.p, U_.p, ctrl, gate_reject)
+    if (n_sub_) switch (sub_block_) { case 1024: SUBF(1024); break; case 512: SUBF(512); break; default: SUBF(256); break; }
+#undef SUBF
     for (auto& L : levels_) {
         if (L.asm_count)
             hipLaunchKernelGGL(k_asm, dim3(L.asm_count), dim3(256), 0, s, T, L.asm_first, ell_.p, b, U_.p, Fg_.p, ctrl, gate_reject);
 #define FWD(BL) hipLaunchKernelGGL(k_fwd<BL>, dim3(L.fwd_count), dim3(BL), L.lds_fwd, s, T, L.fwd_first, Gr_.p, Gc_.p, ell_.p, b, Y_.p, U_.p, Fg_.p, ctrl, gate_reject)
-        switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
+        if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
+        if (L.ft_count) {
+            hipLaunchKernelGGL(k_fwd_tile, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, Fg_.p, bpart_.p,
+                               ctrl, gate_reject);
+            hipLaunchKernelGGL(k_fwd_red, dim3(L.frd_count), dim3(64), 0, s, freds_.p, L.fr_first, bpart_.p, Fg_.p, Y_.p,
+                               U_.p, ctrl, gate_reject);
+        }
 #undef FWD
     }
     // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
@@ -604,12 +801,18 @@ void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject
     for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
         const Level& L = *it;
 #define BWD(BL) hipLaunchKernelGGL(k_bwd<BL>, dim3(L.bwd_count), dim3(BL), L.lds_bwd, s, T, L.bwd_first, Gr_.p, Gc_.p, bnd_.p, Y_.p, x, ctrl, gate_reject)
-        switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
+        if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
+        if (L.bt_count) {
+            hipLaunchKernelGGL(k_bwd_tile, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p, x,
+                               bpart_.p, ctrl, gate_reject);
+            hipLaunchKernelGGL(k_bwd_red, dim3(L.br_count), dim3(64), 0, s, breds_.p, L.br_first, bpart_.p, x, ctrl, gate_reject);
+        }
     }
-    if (n_sub_)
-        hipLaunchKernelGGL(k_bwd_sub, dim3(n_sub_), dim3(256), sub_lds_b_, s, sub_trees_.p, sub_levels_.p, sub_nodes_.p,
-                           sub_items_.p, Gr_.p, bnd_.p, Y_.p, x, ctrl, gate_reject);
+#define SUBB(BL) hipLaunchKernelGGL(k_bwd_sub<BL>, dim3(n_sub_), dim3(BL), sub_lds_b_, s, sub_trees_.p, sub_levels_.p, \
+                                    sub_nodes_.p, sub_items_.p, Gr_.p, bnd_.p, Y_.p, x, ctrl, gate_reject)
+    if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }
+#undef SUBB
     AA_CHECK_LAUNCH();
 }
 

@@ -63,11 +63,21 @@ public:
     };
     struct SubLevel { int n0, fa0, nfa, fr0, nfr, bv0, nbv, bc0, nbc, pad; };   // item ranges
     struct SubTree { int lvl0, nlvl; };
+    // split-K backward of large supernodes: a tile (64 columns from c0, nr rows from r0) and the
+    // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
+    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, pad; long long goff, poff; };
+    struct BRed { int beg, c0, nc, nt; long long poff; };
+    // split-K forward of large supernodes: tile (64 rows from r0, nc columns from c0) and the
+    // per-row-block reduction of its nt partials
+    struct FTile { int beg, p, R, c0, r0, nc, pad0, pad1; long long goff, foff, poff; };
+    struct FRed { int beg, p, r0, nr, nt, pad; long long uoff, foff, poff; };
 
 private:
     struct Level {
         int fwd_first = 0, fwd_count = 0, bwd_first = 0, bwd_count = 0;
         int asm_first = 0, asm_count = 0;     // assembly tasks of the wave-mode supernodes
+        int bt_first = 0, bt_count = 0, br_first = 0, br_count = 0;   // split-K backward tiles
+        int ft_first = 0, ft_count = 0, fr_first = 0, frd_count = 0;  // split-K forward tiles
         int fblock = 256, bblock = 256, lds_fwd = 0, lds_bwd = 0;
     };
     int n_ = 0, nn_ = 0, kernels_ = 0, top_beg_ = 0;
@@ -78,9 +88,14 @@ private:
     DevBuf<long long> ell_;   // per front row, ell_w pull offsets into U (-1 = none)
     DevBuf<double> Gr_, Gc_, Y_, U_, Fg_;
     DevBuf<Task> tasks_;
+    DevBuf<BTile> btiles_;
+    DevBuf<BRed> breds_;
+    DevBuf<FTile> ftiles_;
+    DevBuf<FRed> freds_;
+    DevBuf<double> bpart_;
     std::vector<Level> levels_;
     // fused bottom subtrees
-    int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1;
+    int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1, sub_block_ = 256;
     DevBuf<SubNode> sub_nodes_;
     DevBuf<SubLevel> sub_levels_;
     DevBuf<SubTree> sub_trees_;
