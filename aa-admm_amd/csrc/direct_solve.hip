@@ -366,9 +366,21 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
 }
 
 // backward sweep of a whole bottom subtree (one workgroup), its levels top-down
+// The column products are split over row segments of kSubSegRows rows (items (node, segment,
+// column), consecutive threads on consecutive columns of one row -> coalesced), partials in
+// LDS, then one item per column sums its segments in order: short loops instead of one thread
+// walking all R rows of a column.
+constexpr int kSubSegRows = 64;
+__device__ __forceinline__ int sub_seg_off(int seg, int p) {   // partial slots before segment seg
+    int o = 0;
+    for (int q = 0; q < seg; ++q) o += min(p, (q + 1) * kSubSegRows);
+    return o;
+}
+
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
                                                  const SubNode* __restrict__ nodes, const int* __restrict__ items,
+                                                 const long long* __restrict__ items2,
                                                  const double* __restrict__ Gr, const int* __restrict__ bnd,
                                                  const double* __restrict__ Y, double* __restrict__ X,
                                                  const Ctrl* ctrl, int gate_reject) {
@@ -389,17 +401,34 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             v[0] = sg * src[o]; v[1] = sg * src[o + 1]; v[2] = sg * src[o + 2];
         }
         __syncthreads();
-        for (int i = tid; i < L.nbc; i += BLOCK) {          // columns of G^T . v
+        for (int i = tid; i < L.nbs; i += BLOCK) {          // segment partials of G^T . v
+            const long long it = items2[L.bs0 + i];
+            const SubNode nd = nodes[L.n0 + (int)(it >> 40)];
+            const int seg = (int)((it >> 20) & 0xfffff), j = (int)(it & 0xfffff), p = nd.p, R = p + nd.nb;
+            const double* v = lds + nd.lds;
+            const double* G = Gr + nd.goff + j;
+            const int r1 = min(R, (seg + 1) * kSubSegRows);
+            double a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll 8
+            for (int r = max(j, seg * kSubSegRows); r < r1; ++r) {
+                const double g = G[(size_t)r * p];
+                a0 += g * v[3 * r]; a1 += g * v[3 * r + 1]; a2 += g * v[3 * r + 2];
+            }
+            double* q = lds + nd.slot + 3 * (sub_seg_off(seg, p) + j);
+            q[0] = a0; q[1] = a1; q[2] = a2;
+        }
+        __syncthreads();
+        for (int i = tid; i < L.nbc; i += BLOCK) {          // columns: sum of their segments
             const int it = items[L.bc0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
             const int j = it & 0xffff, p = nd.p, R = p + nd.nb;
-            const double* v = lds + nd.lds;
-            const double* G = Gr + nd.goff + j;
+            const int nseg = (R + kSubSegRows - 1) / kSubSegRows, s0 = j / kSubSegRows;
+            int off = sub_seg_off(s0, p);
             double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 8
-            for (int r = j; r < R; ++r) {
-                const double g = G[(size_t)r * p];
-                a0 += g * v[3 * r]; a1 += g * v[3 * r + 1]; a2 += g * v[3 * r + 2];
+            for (int seg = s0; seg < nseg; ++seg) {
+                const double* q = lds + nd.slot + 3 * (off + j);
+                a0 += q[0]; a1 += q[1]; a2 += q[2];
+                off += min(p, (seg + 1) * kSubSegRows);
             }
             const size_t o = 3 * (size_t)(nd.beg + j);
             X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
@@ -515,8 +544,9 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     const bool stats = std::getenv("AA_SOLVE_STATS") != nullptr;
     const char* sb = std::getenv("AA_SUB_BLOCK");
     sub_block_ = sb ? std::atoi(sb) : 1024;
-    const int min_sub = ms ? std::atoi(ms) : 96;
-    constexpr int kSubLds = 64 * 1024, kMaxItemRow = 0xffff;
+    const int min_sub = ms ? std::atoi(ms) : 256;
+    constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
+    static_assert(kSubSegRows == 64, "LDS accounting below assumes 64-row segments");
     auto roots_at = [&](int H) {
         std::vector<int> r;
         for (int sn = 0; sn < nn_; ++sn)
@@ -537,11 +567,14 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             std::vector<long long> lf(H + 1, 0), lb(H + 1, 0), nodes_at(H + 1, 0);
             for (int v : collect(rt)) {
                 lf[F.height[v]] += 24LL * p[v];
-                lb[F.height[v]] += 24LL * (p[v] + nb[v]);
+                long long slots = 0;
+                for (int sg = 0; sg < (p[v] + nb[v] + 63) / 64; ++sg) slots += std::min(p[v], (sg + 1) * 64);
+                lb[F.height[v]] += 24LL * (p[v] + nb[v]) + 24LL * slots;
                 nodes_at[F.height[v]] += 1;
                 if (p[v] + nb[v] > kMaxItemRow) ok = false;
             }
-            for (int h = 0; h <= H; ++h) if (lf[h] > kSubLds || lb[h] > kSubLds || nodes_at[h] > kMaxItemRow) ok = false;
+            for (int h = 0; h <= H; ++h)
+                if (lf[h] > kSubLds || lb[h] > kSubLdsB || nodes_at[h] > kMaxItemRow) ok = false;
             if (!ok) break;
         }
         if (ok) { cut_height_ = H; break; }
@@ -552,6 +585,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         std::vector<SubLevel> slevels;
         std::vector<SubTree> strees;
         std::vector<int> items;
+        std::vector<long long> items2;
         sub_lds_f_ = sub_lds_b_ = 0;
         if (cut_height_ >= 0) {
             for (int rt : roots_at(cut_height_)) {
@@ -597,6 +631,20 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     for (size_t k = 0; k < lv.size(); ++k)
                         for (int r = 0; r < p[lv[k]] + nb[lv[k]]; ++r) items.push_back(((int)(k + (n1 - L.n0)) << 16) | r);
                     L.nbv = (int)items.size() - L.bv0;
+                    // segment partial slots after the level's vectors; items (node, segment, column)
+                    L.bs0 = (int)items2.size();
+                    for (size_t k = 0; k < lv.size(); ++k) {
+                        SubNode& nd = snodes[n1 + k];
+                        nd.slot = lb / 8;
+                        const int pp = p[lv[k]], RR = pp + nb[lv[k]];
+                        for (int sg = 0; sg * kSubSegRows < RR; ++sg) {
+                            const int nc = std::min(pp, (sg + 1) * kSubSegRows);
+                            for (int j = 0; j < nc; ++j)
+                                items2.push_back(((long long)(k + (n1 - L.n0)) << 40) | ((long long)sg << 20) | j);
+                            lb += 24 * nc;
+                        }
+                    }
+                    L.nbs = (int)items2.size() - L.bs0;
                     L.bc0 = (int)items.size();
                     for (size_t k = 0; k < lv.size(); ++k)
                         for (int j = 0; j < p[lv[k]]; ++j) items.push_back(((int)(k + (n1 - L.n0)) << 16) | j);
@@ -621,6 +669,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         sub_levels_.upload(slevels, s);
         sub_trees_.upload(strees, s);
         sub_items_.upload(items, s);
+        sub_items2_.upload(items2, s);
     }
     // levels by height and their row tasks
     std::vector<std::vector<int>> hl(F.max_height + 1);
@@ -762,6 +811,10 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     Y_.alloc(3 * (size_t)n_);
     U_.alloc(std::max<long long>(uo, 3));
     Fg_.alloc(std::max<long long>(fo, 3));
+    if (std::max(sub_lds_f_, sub_lds_b_) > 64 * 1024)
+        for (const void* k : {(const void*)k_fwd_sub<256>, (const void*)k_fwd_sub<512>, (const void*)k_fwd_sub<1024>,
+                              (const void*)k_bwd_sub<256>, (const void*)k_bwd_sub<512>, (const void*)k_bwd_sub<1024>})
+            AA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (max_lds > 64 * 1024) {   // large fronts: opt in to more than the default 64 KiB of LDS
         for (const void* k : {(const void*)k_fwd<64>, (const void*)k_fwd<128>, (const void*)k_fwd<256>,
                               (const void*)k_bwd<64>, (const void*)k_bwd<128>, (const void*)k_bwd<256>})
@@ -810,7 +863,7 @@ void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject
         }
     }
 #define SUBB(BL) hipLaunchKernelGGL(k_bwd_sub<BL>, dim3(n_sub_), dim3(BL), sub_lds_b_, s, sub_trees_.p, sub_levels_.p, \
-                                    sub_nodes_.p, sub_items_.p, Gr_.p, bnd_.p, Y_.p, x, ctrl, gate_reject)
+                                    sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x, ctrl, gate_reject)
     if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }
 #undef SUBB
     AA_CHECK_LAUNCH();

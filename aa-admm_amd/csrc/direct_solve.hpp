@@ -57,11 +57,11 @@ public:
 
     // Bottom subtrees (all supernodes up to a cut height) are solved whole by one workgroup
     // each: their levels are separated by workgroup barriers instead of kernel boundaries.
-    struct SubNode {   // a supernode inside a fused subtree; lds = its vector's offset in LDS
-        int p, nb, beg, bnd_off, ell_w, lds, pad0, pad1;
+    struct SubNode {   // a supernode inside a fused subtree; lds = its vector's offset in LDS,
+        int p, nb, beg, bnd_off, ell_w, lds, slot, pad1;   // slot = its backward segment partials
         long long goff, uoff, ell_off;
     };
-    struct SubLevel { int n0, fa0, nfa, fr0, nfr, bv0, nbv, bc0, nbc, pad; };   // item ranges
+    struct SubLevel { int n0, fa0, nfa, fr0, nfr, bv0, nbv, bc0, nbc, bs0, nbs, pad; };   // item ranges
     struct SubTree { int lvl0, nlvl; };
     // split-K backward of large supernodes: a tile (64 columns from c0, nr rows from r0) and the
     // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
@@ -100,6 +100,7 @@ private:
     DevBuf<SubLevel> sub_levels_;
     DevBuf<SubTree> sub_trees_;
     DevBuf<int> sub_items_;   // (local node << 16 | row) per item
+    DevBuf<long long> sub_items2_;   // backward segment items (local node << 40 | segment << 20 | column)
 };
 
 }  // namespace aa
