@@ -89,9 +89,14 @@ __device__ __forceinline__ double d9(const double* a, const double* b) {
 }
 
 // x: in = v (start point), out = prox. Returns iterations; sets *fail on a collapsed line search.
+// The history is a shift register (slot 0 = newest) instead of mcloptlib's ring buffer: every
+// index is a compile-time constant, so s, y stay in registers (the ring buffer's dynamic
+// indices put 864 B per thread in scratch). The two-loop recursion visits the pairs in the
+// same order (newest -> oldest, then back), so the arithmetic is the reference's.
 __device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, double k, double vol, const double* v,
                                           double* x, int* fail) {
-    double s[6][9], y[6][9], ys_h[6], alpha[6], g[9], gp[9], xp[9], drt[9];
+    constexpr int M = 6;
+    double s[M][9], y[M][9], ys_h[M], alpha[M], g[9], gp[9], xp[9], drt[9];
     double fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
     double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
     double fpast = fx;
@@ -99,7 +104,7 @@ __device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, dou
 #pragma unroll
     for (int i = 0; i < 9; ++i) drt[i] = -g[i];
     double step = 1.0 / sqrt(d9(drt, drt));
-    int k_it = 1, end = 0;
+    int k_it = 1;
     for (;;) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) { xp[i] = x[i]; gp[i] = g[i]; }
@@ -120,32 +125,41 @@ __device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, dou
         if (fabs(fpast - fx) < 1e-16) return k_it;
         fpast = fx;
         if (k_it >= 100) return k_it;
+        // push (s, y) into slot 0
+#pragma unroll
+        for (int q = M - 1; q > 0; --q) {
+            ys_h[q] = ys_h[q - 1];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) { s[q][i] = s[q - 1][i]; y[q][i] = y[q - 1][i]; }
+        }
         double ys = 0, yy = 0;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
             const double si = x[i] - xp[i], yi = g[i] - gp[i];
-            s[end][i] = si; y[end][i] = yi;
+            s[0][i] = si; y[0][i] = yi;
             ys += yi * si; yy += yi * yi;
         }
-        ys_h[end] = ys;
+        ys_h[0] = ys;
 #pragma unroll
         for (int i = 0; i < 9; ++i) drt[i] = -g[i];
-        const int bound = k_it < 6 ? k_it : 6;
-        end = (end + 1) % 6;
-        int j = end;
-        for (int i = 0; i < bound; ++i) {
-            j = (j + 5) % 6;
-            alpha[j] = d9(s[j], drt) / ys_h[j];
+        const int bound = k_it < M ? k_it : M;
 #pragma unroll
-            for (int t = 0; t < 9; ++t) drt[t] -= alpha[j] * y[j][t];
+        for (int q = 0; q < M; ++q) {
+            if (q < bound) {
+                alpha[q] = d9(s[q], drt) / ys_h[q];
+#pragma unroll
+                for (int t = 0; t < 9; ++t) drt[t] -= alpha[q] * y[q][t];
+            }
         }
 #pragma unroll
         for (int t = 0; t < 9; ++t) drt[t] *= ys / yy;
-        for (int i = 0; i < bound; ++i) {
-            const double beta = d9(y[j], drt) / ys_h[j];
 #pragma unroll
-            for (int t = 0; t < 9; ++t) drt[t] += (alpha[j] - beta) * s[j][t];
-            j = (j + 1) % 6;
+        for (int q = M - 1; q >= 0; --q) {
+            if (q < bound) {
+                const double beta = d9(y[q], drt) / ys_h[q];
+#pragma unroll
+                for (int t = 0; t < 9; ++t) drt[t] += (alpha[q] - beta) * s[q][t];
+            }
         }
         step = 1.0;
         ++k_it;
