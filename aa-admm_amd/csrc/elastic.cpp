@@ -312,7 +312,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     groups_.resize(dgroups.size());
     long long zoff = 0, yrow = 0;
     red_blocks_ = 0;
-    std::vector<std::vector<std::pair<long long, double>>> dtr(nf_);
+    std::vector<std::vector<long long>> dtr(nf_);   // per free node: its vertex slots
     for (size_t gi = 0; gi < dgroups.size(); ++gi) {
         auto& hg = dgroups[gi];
         auto& dg = groups_[gi];
@@ -327,8 +327,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
             for (int a = 0; a < hg.nv; ++a) {
                 const int q = node2int_[hg.idx[(size_t)t * hg.nv + a]];
                 if (q >= nf_) continue;
-                for (int c = 0; c < hg.ncol; ++c)
-                    dtr[q].push_back({yrow + (long long)t * hg.ncol + c, hg.G[((size_t)t * hg.ncol + c) * hg.nv + a]});
+                dtr[q].push_back(yrow + (long long)t * hg.nv + a);
             }
         }
         dg.idx.upload(idx, s());
@@ -342,21 +341,22 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
         d.mu = hg.lame.mu; d.lambda = hg.lame.lambda; d.k = hg.lame.lambda + (2.0 / 3.0) * hg.lame.mu;
         d.lmin = hg.lame.limit_min; d.lmax = hg.lame.limit_max;
         zoff += (long long)d.dim * cnt;
-        yrow += (long long)d.ncol * cnt;
+        yrow += (long long)d.nv * cnt;
         red_blocks_ += blocks_for(cnt);
     }
     Z_ = zoff;
+    Yslots_ = yrow;
     if (P == 1) { nbg_ = red_blocks_; zmax = Z_; }
     {
         std::vector<int> ptr(nf_ + 1, 0), row;
-        std::vector<double> val;
         for (int q = 0; q < nf_; ++q) {
             auto& r = dtr[q];
             std::sort(r.begin(), r.end());
-            for (auto& e : r) { row.push_back((int)e.first); val.push_back(e.second); }
+            if (!r.empty() && r.back() > 0x7fffffffLL) throw Error(ERR_ARG, "initialize: too many element vertices");
+            for (long long e : r) row.push_back((int)e);
             ptr[q + 1] = (int)row.size();
         }
-        dt_ptr_.upload(ptr, s()); dt_row_.upload(row, s()); dt_val_.upload(val, s());
+        dt_ptr_.upload(ptr, s()); dt_row_.upload(row, s());
     }
     // ---- state and work buffers
     std::vector<double> xs(3 * (size_t)n), ms(n);
@@ -370,7 +370,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     xfull_.alloc(3 * (size_t)n); xlast_.alloc(3 * (size_t)n); cxfull_.alloc(3 * (size_t)n);
     xfull_.zero(s()); xlast_.zero(s()); cxfull_.zero(s());
     xbar_.alloc(3 * (size_t)nf_); Mxbar_.alloc(3 * (size_t)nf_); b_.alloc(3 * (size_t)nf_); dx_.alloc(3 * (size_t)nf_);
-    z_.alloc(Z_); u_.alloc(Z_); y_.alloc(Z_); du_.alloc(Z_);
+    z_.alloc(Z_); u_.alloc(Z_); y_.alloc(3 * std::max<long long>(1, Yslots_)); du_.alloc(Z_);
     if (st_.variant == AA_VARIANT_Z) { dz_.alloc(Z_); lastz_.alloc(Z_); cz_.alloc(Z_); }
     // residual block partials [a | b], padded to the largest rank's block count (zeros beyond
     // this rank's blocks), and their all-rank sums (the same buffer on one GPU)
@@ -411,19 +411,19 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     double lz = 0, rs = 0;
     for (auto& g : groups_) {
         const double per = 4.0 * g.d.nv + 8.0 * g.d.ncol * g.d.nv + 8.0;
-        lz += g.d.count * (per + 3 * 8.0 * g.d.dim);
+        lz += g.d.count * (per + 2 * 8.0 * g.d.dim + 24.0 * g.d.nv);   // u in, z out, vertex slots out
         rs += g.d.count * (per + 3 * 8.0 * g.d.dim);
     }
     kstats_["local_z"].bytes = lz + 24.0 * n;
     kstats_["resid"].bytes = rs + 48.0 * n;
     kstats_["solve"].bytes = solver_.bytes_per_solve();
-    kstats_["rhs"].bytes = 12.0 * (double)dt_row_.n + 8.0 * Z_ + 48.0 * nf_;
-    // Z variant: u = W^-1 grad E(z) and y rows (reads idx, G, w, z; writes u, y), prim (reads
-    // idx, G, w, z, u; writes block partials)
+    kstats_["rhs"].bytes = 28.0 * (double)dt_row_.n + 48.0 * nf_;   // slot index + 3 doubles per slot; Mxbar, b
+    // Z variant: u = W^-1 grad E(z) and the vertex slots (reads idx, G, w, z; writes u, slots),
+    // prim (reads idx, G, w, z, u; writes block partials)
     double gy = 0, pr = 0;
     for (auto& g : groups_) {
         const double per = 4.0 * g.d.nv + 8.0 * g.d.ncol * g.d.nv + 8.0;
-        gy += g.d.count * (per + 8.0 * 3 * g.d.dim);
+        gy += g.d.count * (per + 8.0 * 2 * g.d.dim + 24.0 * g.d.nv);
         pr += g.d.count * (per + 8.0 * 2 * g.d.dim);
     }
     kstats_["grad"].bytes = gy + 24.0 * n;
@@ -518,7 +518,7 @@ void ElasticSolver::prologue() {
     const long long nx = 3LL * nf_;
     if (st_.variant == AA_VARIANT_UX) {
         local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_INIT, false);
-        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
+        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
         solver_.solve(b_.p, xfull_.p, nullptr, 0, s());
         {
             int off = 0;
@@ -535,7 +535,7 @@ void ElasticSolver::prologue() {
         }
     } else {
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 2, 0, ctrl_.p, s());
-        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
+        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
         solver_.solve(b_.p, xfull_.p, nullptr, 0, s());
         local_z_all(xfull_.p, u_.p, z_.p, nullptr, LZ_INIT, false);
         launch_copy(dz_.p, z_.p, Z_, nullptr, 0, s());
@@ -558,7 +558,7 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
         reduce_partials();
     }
     ev_begin("rhs");
-    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s(), xfull_.p, xlast_.p,
+    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s(), xfull_.p, xlast_.p,
                ga_, nbg_);
     ev_end("rhs");
     ev_begin("solve");
@@ -598,7 +598,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
     for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, accel ? 1 : 0, 0, c, s());
     ev_end("grad");
     ev_begin("rhs");
-    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
     ev_end("rhs");
     ev_begin("solve");
     solver_.solve(b_.p, xfull_.p, c, 0, s());
@@ -621,7 +621,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         launch_copy(z_.p, dz_.p, Z_, c, 1, s());
         launch_copy(aa_cur_.p, dz_.p, Z_, c, 1, s());   // accelerator.replace(curr_z)
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 0, 1, c, s());
-        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());
+        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());
         solver_.solve(b_.p, xfull_.p, c, 1, s());
         prim_all(xfull_.p, z_.p, nullptr, 1);
         reduce_partials();
@@ -646,7 +646,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
         ev_begin("comb");
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, dz_.p, u_.p, y_.p, nf_, 2, 0, c, s());
-        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, dt_val_.p, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
         solver_.solve(b_.p, cxfull_.p, c, 0, s());
         local_z_all(cxfull_.p, u_.p, cz_.p, nullptr, LZ_NORMAL, false);
         prim_all(cxfull_.p, cz_.p, dz_.p, 0);

@@ -73,7 +73,7 @@ private:
 
     // internal numbering: free nodes in nested-dissection order, then pinned (sorted)
     int n_ = 0, nf_ = 0, np_ = 0;
-    long long Z_ = 0;
+    long long Z_ = 0, Yslots_ = 0;
     std::vector<int> node2int_, int2node_;
     double pdt2_ = 0;
 
@@ -81,7 +81,6 @@ private:
     std::vector<DevGroup> groups_;
     DirectSolver solver_;
     DevBuf<int> dt_ptr_, dt_row_;
-    DevBuf<double> dt_val_;
     DevBuf<double> xs_, vs_, mass_, xfull_, xlast_, xbar_, Mxbar_, b_, cxfull_;
     DevBuf<double> z_, u_, y_, du_, dz_, dx_, lastz_, cz_;
     DevBuf<double> aa_cur_, aa_dF_, aa_dG_, aa_red_, aa_red_g_;

@@ -89,6 +89,31 @@ __device__ __forceinline__ void gather_P(const GroupDev& g, int e, const double*
     }
 }
 
+// Per-vertex right-hand-side contributions of one element: with y_c = w (w z_c - w Cp_c - u_c)
+// (the element's rows of W z + C - u, Solver.cpp:105/175), vertex a of a free node receives
+// f_a = sum_c G[c][a] y_c, written to slot (yrow + e*NV + a); the rhs kernel then only sums
+// the slots of each node (no coefficient array, no per-column gathers).
+template <int NV>
+__device__ __forceinline__ void write_slots(const GroupDev& g, int e, int nf, double w, const double* zz,
+                                            const double* Cp, const double* uu, double* __restrict__ y) {
+    constexpr int NC = NV - 1;
+    double yc[3 * NC];
+#pragma unroll
+    for (int i = 0; i < 3 * NC; ++i) yc[i] = w * (w * zz[i] - w * Cp[i] - uu[i]);
+#pragma unroll
+    for (int a = 0; a < NV; ++a) {
+        if (g.idx[(size_t)a * g.count + e] >= nf) continue;   // pinned: no rhs row
+        double f0 = 0, f1 = 0, f2 = 0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
+            f0 += gc * yc[3 * c]; f1 += gc * yc[3 * c + 1]; f2 += gc * yc[3 * c + 2];
+        }
+        double* o = y + 3 * (size_t)(g.yrow + (long long)e * NV + a);
+        o[0] = f0; o[1] = f1; o[2] = f2;
+    }
+}
+
 // ------------------------------------------------------------------ local step
 template <int NV, int HYPER>
 __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __restrict__ xfull,
@@ -126,13 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
             part += r * r;
             z[g.zoff + (size_t)i * g.count + e] = zz[i];
         }
-        if (y) {
-#pragma unroll
-            for (int c = 0; c < NC; ++c)
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    y[3 * (size_t)(g.yrow + (long long)e * NC + c) + j] = w * (w * zz[3 * c + j] - w * Cp[3 * c + j] - uu[3 * c + j]);
-        }
+        if (y) write_slots<NV>(g, e, nf, w, zz, Cp, uu, y);
     }
     if (red) {
         const double s = block_sum(part, sm);
@@ -212,11 +231,7 @@ __global__ __launch_bounds__(kBlock) void k_u_and_y(GroupDev g, const double* __
 #pragma unroll
         for (int i = 0; i < D; ++i) u[g.zoff + (size_t)i * g.count + e] = uu[i];
     }
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-            y[3 * (size_t)(g.yrow + (long long)e * NC + c) + j] = w * (w * zz[3 * c + j] - w * Cp[3 * c + j] - uu[3 * c + j]);
+    write_slots<NV>(g, e, nf, w, zz, Cp, uu, y);
 }
 
 template <int NV>
@@ -282,11 +297,19 @@ __global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ 
         xlast[3 * (size_t)i + 2] = xsrc[3 * (size_t)i + 2];
     }
     double s0 = 0, s1 = 0, s2 = 0;
+    if (val) {
 #pragma unroll 4
-    for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
-        const double v = val[k];
-        const size_t r = 3 * (size_t)row[k];
-        s0 += v * y[r]; s1 += v * y[r + 1]; s2 += v * y[r + 2];
+        for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
+            const double v = val[k];
+            const size_t r = 3 * (size_t)row[k];
+            s0 += v * y[r]; s1 += v * y[r + 1]; s2 += v * y[r + 2];
+        }
+    } else {   // vertex slots (write_slots): plain sums
+#pragma unroll 4
+        for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
+            const size_t r = 3 * (size_t)row[k];
+            s0 += y[r]; s1 += y[r + 1]; s2 += y[r + 2];
+        }
     }
     b[3 * (size_t)i + 0] = Mxbar[3 * (size_t)i + 0] + pdt2 * s0;
     b[3 * (size_t)i + 1] = Mxbar[3 * (size_t)i + 1] + pdt2 * s1;
@@ -843,7 +866,10 @@ void launch_finalize(int n, int nf, const double* xsrc, const double* xfull, dou
     AA_CHECK_LAUNCH();
 }
 
-int aa_reduce_blocks(long long dim) { return grid_for(dim) < 512 ? grid_for(dim) : 512; }
+int aa_reduce_blocks(long long dim) {   // more partials only pay off on large vectors (k_aa_solve sums them)
+    const int cap = dim > (4LL << 20) ? 2048 : 512;
+    return grid_for(dim) < cap ? grid_for(dim) : cap;
+}
 
 static int mm_bucket(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : 32); }
 

@@ -14,7 +14,7 @@ struct GroupDev {
     int count;           // elements
     int nv, ncol, dim;   // 4/3/9 for tets, 3/2/6 for tris
     long long zoff;      // z/u offset: component c of element e at zoff + c*count + e
-    long long yrow;      // first row of this group in the (Z/3) x 3 row array y
+    long long yrow;      // first vertex slot of this group in the slot array y (slot e*nv + a, 3 doubles)
     const int* idx;      // [nv][count] internal node ids
     const double* G;     // [(c*nv + a)][count]  F[:,c] = sum_a G[c][a] x_a
     const double* w;     // [count] ADMM weights sqrt(k*vol)
