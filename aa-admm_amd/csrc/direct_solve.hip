@@ -20,6 +20,26 @@ __device__ __forceinline__ bool solve_gated(const Ctrl* c, int gate_reject) {
 
 using Task = DirectSolver::Task;
 
+// Split-K hand-off inside one launch (MI355X_MICROARCH.md "Valid forms"; the publish recipe of
+// cdna_hip_programming.md Guideline 16): partials are stored write-through (sc1: relaxed
+// agent-scope 8-B atomic stores, so no release / L2 write-back), the storing wave drains
+// (s_waitcnt vmcnt(0)), then one lane adds to the block's counter; the workgroup whose add
+// returns nt-1 takes ONE agent acquire and reads the partials with plain (pipelined) loads.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// storing wave: drain its sc1 stores, then lane 0 adds; returns true (wave-uniform) in the
+// workgroup whose add completes the count
+__device__ __forceinline__ bool arrive_last(int* cnt, int nt, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __shfl(prev, 0, 64);
+    return (int)prev == nt - 1;
+}
+
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -176,8 +196,8 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
 
 // Backward sweep of the large supernodes (R > kWaveR) as a split-K GEMV: tile = 64 columns
 // (lanes) x kBwdTileRows rows (4 waves x 32 rows) of the row-major G, the tile's slice of
-// [y_P ; -x_B] staged in LDS, one 64 x 3 partial per tile; k_bwd_red sums the partials of each
-// column block in tile order (deterministic). Gives (columns/64) x (rows/128) workgroups per
+// [y_P ; -x_B] staged in LDS, one 64 x 3 partial per tile; the last tile of a column block to finish
+// sums the block's partials in tile order (deterministic; hand-off protocol above). Gives (columns/64) x (rows/128) workgroups per
 // supernode instead of one wave per column with a serial loop over all R rows.
 using BTile = DirectSolver::BTile;
 using BRed = DirectSolver::BRed;
@@ -185,7 +205,8 @@ constexpr int kBwdTileRows = 128;
 
 __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tiles, int first, const double* __restrict__ Gr,
                                                   const int* __restrict__ bnd, const double* __restrict__ Y,
-                                                  const double* __restrict__ X, double* __restrict__ part,
+                                                  double* __restrict__ X, double* __restrict__ part,
+                                                  const BRed* __restrict__ reds, int* __restrict__ cnt,
                                                   const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     __shared__ double v[3 * kBwdTileRows];
@@ -218,37 +239,38 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
     }
     if (w > 0) { red[w - 1][3 * lane] = a0; red[w - 1][3 * lane + 1] = a1; red[w - 1][3 * lane + 2] = a2; }
     __syncthreads();
-    if (w == 0) {
+    if (w != 0) return;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { a0 += red[k][3 * lane]; a1 += red[k][3 * lane + 1]; a2 += red[k][3 * lane + 2]; }
-        double* o = part + t.poff + 3 * lane;
-        o[0] = a0; o[1] = a1; o[2] = a2;
+    for (int k = 0; k < 3; ++k) { a0 += red[k][3 * lane]; a1 += red[k][3 * lane + 1]; a2 += red[k][3 * lane + 2]; }
+    double* o = part + t.poff + 3 * lane;
+    st_sc1(o, a0); st_sc1(o + 1, a1); st_sc1(o + 2, a2);
+    const BRed rd = reds[t.rid];
+    if (!arrive_last(cnt + t.rid, rd.nt, lane)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // last tile of the column block: sum its partials in tile order (deterministic)
+    if (lane < rd.nc) {
+        double b0 = 0, b1 = 0, b2 = 0;
+        const double* q = part + rd.poff + 3 * lane;
+#pragma unroll 8
+        for (int k = 0; k < rd.nt; ++k, q += 3 * 64) { b0 += q[0]; b1 += q[1]; b2 += q[2]; }
+        const size_t xo = 3 * (size_t)(rd.beg + rd.c0 + lane);
+        X[xo] = b0; X[xo + 1] = b1; X[xo + 2] = b2;
     }
-}
-
-__global__ __launch_bounds__(64) void k_bwd_red(const BRed* __restrict__ reds, int first, const double* __restrict__ part,
-                                                double* __restrict__ X, const Ctrl* ctrl, int gate_reject) {
-    if (solve_gated(ctrl, gate_reject)) return;
-    const BRed t = reds[first + blockIdx.x];
-    const int lane = threadIdx.x;
-    if (lane >= t.nc) return;
-    double a0 = 0, a1 = 0, a2 = 0;
-    const double* q = part + t.poff + 3 * lane;
-    for (int k = 0; k < t.nt; ++k, q += 3 * 64) { a0 += q[0]; a1 += q[1]; a2 += q[2]; }
-    const size_t o = 3 * (size_t)(t.beg + t.c0 + lane);
-    X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
+    if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Forward sweep of the large supernodes (p > kWaveP) as a split-K GEMV on the column-major G:
 // tile = 64 rows (lanes) x kFwdTileCols columns (4 waves x 32), the tile's slice of the
-// assembled front f_P staged in LDS, one 64 x 3 partial per tile; k_fwd_red sums a row block's
-// partials in tile order and writes y_P (rows < p) or the update vector u = f_B - M f_P.
+// assembled front f_P staged in LDS, one 64 x 3 partial per tile; the last tile of a row block to finish sums
+// its partials in tile order and writes y_P (rows < p) or the update vector u = f_B - M f_P.
 using FTile = DirectSolver::FTile;
 using FRed = DirectSolver::FRed;
 constexpr int kFwdTileCols = 128;
 
 __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tiles, int first, const double* __restrict__ Gc,
                                                   const double* __restrict__ Fg, double* __restrict__ part,
+                                                  const FRed* __restrict__ reds, int* __restrict__ cnt,
+                                                  double* __restrict__ Y, double* __restrict__ U,
                                                   const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     __shared__ double f[3 * kFwdTileCols];
@@ -272,33 +294,31 @@ __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tile
     }
     if (w > 0) { red[w - 1][3 * lane] = a0; red[w - 1][3 * lane + 1] = a1; red[w - 1][3 * lane + 2] = a2; }
     __syncthreads();
-    if (w == 0) {
+    if (w != 0) return;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { a0 += red[k][3 * lane]; a1 += red[k][3 * lane + 1]; a2 += red[k][3 * lane + 2]; }
-        double* o = part + t.poff + 3 * lane;
-        o[0] = a0; o[1] = a1; o[2] = a2;
+    for (int k = 0; k < 3; ++k) { a0 += red[k][3 * lane]; a1 += red[k][3 * lane + 1]; a2 += red[k][3 * lane + 2]; }
+    double* o = part + t.poff + 3 * lane;
+    st_sc1(o, a0); st_sc1(o + 1, a1); st_sc1(o + 2, a2);
+    const FRed rd = reds[t.rid];
+    if (!arrive_last(cnt + t.rid, rd.nt, lane)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // last tile of the row block: sum its partials in tile order (deterministic)
+    if (lane < rd.nr) {
+        double b0 = 0, b1 = 0, b2 = 0;
+        const double* q = part + rd.poff + 3 * lane;
+#pragma unroll 8
+        for (int k = 0; k < rd.nt; ++k, q += 3 * 64) { b0 += q[0]; b1 += q[1]; b2 += q[2]; }
+        const int rr = rd.r0 + lane;
+        if (rr < rd.p) {
+            const size_t yo = 3 * (size_t)(rd.beg + rr);
+            Y[yo] = b0; Y[yo + 1] = b1; Y[yo + 2] = b2;
+        } else {
+            const double* fb = Fg + rd.foff + 3 * (size_t)rr;
+            double* u = U + rd.uoff + 3 * (size_t)(rr - rd.p);
+            u[0] = fb[0] - b0; u[1] = fb[1] - b1; u[2] = fb[2] - b2;
+        }
     }
-}
-
-__global__ __launch_bounds__(64) void k_fwd_red(const FRed* __restrict__ reds, int first, const double* __restrict__ part,
-                                                const double* __restrict__ Fg, double* __restrict__ Y,
-                                                double* __restrict__ U, const Ctrl* ctrl, int gate_reject) {
-    if (solve_gated(ctrl, gate_reject)) return;
-    const FRed t = reds[first + blockIdx.x];
-    const int lane = threadIdx.x;
-    if (lane >= t.nr) return;
-    double a0 = 0, a1 = 0, a2 = 0;
-    const double* q = part + t.poff + 3 * lane;
-    for (int k = 0; k < t.nt; ++k, q += 3 * 64) { a0 += q[0]; a1 += q[1]; a2 += q[2]; }
-    const int r = t.r0 + lane;
-    if (r < t.p) {
-        const size_t o = 3 * (size_t)(t.beg + r);
-        Y[o] = a0; Y[o + 1] = a1; Y[o + 2] = a2;
-    } else {
-        const double* fb = Fg + t.foff + 3 * (size_t)r;
-        double* u = U + t.uoff + 3 * (size_t)(r - t.p);
-        u[0] = fb[0] - a0; u[1] = fb[1] - a1; u[2] = fb[2] - a2;
-    }
+    if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 using SubNode = DirectSolver::SubNode;
@@ -739,6 +759,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     ft.beg = beg[sn]; ft.p = p[sn]; ft.R = R; ft.c0 = c0; ft.r0 = r0;
                     ft.nc = std::min(kFwdTileCols, p[sn] - c0);
                     ft.goff = goff[sn]; ft.foff = foff[sn]; ft.poff = poff;
+                    ft.rid = (int)freds.size();
                     poff += 3 * 64;
                     ftiles.push_back(ft);
                     ++rd.nt;
@@ -772,6 +793,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     bt.beg = beg[sn]; bt.p = p[sn]; bt.nb = nb[sn]; bt.bnd_off = bnd_off[sn];
                     bt.c0 = c0; bt.r0 = r0; bt.nr = std::min(kBwdTileRows, R - r0);
                     bt.goff = goff[sn]; bt.poff = poff;
+                    bt.rid = (int)breds.size();
                     poff += 3 * 64;
                     btiles.push_back(bt);
                     ++rd.nt;
@@ -782,8 +804,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         L.bt_count = (int)btiles.size() - L.bt_first;
         L.br_count = (int)breds.size() - L.br_first;
         max_lds = std::max(max_lds, std::max(L.lds_fwd, L.lds_bwd));
-        kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.asm_count ? 1 : 0) + (L.bt_count ? 2 : 0) +
-                    (L.ft_count ? 2 : 0);
+        kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.asm_count ? 1 : 0) + (L.bt_count ? 1 : 0) +
+                    (L.ft_count ? 1 : 0);
         levels_.push_back(L);
         if (stats) {
             double by = 0;
@@ -806,6 +828,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     btiles_.upload(btiles, s);
     ftiles_.upload(ftiles, s);
     freds_.upload(freds, s);
+    fcnt_.alloc(std::max<size_t>(freds.size(), 1)); fcnt_.zero(s);
+    bcnt_.alloc(std::max<size_t>(breds.size(), 1)); bcnt_.zero(s);
     breds_.upload(breds, s);
     bpart_.alloc(std::max<long long>(poff, 3));
     Y_.alloc(3 * (size_t)n_);
@@ -839,9 +863,7 @@ void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
         if (L.ft_count) {
             hipLaunchKernelGGL(k_fwd_tile, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, Fg_.p, bpart_.p,
-                               ctrl, gate_reject);
-            hipLaunchKernelGGL(k_fwd_red, dim3(L.frd_count), dim3(64), 0, s, freds_.p, L.fr_first, bpart_.p, Fg_.p, Y_.p,
-                               U_.p, ctrl, gate_reject);
+                               freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
         }
 #undef FWD
     }
@@ -858,8 +880,7 @@ void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject
 #undef BWD
         if (L.bt_count) {
             hipLaunchKernelGGL(k_bwd_tile, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p, x,
-                               bpart_.p, ctrl, gate_reject);
-            hipLaunchKernelGGL(k_bwd_red, dim3(L.br_count), dim3(64), 0, s, breds_.p, L.br_first, bpart_.p, x, ctrl, gate_reject);
+                               bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
         }
     }
 #define SUBB(BL) hipLaunchKernelGGL(k_bwd_sub<BL>, dim3(n_sub_), dim3(BL), sub_lds_b_, s, sub_trees_.p, sub_levels_.p, \

@@ -65,11 +65,11 @@ public:
     struct SubTree { int lvl0, nlvl; };
     // split-K backward of large supernodes: a tile (64 columns from c0, nr rows from r0) and the
     // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
-    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, pad; long long goff, poff; };
+    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid; long long goff, poff; };
     struct BRed { int beg, c0, nc, nt; long long poff; };
     // split-K forward of large supernodes: tile (64 rows from r0, nc columns from c0) and the
     // per-row-block reduction of its nt partials
-    struct FTile { int beg, p, R, c0, r0, nc, pad0, pad1; long long goff, foff, poff; };
+    struct FTile { int beg, p, R, c0, r0, nc, rid, pad; long long goff, foff, poff; };
     struct FRed { int beg, p, r0, nr, nt, pad; long long uoff, foff, poff; };
 
 private:
@@ -92,6 +92,7 @@ private:
     DevBuf<BRed> breds_;
     DevBuf<FTile> ftiles_;
     DevBuf<FRed> freds_;
+    DevBuf<int> fcnt_, bcnt_;   // tiles finished per reduction task (reset by the last tile)
     DevBuf<double> bpart_;
     std::vector<Level> levels_;
     // fused bottom subtrees
