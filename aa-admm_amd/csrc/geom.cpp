@@ -225,6 +225,15 @@ void GeomSolver::setup(int n_points, double penalty, int spd_solver_type) {
     auto t0 = std::chrono::steady_clock::now();
     n_ = n_points;
     rho_ = penalty;
+    // the reference builds the hard rows, then the soft rows (ALMGeometrySolver.h:97-129) and
+    // sums rho D_h^T D_h + D_s^T D_s + L^T L in that order: keep that order whatever the order
+    // of the add_*_constraint calls (so the C++ facade and the bindings assemble identically)
+    std::stable_partition(hgroups_.begin(), hgroups_.end(), [](const decltype(hgroups_)::value_type& g) { return g.hard; });
+    group_of_.clear();
+    for (size_t gi = 0; gi < hgroups_.size(); ++gi) {
+        const auto& g = hgroups_[gi];
+        group_of_.emplace(std::make_tuple(g.hard, g.type, g.K, g.weight, g.surf), (int)gi);
+    }
     arows_.assign(n_, {});
     for (auto& g : hgroups_) {
         for (int v : g.idx) if (v >= n_) throw Error(ERR_ARG, "constraint references a point index >= n_points");
@@ -256,7 +265,7 @@ void GeomSolver::setup(int n_points, double penalty, int spd_solver_type) {
     }
     for (int i = 0; i < n_; ++i) {
         auto& row = arows_[i];
-        std::sort(row.begin(), row.end(), [](const std::pair<int, double>& a, const std::pair<int, double>& b) { return a.first < b.first; });
+        std::stable_sort(row.begin(), row.end(), [](const std::pair<int, double>& a, const std::pair<int, double>& b) { return a.first < b.first; });
         size_t w = 0;
         for (size_t k = 0; k < row.size();) {
             size_t k2 = k;

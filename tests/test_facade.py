@@ -1,5 +1,8 @@
-"""The C++ drop-in facade (include/aa_admm.hpp): compiles against the C ABI on CPU; on the GPU
-it runs a reference-style caller (tests/cpp/facade_cloth.cpp) checked against the oracle."""
+"""The C++ drop-in facades compile against the C ABI on CPU; on the GPU they run reference-style
+callers: include/aa_admm.hpp (admm::Solver, tests/cpp/facade_cloth.cpp) checked against the
+oracle, include/aa_geometry.hpp (ALMGeometrySolver<3> + Constraint<3>,
+tests/cpp/facade_geom.cpp) checked bit for bit against the same scene bound through the Python
+binding (both drive the identical device path, so any mapping error shows)."""
 import os
 import subprocess
 
@@ -12,14 +15,45 @@ from golden_io import scenes
 SRC = os.path.join(REPO, "tests", "cpp", "facade_cloth.cpp")
 
 
-def build(out):
+GEOM_SRC = os.path.join(REPO, "tests", "cpp", "facade_geom.cpp")
+
+
+def build(out, src=SRC):
     lib = os.path.join(REPO, "aa-admm_amd")
-    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-I" + os.path.join(REPO, "include"), SRC, "-o", out,
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-I" + os.path.join(REPO, "include"), src, "-o", out,
                     "-L" + lib, "-laa_admm", "-Wl,-rpath," + lib], check=True)
 
 
 def test_facade_builds(tmp_path):
     build(str(tmp_path / "facade_cloth"))
+
+
+def test_geometry_facade_builds(tmp_path):
+    build(str(tmp_path / "facade_geom"), GEOM_SRC)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("builder", [
+    lambda gs: gs.pq_heightfield(12, 10, iters=40, aa_m=10, noise=0.3),
+    lambda gs: gs.wire_grid(12, 12, iters=40, aa_m=20),
+])
+def test_geometry_facade_matches_binding(builder, tmp_path, pkg, ctx):
+    sc = builder(pkg.geom_scenes)
+    exe, scene, out = str(tmp_path / "facade_geom"), str(tmp_path / "s.bin"), str(tmp_path / "o.bin")
+    build(exe, GEOM_SRC)
+    pkg.geom_scenes.write_geom_scene(sc, scene)
+    eps = 1e-8 * max(sc.avg_edge_length(), 1e-300)
+    r = subprocess.run([exe, scene, out, repr(eps)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(out, "rb").read()
+    nf = int(np.frombuffer(raw[:4], np.int32)[0])
+    comb = np.frombuffer(raw[4:4 + 8 * nf], np.float64)
+    x = np.frombuffer(raw[4 + 8 * nf:], np.float64).reshape(-1, 3)
+    want, g = pkg.capi.run_geom(ctx, sc)
+    g.close()
+    assert nf == len(want["comb"]) == sc.iters
+    assert np.array_equal(comb, want["comb"])
+    assert np.array_equal(x, want["x"])
 
 
 @pytest.mark.gpu
