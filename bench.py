@@ -97,6 +97,24 @@ def time_to_eps(comb, step_ms, iters_run):
     return (hit[0] + 1) * step_ms / iters_run
 
 
+def run_logged(cmd, cwd, env, timeout):
+    """subprocess.run with a heartbeat on stderr every 30 s (long CPU-baseline legs must not look
+    hung to a supervisor that watches the output)."""
+    p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    t0 = time.time()
+    while True:
+        try:
+            out, err = p.communicate(timeout=30)
+            return subprocess.CompletedProcess(cmd, p.returncode, out, err)
+        except subprocess.TimeoutExpired:
+            el = time.time() - t0
+            print(f"[bench] {os.path.basename(cmd[0])} running for {el:.0f} s", file=sys.stderr, flush=True)
+            if el > timeout:
+                p.kill()
+                p.communicate()
+                raise
+
+
 def cpu_baseline(sc, scale=1.0, what=""):
     """The REFERENCE (oracle/_ref/ref_elastic_{h,x}, compiled from the reference's own sources)
     on the host cores, bounded sample `sc` (3 time steps); the first step (OpenMP spin-up,
@@ -110,7 +128,7 @@ def cpu_baseline(sc, scale=1.0, what=""):
         if os.path.exists(drv):
             env = dict(os.environ, OMP_NUM_THREADS=str(threads))
             t0 = time.time()
-            r = subprocess.run([drv, "s.bin", "o.bin"], cwd=tmp, capture_output=True, text=True, env=env, timeout=900)
+            r = run_logged([drv, "s.bin", "o.bin"], tmp, env, 900)
             wall = time.time() - t0
             if r.returncode != 0:
                 raise RuntimeError(r.stderr[-500:])
@@ -148,7 +166,10 @@ def geom_cpu_baseline(args):
     """The REFERENCE's ALMGeometrySolver (oracle/_ref/ref_geom, compiled from its own sources) on
     the host cores, bounded sample: the same scene with a reduced iteration count."""
     gs = importlib.import_module("aa-admm_amd.geom_scenes")
-    sc, _ = geom_scene(argparse.Namespace(**{**vars(args), "iters": args.cpu_iters}))
+    # bounded sample (~10-30 s of CPU work): the 500k-point wire mesh costs ~0.6 s per reference
+    # iteration plus two LDLT factorisations, so it gets fewer iterations than the PQ mesh
+    iters = args.cpu_iters if args.config == "c3" else min(args.cpu_iters, 10)
+    sc, _ = geom_scene(argparse.Namespace(**{**vars(args), "iters": iters}))
     drv = os.path.join(REPO, "oracle", "_ref", "ref_geom")
     threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
     if not os.path.exists(drv):
@@ -156,13 +177,13 @@ def geom_cpu_baseline(args):
     with tempfile.TemporaryDirectory() as tmp:
         gs.write_geom_scene(sc, os.path.join(tmp, "s.bin"))
         env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-        r = subprocess.run([drv, "s.bin", "o.bin"], cwd=tmp, capture_output=True, text=True, env=env, timeout=900)
+        r = run_logged([drv, "s.bin", "o.bin"], tmp, env, 900)
         if r.returncode != 0:
             raise RuntimeError(r.stderr[-500:])
         res = gs.read_geom_result(os.path.join(tmp, "o.bin"), sc.n_points)
     return {"value": round(len(res["comb"]) / res["loop_s"], 3), "unit": "ADMM iters/s", "cores": threads,
             "kind": "reference", "setup_s": round(res["setup_s"], 3),
-            "sample": f"{sc.name}: one solve_ADMM of {args.cpu_iters} accepted iterations (m={sc.aa_m}), loop time "
+            "sample": f"{sc.name}: one solve_ADMM of {iters} accepted iterations (m={sc.aa_m}), loop time "
                       f"(setup excluded, as ALMGeometrySolver.h:194-195), OMP_NUM_THREADS={threads}"}
 
 
@@ -180,6 +201,7 @@ def main_geom(args, world, rank, local, dist):
         g.solve(sc.x0, 1e-8 * sc.avg_edge_length(), sc.iters, sc.aa_m)   # first solve also orders + factors
     rt0 = g.runtime()
     setup_ms = (time.time() - t0) * 1e3
+    print(f"[bench] {args.config} setup + warm-up {setup_ms / 1e3:.1f} s", file=sys.stderr, flush=True)
     barrier(dist, ctx)
     t0 = time.perf_counter()
     acc, xupd, tte = 0, 0, []
@@ -212,6 +234,7 @@ def main_geom(args, world, rank, local, dist):
                 "phase_us_per_iter": {kk: round(v["avg_ms"] * 1e3, 2) for kk, v in stats.items()},
                 "phase_bytes_per_iter": {kk: v["bytes"] for kk, v in stats.items()}}
         if world == 1 and not args.no_cpu_baseline:
+            print("[bench] timing the reference CPU baseline", file=sys.stderr, flush=True)
             try:
                 cpu = geom_cpu_baseline(args)
             except Exception as e:
@@ -293,6 +316,7 @@ def main():
     t0 = time.time()
     solver.initialize(capi.settings_from_scene(sc))
     setup_ms = (time.time() - t0) * 1e3
+    print(f"[bench] {args.config} setup {setup_ms / 1e3:.1f} s", file=sys.stderr, flush=True)
     for _ in range(args.warmup):
         solver.step()
 
@@ -336,8 +360,17 @@ def main():
                 "phase_us_per_launch": {kk: round(v["avg_ms"] * 1e3, 2) for kk, v in stats.items()},
                 "phase_bytes_per_launch": {kk: v["bytes"] for kk, v in stats.items()},
                 "dominant_phase": max(per_iter, key=per_iter.get)}
+    if roof is not None:   # HBM bytes per solve from the committed PMC passes (tools/gpu_pmc.sh)
+        pmc = os.path.join(REPO, "profiles", f"r1_{args.config}_pmc.json")
+        if os.path.exists(pmc) and comm is None:
+            sp = json.load(open(pmc)).get("solve_per_launch") or {}
+            if sp.get("traffic_B"):
+                roof["traffic"] = sp["traffic_B"]
+                roof["traffic_source"] = (f"profiles/r1_{args.config}_pmc.json: FETCH_SIZE (x2, calibrated on k_copy) "
+                                          f"+ WRITE_SIZE over one solve's {sp['kernels']} kernels, separate --pmc passes")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        print("[bench] timing the reference CPU baseline", file=sys.stderr, flush=True)
         try:
             cpu = elastic_cpu_baseline(args)
         except Exception as e:  # report, never fail the GPU number on the baseline leg

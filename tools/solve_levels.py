@@ -1,5 +1,6 @@
 """Per-launch durations of the last global solve in a rocprofv3 kernel trace (NO_GRAPH runs)."""
 import csv
+import re
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
@@ -14,7 +15,8 @@ tot = 0
 for r in rows[start:end + 1]:
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
     tot += d
-    nm = r["Kernel_Name"].split("::")[-1].split("(")[0]
+    m = re.search(r"(k_[a-z_0-9]+(<[^>]*>)?)", r["Kernel_Name"])
+    nm = m.group(1) if m else r["Kernel_Name"][:20]
     print("  %-14s grid %8d wg %4s lds %6s vgpr %3s %7.2f us" % (nm, int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]),
           r["Workgroup_Size_X"], r["LDS_Block_Size"], r["VGPR_Count"], d))
 print(" kernels", end - start + 1, "sum %.1f us, wall %.1f us" % (tot, (int(rows[end]["End_Timestamp"]) - int(rows[start]["Start_Timestamp"])) / 1000))
