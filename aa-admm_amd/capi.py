@@ -26,7 +26,7 @@ EXPORTS = [
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats",
     "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_destroy", "aa_comm_info",
-    "aa_comm_allreduce_host", "aa_elastic_set_comm",
+    "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
     "aa_geom_create", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
     "aa_geom_add_closeness", "aa_geom_setup", "aa_geom_solve", "aa_geom_get_solution", "aa_geom_get_history",
     "aa_geom_runtime_info", "aa_geom_closest_points", "aa_geom_bench_iterations", "aa_geom_kernel_stats",
@@ -380,6 +380,11 @@ class GeomSolver:
         t = np.ascontiguousarray(target, np.float64)
         _chk(lib().aa_geom_add_closeness(self.h, C.c_int(idx), C.c_double(weight), _dp(t)))
 
+    def set_comm(self, comm):
+        """Partition over comm's ranks at the first solve (every rank adds the same problem)."""
+        self.comm = comm
+        _chk(lib().aa_geom_set_comm(self.h, comm.h if comm is not None else None))
+
     def setup(self, n_points, penalty, spd=AA_SPD_LDLT):
         self.n = n_points
         _chk(lib().aa_geom_setup(self.h, C.c_int(n_points), C.c_double(penalty), C.c_int(spd)))
@@ -423,9 +428,11 @@ class GeomSolver:
         return dict(avg_ms=a.value, bytes=b.value, launches=n.value)
 
 
-def geom_from_scene(ctx: Context, sc) -> GeomSolver:
+def geom_from_scene(ctx: Context, sc, comm=None) -> GeomSolver:
     """Binds a geom_scenes.GeomScene the way optimize_mesh (PlanarityOpt.cpp / WireMeshOpt.cpp) does."""
     g = GeomSolver(ctx)
+    if comm is not None:
+        g.set_comm(comm)
     sids = [g.add_ref_surface(V, F) for V, F in sc.surfaces]
     for grp in sc.groups:
         prm = grp.params
@@ -444,9 +451,9 @@ def geom_from_scene(ctx: Context, sc) -> GeomSolver:
     return g
 
 
-def run_geom(ctx: Context, sc):
+def run_geom(ctx: Context, sc, comm=None):
     """setup_ADMM + solve_ADMM of a GeomScene; returns dict(comb, time_s, x) and the solver."""
-    g = geom_from_scene(ctx, sc)
+    g = geom_from_scene(ctx, sc, comm)
     g.solve(sc.x0, 1e-8 * max(sc.avg_edge_length(), 1e-300), sc.iters, sc.aa_m)
     h = g.history()
     h["x"] = g.solution()

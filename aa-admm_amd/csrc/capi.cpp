@@ -235,6 +235,10 @@ int aa_elastic_set_comm(aa_elastic h, aa_comm c) {
     return guarded([&] { NEED(h, "null handle"); h->s->set_comm(c ? c->c.get() : nullptr); });
 }
 
+int aa_geom_set_comm(aa_geom h, aa_comm c) {
+    return guarded([&] { NEED(h, "null handle"); h->s->set_comm(c ? c->c.get() : nullptr); });
+}
+
 int aa_elastic_bench_iterations(aa_elastic h, int iters, double* ms) {
     return guarded([&] {
         NEED(h && iters >= 0, "bad argument");

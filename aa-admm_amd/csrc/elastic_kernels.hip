@@ -451,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
                                                       double* __restrict__ dF, double* __restrict__ dG, Ctrl* ctrl,
                                                       double* red, Seg2 copy_to, const double* comb_a,
                                                       const double* comb_b, int comb_nb, double* hist_prim,
-                                                      double* hist_comb, int* hist_rej) {
+                                                      double* hist_comb, int* hist_rej, AAMask mask) {
     if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
     constexpr int NVAL = 2 + 2 * MM;
     __shared__ double sm[kBlock / 64][NVAL];
@@ -486,6 +486,10 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
             const double f = g - cur[i];
             const double dfj = dF[(size_t)col * eff + i] + f;
             dF[(size_t)col * eff + i] = dfj;
+            if (i >= G.na) {
+                const long long j = i - G.na;
+                if (!((j >= mask.lo1 && j < mask.hi1) || (j >= mask.lo2 && j < mask.hi2))) continue;
+            }
             acc[0] += dfj * dfj;
             acc[1] += dfj * f;
 #pragma unroll
@@ -875,8 +879,8 @@ static int mm_bucket(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : 32); }
 
 void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, double* red,
                       int nblocks, Seg2 copy_to, int m, hipStream_t s, const double* comb_a, const double* comb_b,
-                      int comb_nb, double* hist_prim, double* hist_comb, int* hist_rej) {
-#define AA_RED_ARGS G, cur, eff, dF, dG, ctrl, red, copy_to, comb_a, comb_b, comb_nb, hist_prim, hist_comb, hist_rej
+                      int comb_nb, double* hist_prim, double* hist_comb, int* hist_rej, AAMask mask) {
+#define AA_RED_ARGS G, cur, eff, dF, dG, ctrl, red, copy_to, comb_a, comb_b, comb_nb, hist_prim, hist_comb, hist_rej, mask
     switch (mm_bucket(m)) {
         case 8: hipLaunchKernelGGL(k_aa_reduce<8>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
         case 16: hipLaunchKernelGGL(k_aa_reduce<16>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;

@@ -43,6 +43,13 @@ struct Seg2 {
     double* b; long long nb;
 };
 
+// Entries of the second segment that enter the Anderson dot products (partitioned solvers: the
+// x entries this rank owns -- its part and, on rank 0, the shared separators); the first
+// segment always counts. Default: everything.
+struct AAMask {
+    long long lo1 = 0, hi1 = 0x7fffffffffffffffLL, lo2 = 0, hi2 = 0;
+};
+
 struct ElasticLaunch;  // fwd
 
 // ---- launchers (elastic_kernels.hip) ---------------------------------------------------
@@ -98,7 +105,7 @@ int aa_reduce_blocks(long long dim);
 void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, double* red,
                       int nblocks, Seg2 copy_to, int m, hipStream_t s, const double* comb_a = nullptr,
                       const double* comb_b = nullptr, int comb_nb = 0, double* hist_prim = nullptr,
-                      double* hist_comb = nullptr, int* hist_rej = nullptr);
+                      double* hist_comb = nullptr, int* hist_rej = nullptr, AAMask mask = AAMask());
 void launch_aa_solve(Ctrl* ctrl, const double* red, int nblocks, int m, hipStream_t s);
 void launch_aa_mix(Seg2 G, double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, Seg2 out, int m,
                    hipStream_t s);

@@ -286,16 +286,63 @@ void GeomSolver::setup(int n_points, double penalty, int spd_solver_type) {
     rt_.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+void GeomSolver::set_comm(Comm* c) {
+    if (factored_) throw Error(ERR_STATE, "set_comm after the first solve_ADMM is not supported");
+    comm_ = c;
+    rank_ = c ? c->rank() : 0;
+}
+
 void GeomSolver::factor_and_upload(const double* init_x3) {
     auto t0 = std::chrono::steady_clock::now();
     drop_graph();
     // nested-dissection order over the matrix graph, bisected on the initial point positions
     std::vector<int> aptr(n_ + 1, 0), aj;
+    const bool parted = comm_ && comm_->size() > 1;
+    std::vector<std::vector<int>> cl;
+    if (parted) {
+        // partitioned: every constraint's points must land in one part (plus separators), but
+        // D^T D need not couple them all (an angle constraint's two side points have no matrix
+        // entry): dissect the graph with each constraint's points made a clique. Separators of
+        // this supergraph also separate the matrix graph, so the tree stays a valid elimination
+        // order for the factor.
+        cl.resize(n_);
+        for (auto& g : hgroups_)
+            for (int c = 0; c < g.count(); ++c)
+                for (int a = 0; a < g.K; ++a)
+                    for (int b = 0; b < g.K; ++b)
+                        if (a != b) cl[g.idx[(size_t)c * g.K + a]].push_back(g.idx[(size_t)c * g.K + b]);
+    }
     for (int i = 0; i < n_; ++i) {
+        const size_t s0 = aj.size();
         for (auto& e : arows_[i]) if (e.first != i) aj.push_back(e.first);
+        if (parted) {
+            aj.insert(aj.end(), cl[i].begin(), cl[i].end());
+            std::sort(aj.begin() + s0, aj.end());
+            aj.erase(std::unique(aj.begin() + s0, aj.end()), aj.end());
+            std::vector<int>().swap(cl[i]);
+        }
         aptr[i + 1] = (int)aj.size();
     }
-    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, 32, DirectSolver::kTopRows);
+    // partitioned: the first log2(P) bisections are forced; part r (a contiguous
+    // range of points) belongs to rank r, the separators ("top") are shared
+    const int P = comm_ ? comm_->size() : 1;
+    int levels = 0;
+    while ((1 << levels) < P) ++levels;
+    if ((1 << levels) != P) throw Error(ERR_ARG, "solve_ADMM: the number of ranks must be a power of two");
+    if (P > 1) {   // every rank must have been handed the same problem
+        double h[4] = {(double)n_, (double)hgroups_.size(), 0, 0};
+        for (auto& g : hgroups_) h[2] += (double)g.idx.size();
+        for (int i = 0; i < 3 * n_; ++i) h[3] += init_x3[i];
+        double r[4] = {h[0], h[1], h[2], h[3]};
+        comm_->allreduce_sum_host(r, 4);
+        for (int i = 0; i < 4; ++i)
+            if (std::fabs(r[i] - P * h[i]) > 1e-12 * std::fabs(P * h[i]))
+                throw Error(ERR_ARG, "solve_ADMM: the ranks were given different problems");
+    }
+    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, levels);
+    top_beg_ = P > 1 ? tree.top_beg : n_;
+    own_beg_ = P > 1 ? tree.part_beg[rank_] : 0;
+    own_end_ = P > 1 ? tree.part_end[rank_] : n_;
     int2user_ = tree.perm;
     user2int_.assign(n_, -1);
     for (int q = 0; q < n_; ++q) user2int_[int2user_[q]] = q;
@@ -315,17 +362,51 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     } catch (const std::runtime_error& e) {
         throw Error(ERR_NUMERIC, std::string("Error: SPD solver initialization failed: ") + e.what());
     }
-    solver_.build(F, s());
+    solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_);
     rt_.nnz_factor = (long long)F.nnz_L;
+
+    // constraint ownership (partitioned): a constraint touching a point of part r belongs to
+    // rank r (it cannot touch another part); constraints on separator points only go
+    // round-robin. Every rank computes the same assignment.
+    std::vector<HostGroup> owned;
+    nbg_ = 0;
+    long long zhmax = 0;
+    if (P > 1) {
+        std::vector<int> qpart(n_, -1);
+        for (int r = 0; r < P; ++r) for (int q = tree.part_beg[r]; q < tree.part_end[r]; ++q) qpart[q] = r;
+        std::vector<long long> zr(P, 0);
+        std::vector<int> br(P, 0);
+        long long rr = 0;
+        for (auto& hg : hgroups_) {
+            const int cnt = hg.count(), K = hg.K, Pn = n_params(hg.type), C = cols_of(hg.type, K);
+            std::vector<int> c(P, 0);
+            HostGroup lg = hg;
+            lg.idx.clear(); lg.prm.clear();
+            for (int e = 0; e < cnt; ++e) {
+                int o = -1;
+                for (int a = 0; a < K && o < 0; ++a) o = qpart[user2int_[hg.idx[(size_t)e * K + a]]];
+                if (o < 0) o = (int)(rr++ % P);
+                ++c[o];
+                if (o != rank_) continue;
+                lg.idx.insert(lg.idx.end(), hg.idx.begin() + (size_t)e * K, hg.idx.begin() + (size_t)(e + 1) * K);
+                lg.prm.insert(lg.prm.end(), hg.prm.begin() + (size_t)e * Pn, hg.prm.begin() + (size_t)(e + 1) * Pn);
+            }
+            if (hg.hard)
+                for (int r = 0; r < P; ++r) { br[r] += geo_u_blocks(c[r]); zr[r] += 3LL * C * c[r]; }
+            owned.push_back(std::move(lg));
+        }
+        for (int r = 0; r < P; ++r) { nbg_ = std::max(nbg_, br[r]); zhmax = std::max(zhmax, zr[r]); }
+    }
+    const std::vector<HostGroup>& dgroups = P > 1 ? owned : hgroups_;
 
     // device constraint groups (internal point ids), z/u offsets, rhs slots
     groups_.clear();
-    groups_.resize(hgroups_.size());
+    groups_.resize(dgroups.size());
     Zh_ = 0; slots_ = 0; red_blocks_ = 0;
     std::vector<std::vector<int>> pslots(n_);
     long long soft_cols = 0, ncons = 0;
-    for (size_t gi = 0; gi < hgroups_.size(); ++gi) {
-        const HostGroup& hg = hgroups_[gi];
+    for (size_t gi = 0; gi < dgroups.size(); ++gi) {
+        const HostGroup& hg = dgroups[gi];
         DevGroup& dg = groups_[gi];
         const int cnt = hg.count(), K = hg.K, P = n_params(hg.type), C = cols_of(hg.type, K);
         std::vector<int> idx((size_t)K * cnt);
@@ -373,13 +454,26 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     std::vector<double> rf(3 * (size_t)n_);
     for (int q = 0; q < n_; ++q)
         for (int d = 0; d < 3; ++d) rf[3 * (size_t)q + d] = rhs_fixed_user_[3 * (size_t)int2user_[q] + d];
+    // partitioned: a shared separator row's constant (regularisation) term enters once (rank 0)
+    if (P > 1 && rank_ != 0) std::fill(rf.begin() + 3 * (size_t)top_beg_, rf.end(), 0.0);
+    if (P == 1) { nbg_ = red_blocks_; zhmax = Zh_; }
+    zh_max_ = zhmax;
+    aamask_ = AAMask();
+    if (P > 1) {   // the x entries this rank owns enter the Anderson dot products
+        aamask_.lo1 = 3LL * own_beg_; aamask_.hi1 = 3LL * own_end_;
+        aamask_.lo2 = rank_ == 0 ? 3LL * top_beg_ : 0; aamask_.hi2 = rank_ == 0 ? 3LL * n_ : 0;
+    }
     rhs_fixed_.upload(rf, s());
     const size_t nx = 3 * (size_t)n_, nu = std::max<size_t>(1, (size_t)Zh_);
     b_.alloc(nx); y_.alloc(std::max<size_t>(3, 3 * (size_t)slots_));
     cur_x_.alloc(nx); new_x_.alloc(nx); def_x_.alloc(nx);
+    cur_x_.zero(s()); new_x_.zero(s()); def_x_.zero(s());   // rows of other parts stay finite
     cur_u_.alloc(nu); new_u_.alloc(nu); def_u_.alloc(nu); z_.alloc(nu);
-    red_.alloc(std::max(1, red_blocks_));
+    nbg_ = std::max(1, nbg_);
+    red_.alloc(nbg_);   // this rank's partials, padded to the largest rank's block count
     red_.zero(s());
+    if (comm_) { red_g_.alloc(nbg_); red_g_.zero(s()); redg_ = red_g_.p; }
+    else redg_ = red_.p;
     ctrl_.alloc(1);
     clock0_.alloc(1);
     int khz = 0;
@@ -417,9 +511,11 @@ void GeomSolver::prepare_m(int m) {
         aa_cur_.alloc(dim);
         aa_dF_.alloc((size_t)m * dim); aa_dF_.zero(s());
         aa_dG_.alloc((size_t)m * dim); aa_dG_.zero(s());
-        aa_blocks_ = aa_reduce_blocks(dim);
+        aa_blocks_ = aa_reduce_blocks(zh_max_ + 3LL * n_);   // the same grid on every rank
         const int mm = m <= 8 ? 8 : (m <= 16 ? 16 : 32);
-        aa_red_.alloc((size_t)aa_blocks_ * (2 + 2 * mm));
+        aa_red_.alloc((size_t)aa_blocks_ * (2 + 2 * mm)); aa_red_.zero(s());
+        if (comm_) { aa_red_g_.alloc(aa_red_.n); aa_red_g_.zero(s()); aag_ = aa_red_g_.p; }
+        else aag_ = aa_red_.p;
         kstats_["aa"].bytes = 8.0 * dim * (2.0 * std::min(m, 32) + 8.0);
     } else {
         aa_cur_.release(); aa_dF_.release(); aa_dG_.release(); aa_red_.release();
@@ -490,14 +586,17 @@ void GeomSolver::enqueue_iteration(int m) {
     }
     ev_mark("u");
     ev_mark("aa");
-    launch_geo_control(c, red_.p, red_blocks_, m > 0, hist_comb_.p, hist_clock_.p, s());
+    if (comm_) comm_->allreduce_sum(red_.p, red_g_.p, (size_t)nbg_, s());
+    launch_geo_control(c, redg_, nbg_, m > 0, hist_comb_.p, hist_clock_.p, s());
     if (m > 0) {
         launch_geo_restore(cur_u_.p, cur_x_.p, aa_cur_.p, def_u_.p, def_x_.p, Zh_, nx, c, s());
         Seg2 G{new_u_.p, Zh_, new_x_.p, nx};
         Seg2 cp{def_u_.p, Zh_, def_x_.p, nx};
         Seg2 out{cur_u_.p, Zh_, cur_x_.p, nx};
-        launch_aa_reduce(G, aa_cur_.p, Zh_ + nx, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, cp, m, s());
-        launch_aa_solve(c, aa_red_.p, aa_blocks_, m, s());
+        launch_aa_reduce(G, aa_cur_.p, Zh_ + nx, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, cp, m, s(), nullptr,
+                         nullptr, 0, nullptr, nullptr, nullptr, aamask_);
+        if (comm_) comm_->allreduce_sum(aa_red_.p, aa_red_g_.p, aa_red_.n, s());
+        launch_aa_solve(c, aag_, aa_blocks_, m, s());
         launch_aa_mix(G, aa_cur_.p, Zh_ + nx, aa_dF_.p, aa_dG_.p, c, out, m, s());
     } else {
         if (Zh_) launch_copy(cur_u_.p, new_u_.p, Zh_, c, 0, s());
@@ -541,7 +640,8 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
     prologue(init_x3, max_iter, m, max_iter);
     const int target = std::max(1, max_iter);
     const int chunk = std::min(target, 64);
-    const bool use_graph = !(std::getenv("AA_ADMM_NO_GRAPH") && std::getenv("AA_ADMM_NO_GRAPH")[0] == '1');
+    const bool use_graph = !(std::getenv("AA_ADMM_NO_GRAPH") && std::getenv("AA_ADMM_NO_GRAPH")[0] == '1') &&
+                           !(comm_ && !comm_->capturable());
     auto run_chunk = [&]() {
         if (use_graph) {
             if (!gexec_ || graph_chunk_ != chunk || graph_m_ != m) {
@@ -573,6 +673,16 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
         passes += chunk;
     }
     fetch_results();
+    if (comm_) {   // every rank ends with the full solution: zero what it does not own, sum
+        auto zero = [&](int q0, int q1) {
+            if (q1 > q0) AA_HIP(hipMemsetAsync(new_x_.p + 3 * (size_t)q0, 0, 24 * (size_t)(q1 - q0), s()));
+        };
+        zero(0, own_beg_);
+        zero(own_end_, top_beg_);
+        if (rank_ != 0) zero(top_beg_, n_);
+        comm_->allreduce_sum(new_x_.p, new_x_.p, 3 * (size_t)n_, s());
+        AA_HIP(hipStreamSynchronize(s()));
+    }
     have_solution_ = true;
     rt_.solve_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }

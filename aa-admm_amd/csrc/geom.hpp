@@ -31,6 +31,9 @@ public:
     int history(double* comb, double* time_s, int cap) const;
     aa_geom_runtime runtime() const { return rt_; }
     void closest_points(int surface, const double* p3, int n, double* out3);
+    // multi-GPU: partition the points over comm's ranks at the first solve;
+    // every rank passes the same problem. Not owned; must outlive the solver.
+    void set_comm(Comm* c);
 
     double bench_iterations(int iters);
     bool kernel_stats(const std::string& name, double* avg_ms, double* bytes, int* launches) const;
@@ -84,6 +87,15 @@ private:
     DevBuf<double> rhs_fixed_, b_, y_;
     DevBuf<double> cur_x_, new_x_, def_x_, cur_u_, new_u_, def_u_, z_;
     DevBuf<double> aa_cur_, aa_dF_, aa_dG_, aa_red_, red_;
+    // partition: own points [own_beg_, own_end_), shared top [top_beg_, n_); all-rank sums of
+    // the residual / Anderson partials (aliases of the local ones on one GPU)
+    Comm* comm_ = nullptr;
+    int rank_ = 0, own_beg_ = 0, own_end_ = 0, top_beg_ = 0, nbg_ = 0;
+    long long zh_max_ = 0;
+    DevBuf<double> red_g_, aa_red_g_;
+    double* redg_ = nullptr;
+    double* aag_ = nullptr;
+    AAMask aamask_;
     DevBuf<Ctrl> ctrl_;
     DevBuf<double> hist_comb_;
     DevBuf<unsigned long long> hist_clock_, clock0_;

@@ -197,6 +197,10 @@ int aa_geom_runtime_info(aa_geom h, aa_geom_runtime* out);
 int aa_geom_closest_points(aa_geom h, int surface, const double* p3, int n, double* out3);
 int aa_geom_bench_iterations(aa_geom h, int iters, double* ms);
 int aa_geom_kernel_stats(aa_geom h, const char* name, double* avg_ms, double* bytes, int* launches);
+/* Multi-GPU (see aa_comm above): attach before the first aa_geom_solve; every rank adds the same
+ * constraints; the first solve partitions the points (nested dissection of the global matrix on
+ * the initial positions) and each rank projects the constraints of its part. */
+int aa_geom_set_comm(aa_geom h, aa_comm c);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 scenes = importlib.import_module("aa-admm_amd.scenes")
+geom_scenes = importlib.import_module("aa-admm_amd.geom_scenes")
 
 CASES = {
     # (u,x)-AA cloth with two pinned corners (C2 recipe, 3 200 tris)
@@ -23,4 +24,12 @@ CASES = {
     # no Anderson, z order, linear tets
     "cant_z_noaa": (lambda: scenes.cantilever(10, 3, 3, scenes.LINEAR, iters=30, n_steps=2,
                                               variant=scenes.VARIANT_X, accel=0), 1e-9),
+}
+
+# Geometry (ALM) cases: the same bars as tests/test_gpu_geom.py (comb relative to comb_0: 1e-8 over
+# the first 40 accepted iterations, 1e-6 over the curve; solution 1e-8 / 1e-6 relative)
+GEOM_CASES = {
+    "pq": lambda: geom_scenes.pq_heightfield(24, 20, iters=40, aa_m=10, noise=0.3),
+    "wire": lambda: geom_scenes.wire_grid(24, 24, iters=40, aa_m=20),
+    "pq_noaa": lambda: geom_scenes.pq_heightfield(16, 16, iters=30, aa_m=0, noise=0.3),
 }

@@ -15,20 +15,31 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-from part_cases import CASES  # noqa: E402
+from part_cases import CASES, GEOM_CASES  # noqa: E402
 
 
 def main():
     pkg = importlib.import_module("aa-admm_amd")
     dist.init_process_group("gloo")
     rank, size = dist.get_rank(), dist.get_world_size()
-    sc = CASES[os.environ["AA_CASE"]][0]()
+    case = os.environ["AA_CASE"]
     device = int(os.environ.get("AA_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     ctx = pkg.capi.Context(device)
     if os.environ.get("AA_TRANSPORT", "host") == "rccl":
         comm = pkg.dist.rccl_comm(ctx, rank, size)
     else:
         comm = pkg.dist.host_comm(rank, size)
+    if case.startswith("geom:"):
+        sc = GEOM_CASES[case[5:]]()
+        h, g = pkg.capi.run_geom(ctx, sc, comm=comm)
+        np.savez(os.path.join(os.environ["AA_OUT"], f"rank{rank}.npz"), comb=h["comb"], x=h["x"],
+                 n_constraints=np.array([g.runtime().n_constraints]))
+        g.close()
+        comm.close()
+        ctx.close()
+        dist.destroy_process_group()
+        return
+    sc = CASES[case][0]()
     steps, s = pkg.capi.run_scene(ctx, sc, comm=comm)
     out = {}
     for k, st in enumerate(steps):

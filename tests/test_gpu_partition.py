@@ -19,8 +19,8 @@ import numpy as np
 import pytest
 
 from conftest import REPO
-from golden_io import compare
-from part_cases import CASES
+from golden_io import compare, compare_geom
+from part_cases import CASES, GEOM_CASES
 
 pytestmark = pytest.mark.gpu
 
@@ -82,3 +82,18 @@ def test_rccl_transport_one_rank_is_identity(pkg, ctx):
     s.close()
     assert np.array_equal(comm.allreduce_host(np.arange(5.0)), np.arange(5.0))
     comm.close()
+
+
+@pytest.mark.parametrize("case,nranks", [("pq", 2), ("pq", 4), ("wire", 2), ("pq_noaa", 2)])
+def test_partitioned_geometry_matches_single_gpu(case, nranks, tmp_path, pkg, ctx):
+    sc = GEOM_CASES[case]()
+    want, g = pkg.capi.run_geom(ctx, sc)
+    n_cons = g.runtime().n_constraints
+    g.close()
+    ranks = run_ranks("geom:" + case, nranks, tmp_path)
+    assert sum(int(r["n_constraints"][0]) for r in ranks) == n_cons   # each constraint on one rank
+    for r in ranks[1:]:
+        assert np.array_equal(r["comb"], ranks[0]["comb"]) and np.array_equal(r["x"], ranks[0]["x"])
+    got = {"comb": ranks[0]["comb"], "x": ranks[0]["x"]}
+    fails = compare_geom(want, got, 1e-8, 1e-8, n_check=40) + compare_geom(want, got, 1e-6, 1e-6)
+    assert not fails, fails
