@@ -53,7 +53,7 @@ def parse():
                         "(configs[2]); c5: wire mesh 707x707 (configs[4])")
     p.add_argument("--tets", type=str, default="100,40,50", help="c4 block size in cubes (5 tets per cube)")
     p.add_argument("--partition", default="auto", choices=["auto", "none", "rccl", "host"],
-                   help="elastic configs with N>1: partition ONE mesh over the ranks (rccl: RCCL over xGMI, one "
+                   help="N>1: partition ONE mesh over the ranks (rccl: RCCL over xGMI, one "
                         "GPU per rank; host: host-staged gloo transport, for rehearsals with several ranks on one "
                         "GPU) or run independent replicas (none). auto = rccl when N>1")
     p.add_argument("--same-device", action="store_true", help="all ranks on GPU 0 (rehearsal with --partition host)")
@@ -152,6 +152,22 @@ def cpu_baseline(sc, scale=1.0, what=""):
     return out
 
 
+def make_comm(pkg, ctx, args, world, rank):
+    """Communicator of a mesh-partitioned run (None for replicas)."""
+    part = args.partition if args.partition != "auto" else ("rccl" if world > 1 else "none")
+    comm = None
+    if part == "rccl":
+        try:
+            comm = pkg.dist.rccl_comm(ctx, rank, world)
+        except Exception as e:   # transport only: the compute stays on the GPUs either way
+            print(f"[bench] RCCL communicator failed ({e}); using the host-staged transport", file=sys.stderr)
+            part = "host (rccl init failed)"
+            comm = pkg.dist.host_comm(rank, world)
+    elif part == "host":
+        comm = pkg.dist.host_comm(rank, world)
+    return comm, part
+
+
 def geom_scene(args):
     gs = importlib.import_module("aa-admm_amd.geom_scenes")
     if args.config == "c3":
@@ -192,10 +208,11 @@ def main_geom(args, world, rank, local, dist):
     (inputs resident on the device after setup); value = accepted iterations / wall time."""
     pkg = importlib.import_module("aa-admm_amd")
     capi = pkg.capi
-    ctx = capi.Context(local)
+    ctx = capi.Context(0 if args.same_device else local)
     sc, desc = geom_scene(args)
+    comm, part = make_comm(pkg, ctx, args, world, rank)
     t0 = time.time()
-    g = capi.geom_from_scene(ctx, sc)
+    g = capi.geom_from_scene(ctx, sc, comm)
     eps = 2.0 * (1e-8 * sc.avg_edge_length() * sc.hard_cols()) ** 2   # ALMGeometrySolver.h:173 (commented stop)
     for _ in range(max(1, args.warmup)):
         g.solve(sc.x0, 1e-8 * sc.avg_edge_length(), sc.iters, sc.aa_m)   # first solve also orders + factors
@@ -216,11 +233,15 @@ def main_geom(args, world, rank, local, dist):
     barrier(dist, ctx)
     elapsed = time.perf_counter() - t0
     elapsed_max = allreduce(dist, elapsed, _max_op(dist))
-    acc_all = allreduce(dist, float(acc), _sum_op(dist))
+    # replicas: independent copies (weak scaling); partitioned: one problem (strong scaling)
+    acc_all = float(acc) if comm is not None else allreduce(dist, float(acc), _sum_op(dist))
     value = acc_all / elapsed_max
     roof, cpu = None, None
-    if rank == 0:
+    if comm is not None:
         g.bench_iterations(min(sc.iters, 50))
+    if rank == 0:
+        if comm is None:
+            g.bench_iterations(min(sc.iters, 50))
         stats = {k: g.kernel_stats(k) for k in ("z", "rhs", "solve", "u", "aa")}
         k = max(stats, key=lambda kk: stats[kk]["avg_ms"])
         st = stats[k]
@@ -243,12 +264,14 @@ def main_geom(args, world, rank, local, dist):
         line = {
             "metric": "ADMM iters/sec + time-to-eps (primal+dual residual)", "value": round(value, 2),
             "unit": "ADMM iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed_max * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(elapsed_max * 1e3 / args.steps, 3), "higher_is_better": True,
+            "scaling": "strong" if comm is not None else "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (generated height-field quad mesh)",
             "config": {"workload": f"{desc}, ALM + Anderson m={sc.aa_m}, {sc.iters} accepted iterations per solve "
                                    f"(BASELINE configs[{2 if args.config == 'c3' else 4}])",
                        "points": sc.n_points, "hard_cols": sc.hard_cols(), "anderson_m": sc.aa_m,
-                       "parallelism": f"replicas{world}", "global_solve": "supernodal direct",
+                       "parallelism": (f"mesh-partitioned{world} ({part})" if comm is not None else f"replicas{world}"),
+                       "global_solve": "supernodal direct",
                        "nnz_factor": rt0.nnz_factor, "setup_ms": round(setup_ms, 1),
                        "factor_ms": round(rt0.factor_ms, 1)},
             "accepted_iters": int(acc_all), "x_updates": int(xupd),
@@ -257,6 +280,8 @@ def main_geom(args, world, rank, local, dist):
         }
         print(json.dumps(line))
     g.close()
+    if comm is not None:
+        comm.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
@@ -301,17 +326,7 @@ def main():
 
     ctx = capi.Context(0 if args.same_device else local)
     sc, desc = elastic_scene(args)
-    part = args.partition if args.partition != "auto" else ("rccl" if world > 1 else "none")
-    comm = None
-    if part == "rccl":
-        try:
-            comm = pkg.dist.rccl_comm(ctx, rank, world)
-        except Exception as e:   # transport only: the compute stays on the GPUs either way
-            print(f"[bench] RCCL communicator failed ({e}); using the host-staged transport", file=sys.stderr)
-            part = "host (rccl init failed)"
-            comm = pkg.dist.host_comm(rank, world)
-    elif part == "host":
-        comm = pkg.dist.host_comm(rank, world)
+    comm, part = make_comm(pkg, ctx, args, world, rank)
     solver = capi.solver_from_scene(ctx, sc, comm)
     t0 = time.time()
     solver.initialize(capi.settings_from_scene(sc))
