@@ -60,25 +60,36 @@ struct BvhBuilder {
     std::vector<double> cen;
     std::vector<BvhNode>* nodes;
     std::vector<BvhTri>* tris;
+    static float down(double v) {   // largest float <= v
+        float f = (float)v;
+        if ((double)f > v) f = std::nextafter(f, -INFINITY);
+        return f;
+    }
+    static float up(double v) {     // smallest float >= v
+        float f = (float)v;
+        if ((double)f < v) f = std::nextafter(f, INFINITY);
+        return f;
+    }
     int build(int b, int e) {
         BvhNode nd{};
-        for (int d = 0; d < 3; ++d) { nd.lo[d] = DBL_MAX; nd.hi[d] = -DBL_MAX; }
+        double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
         double clo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, chi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
         for (int i = b; i < e; ++i) {
             const int t = ids[i];
             for (int a = 0; a < 3; ++a)
                 for (int d = 0; d < 3; ++d) {
                     const double v = V[3 * (size_t)F[3 * (size_t)t + a] + d];
-                    nd.lo[d] = std::min(nd.lo[d], v); nd.hi[d] = std::max(nd.hi[d], v);
+                    lo[d] = std::min(lo[d], v); hi[d] = std::max(hi[d], v);
                 }
             for (int d = 0; d < 3; ++d) { clo[d] = std::min(clo[d], cen[3 * (size_t)t + d]); chi[d] = std::max(chi[d], cen[3 * (size_t)t + d]); }
         }
+        for (int d = 0; d < 3; ++d) { nd.lo[d] = down(lo[d]); nd.hi[d] = up(hi[d]); }
         const int me = (int)nodes->size();
+        if (me >= (1 << 29)) throw Error(ERR_ARG, "add_ref_surface: too many BVH nodes");
         nodes->push_back(nd);
         if (e - b <= 4) {
             (*nodes)[me].a = (int)tris->size();
-            (*nodes)[me].b = -(e - b);
-            (*nodes)[me].skip = me + 1;
+            (*nodes)[me].sn = (unsigned)(me + 1) | ((unsigned)(e - b) << 29);
             for (int i = b; i < e; ++i) {
                 BvhTri tr;
                 for (int a = 0; a < 3; ++a)
@@ -95,8 +106,7 @@ struct BvhBuilder {
         build(b, mid);
         const int r = build(mid, e);
         (*nodes)[me].a = r;
-        (*nodes)[me].b = 0;
-        (*nodes)[me].skip = (int)nodes->size();
+        (*nodes)[me].sn = (unsigned)nodes->size();
         return me;
     }
 };

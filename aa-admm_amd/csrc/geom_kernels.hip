@@ -229,9 +229,10 @@ __device__ __forceinline__ void closest_on_tri(const double* t, double px, doubl
 }
 
 __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py, double pz) {
-    const double tx = px < nd.lo[0] ? nd.lo[0] - px : (px > nd.hi[0] ? px - nd.hi[0] : 0.0);
-    const double ty = py < nd.lo[1] ? nd.lo[1] - py : (py > nd.hi[1] ? py - nd.hi[1] : 0.0);
-    const double tz = pz < nd.lo[2] ? nd.lo[2] - pz : (pz > nd.hi[2] ? pz - nd.hi[2] : 0.0);
+    const double l0 = nd.lo[0], l1 = nd.lo[1], l2 = nd.lo[2], h0 = nd.hi[0], h1 = nd.hi[1], h2 = nd.hi[2];
+    const double tx = px < l0 ? l0 - px : (px > h0 ? px - h0 : 0.0);
+    const double ty = py < l1 ? l1 - py : (py > h1 ? py - h1 : 0.0);
+    const double tz = pz < l2 ? l2 - pz : (pz > h2 ? pz - h2 : 0.0);
     return tx * tx + ty * ty + tz * tz;
 }
 
@@ -259,8 +260,8 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         int i = 0;
         for (;;) {
             const BvhNode& nd = S.nodes[i];
-            if (nd.b < 0) {
-                for (int t = nd.a; t < nd.a - nd.b; ++t) test_tri(t);
+            if (bvh_count(nd) > 0) {
+                for (int t = nd.a; t < nd.a + bvh_count(nd); ++t) test_tri(t);
                 break;
             }
             const double dl = box_d2(S.nodes[i + 1], px, py, pz), dr = box_d2(S.nodes[nd.a], px, py, pz);
@@ -272,15 +273,16 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
     while (i < S.n_nodes) {
         const BvhNode nd = S.nodes[i];
         if (box_d2(nd, px, py, pz) < best) {
-            if (nd.b < 0) {
-                for (int t = nd.a; t < nd.a - nd.b; ++t)
+            const int nc = bvh_count(nd);
+            if (nc > 0) {
+                for (int t = nd.a; t < nd.a + nc; ++t)
                     if (t != seed) test_tri(t);
-                i = nd.skip;
+                i = bvh_skip(nd);
             } else {
                 i = i + 1;
             }
         } else {
-            i = nd.skip;
+            i = bvh_skip(nd);
         }
     }
     return best_t;

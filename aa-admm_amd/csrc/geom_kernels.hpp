@@ -16,10 +16,16 @@ constexpr int kGeoMaxK = 8;   // largest plane supported on device (face valence
 // the left child of node i is i+1; `a` is the right child (inner) or the first triangle
 // (leaf), `b` = -(triangle count) for a leaf, 0 otherwise; `skip` is the first node after
 // this node's subtree (the escape link of a stackless traversal).
+// 32-B BVH node: box in fp32 rounded OUTWARD (never prunes a box the fp64 box would keep, so
+// the closest point is unchanged), a = right child (inner) or first triangle (leaf),
+// sn = escape link (node after the subtree, low 29 bits) | leaf triangle count << 29 (0 = inner)
 struct BvhNode {
-    double lo[3], hi[3];
-    int a, b, skip, pad;
+    float lo[3], hi[3];
+    int a;
+    unsigned sn;
 };
+__host__ __device__ inline int bvh_skip(const BvhNode& n) { return (int)(n.sn & 0x1fffffffu); }
+__host__ __device__ inline int bvh_count(const BvhNode& n) { return (int)(n.sn >> 29); }
 struct BvhTri { double v[9]; };   // triangle corners, stored in leaf order
 struct SurfDev {
     const BvhNode* nodes;
