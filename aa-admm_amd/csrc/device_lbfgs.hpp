@@ -41,7 +41,9 @@ __device__ __forceinline__ double hyper_psi_grad(int mat, double mu, double lamb
             const double finvt = cof[i] * invJ;
             g[i] = mu * (x[i] - finvt) + lambda * lJ * finvt;
         }
-        const double lI3 = log(J * J);
+        // log I3 = log J^2 = 2 log J for J > 0 (one log fewer per evaluation; equal to rounding);
+        // an inverted element keeps the reference's log(J^2) (finite) next to its NaN gradient
+        const double lI3 = J > 0.0 ? 2.0 * lJ : log(J * J);
         return 0.5 * mu * (I1 - lI3 - 3.0) + 0.125 * lambda * lI3 * lI3;
     }
     // StVK
@@ -88,24 +90,38 @@ __device__ __forceinline__ double d9(const double* a, const double* b) {
     return s;
 }
 
-// x: in = v (start point), out = prox. Returns iterations; sets *fail on a collapsed line search.
-// The history is a shift register (slot 0 = newest) instead of mcloptlib's ring buffer: every
-// index is a compile-time constant, so s, y stay in registers (the ring buffer's dynamic
-// indices put 864 B per thread in scratch). The two-loop recursion visits the pairs in the
-// same order (newest -> oldest, then back), so the arithmetic is the reference's.
-__device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, double k, double vol, const double* v,
-                                          double* x, int* fail) {
-    constexpr int M = 6;
-    double s[M][9], y[M][9], ys_h[M], alpha[M], g[9], gp[9], xp[9], drt[9];
-    double fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
-    double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
-    double fpast = fx;
-    if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return 1;
+// The L-BFGS of mcloptlib (LBFGS.hpp:205-305) as a resumable per-lane state machine, so a
+// persistent kernel can run one outer iteration per trip for whichever elements its lanes hold
+// (k_local_z_hq) and the plain kernel can run it to completion (hyper_prox). The history is a
+// shift register (slot 0 = newest) instead of mcloptlib's ring buffer: every index is a
+// compile-time constant, so s, y stay in registers (the ring buffer's dynamic indices put 864 B
+// per thread in scratch). The two-loop recursion visits the pairs in the same order (newest ->
+// oldest, then back), so the arithmetic is the reference's.
+struct HyperLbfgs {
+    static constexpr int M = 6;
+    double s[M][9], yv[M][9], ysh[M], g[9], drt[9];
+    double fx, fpast, step;
+    int k_it;
+
+    // x: in = v (start point). true: x already satisfies the gradient test (no iteration)
+    __device__ __forceinline__ bool start(int mat, double mu, double lambda, double k, double vol, const double* v,
+                                          double* x) {
+        fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
+        const double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
+        fpast = fx;
+        k_it = 1;
+        if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return true;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) drt[i] = -g[i];
-    double step = 1.0 / sqrt(d9(drt, drt));
-    int k_it = 1;
-    for (;;) {
+        for (int i = 0; i < 9; ++i) drt[i] = -g[i];
+        step = 1.0 / sqrt(d9(drt, drt));
+        return false;
+    }
+
+    // one outer iteration: Armijo line search, stopping tests, history push, two-loop direction.
+    // true when finished (converged, stalled, capped or a collapsed line search: *fail = 1)
+    __device__ __forceinline__ bool iterate(int mat, double mu, double lambda, double k, double vol, const double* v,
+                                            double* x, int* fail) {
+        double xp[9], gp[9], alpha[M];
 #pragma unroll
         for (int i = 0; i < 9; ++i) { xp[i] = x[i]; gp[i] = g[i]; }
         {
@@ -115,40 +131,38 @@ __device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, dou
                 for (int i = 0; i < 9; ++i) x[i] = xp[i] + step * drt[i];
                 fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
                 if (!(fx > fx_init + step * dg_test)) break;
-                if (step < 1e-20 || step > 1e20) { *fail = 1; return k_it; }
+                if (step < 1e-20 || step > 1e20) { *fail = 1; return true; }
                 step *= 0.5;
             }
         }
-        xnorm = sqrt(d9(x, x));
-        gnorm = sqrt(d9(g, g));
-        if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return k_it;
-        if (fabs(fpast - fx) < 1e-16) return k_it;
+        const double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
+        if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return true;
+        if (fabs(fpast - fx) < 1e-16) return true;
         fpast = fx;
-        if (k_it >= 100) return k_it;
-        // push (s, y) into slot 0
+        if (k_it >= 100) return true;
 #pragma unroll
-        for (int q = M - 1; q > 0; --q) {
-            ys_h[q] = ys_h[q - 1];
+        for (int q = M - 1; q > 0; --q) {   // push (s, y) into slot 0
+            ysh[q] = ysh[q - 1];
 #pragma unroll
-            for (int i = 0; i < 9; ++i) { s[q][i] = s[q - 1][i]; y[q][i] = y[q - 1][i]; }
+            for (int i = 0; i < 9; ++i) { s[q][i] = s[q - 1][i]; yv[q][i] = yv[q - 1][i]; }
         }
         double ys = 0, yy = 0;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
             const double si = x[i] - xp[i], yi = g[i] - gp[i];
-            s[0][i] = si; y[0][i] = yi;
+            s[0][i] = si; yv[0][i] = yi;
             ys += yi * si; yy += yi * yi;
         }
-        ys_h[0] = ys;
+        ysh[0] = ys;
 #pragma unroll
         for (int i = 0; i < 9; ++i) drt[i] = -g[i];
         const int bound = k_it < M ? k_it : M;
 #pragma unroll
         for (int q = 0; q < M; ++q) {
             if (q < bound) {
-                alpha[q] = d9(s[q], drt) / ys_h[q];
+                alpha[q] = d9(s[q], drt) / ysh[q];
 #pragma unroll
-                for (int t = 0; t < 9; ++t) drt[t] -= alpha[q] * y[q][t];
+                for (int t = 0; t < 9; ++t) drt[t] -= alpha[q] * yv[q][t];
             }
         }
 #pragma unroll
@@ -156,14 +170,24 @@ __device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, dou
 #pragma unroll
         for (int q = M - 1; q >= 0; --q) {
             if (q < bound) {
-                const double beta = d9(y[q], drt) / ys_h[q];
+                const double beta = d9(yv[q], drt) / ysh[q];
 #pragma unroll
                 for (int t = 0; t < 9; ++t) drt[t] += (alpha[q] - beta) * s[q][t];
             }
         }
         step = 1.0;
         ++k_it;
+        return false;
     }
+};
+
+// x: in = v (start point), out = prox. Returns iterations; sets *fail on a collapsed line search.
+__device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, double k, double vol, const double* v,
+                                          double* x, int* fail) {
+    HyperLbfgs L;
+    if (L.start(mat, mu, lambda, k, vol, v, x)) return 1;
+    while (!L.iterate(mat, mu, lambda, k, vol, v, x, fail)) {}
+    return L.k_it;
 }
 
 }  // namespace dev

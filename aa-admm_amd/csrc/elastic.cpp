@@ -380,6 +380,8 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     if (comm_) { red_gab_.alloc(2 * (size_t)nbg_); red_gab_.zero(s()); ga_ = red_gab_.p; gb_ = red_gab_.p + nbg_; }
     else { ga_ = pa_; gb_ = pb_; }
     ctrl_.alloc(1);
+    lzq_.alloc(1);
+    if (const char* q = std::getenv("AA_LOCAL_QUEUE")) use_queue_ = q[0] != '0';
     hist_cap_ = std::max(1, st_.admm_iters);
     hist_prim_.alloc(hist_cap_); hist_comb_.alloc(hist_cap_); hist_rej_.alloc(hist_cap_);
     if (accel) {
@@ -492,7 +494,8 @@ void ElasticSolver::local_z_all(const double* xfull, const double* u, double* z,
     const bool timed = mode == LZ_NORMAL && red;
     if (timed) ev_begin("local_z");
     for (auto& g : groups_) {
-        launch_local_z(g.d, xfull, u, z, y, nf_, st_.variant, mode, ctrl_.p, red ? pa_ : nullptr, off, s());
+        launch_local_z(g.d, xfull, u, z, y, nf_, st_.variant, mode, ctrl_.p, red ? pa_ : nullptr, off, s(),
+                       use_queue_ ? lzq_.p : nullptr);
         off += blocks_for(g.d.count);
     }
     if (timed) ev_end("local_z");

@@ -90,6 +90,8 @@ private:
     double *pa_ = nullptr, *pb_ = nullptr, *ga_ = nullptr, *gb_ = nullptr, *aag_ = nullptr;
     int nbg_ = 0;
     DevBuf<Ctrl> ctrl_;
+    DevBuf<int> lzq_;          // work-queue counter of the hyperelastic local step
+    bool use_queue_ = true;
     DevBuf<double> hist_prim_, hist_comb_;
     DevBuf<int> hist_rej_;
     int red_blocks_ = 0, aa_blocks_ = 0, hist_cap_ = 0;

@@ -5,6 +5,9 @@
 // resident), deterministic block partial sums for every residual norm, and a one-block
 // control kernel that makes the reference's data-dependent decisions (Anderson reject,
 // comb < eps break) on the device so the whole ADMM loop is enqueued without host syncs.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 #include "device_lbfgs.hpp"
 #include "device_prox.hpp"
@@ -157,6 +160,74 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
         const double s = block_sum(part, sm);
         if (threadIdx.x == 0) red[red_off + blockIdx.x] = s;
     }
+}
+
+// NeoHookean / StVK local step without residual partials (the Z variant's update_z calls), as a
+// persistent work queue: the per-element L-BFGS takes 1..100 iterations, so with one element per
+// lane a wave runs as long as its slowest lane. Here every lane that finishes its element (z and
+// the optional rhs slots written) takes the next one from a queue (one atomic per wave and
+// refill, ballot-aggregated) and lanes advance one outer L-BFGS iteration per trip. Each
+// element's arithmetic is unchanged, so the results are bit-identical to k_local_z.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double* __restrict__ xfull,
+                                                       const double* __restrict__ u, double* __restrict__ z,
+                                                       double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
+                                                       int* __restrict__ queue, int refill) {
+    if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
+    constexpr int D = 3 * (NV - 1);
+    const int lane = threadIdx.x & 63;
+    dev::HyperLbfgs L;
+    double v[D], x[D];
+    double vol = 0;
+    int e = -1, fail = 0;
+    bool active = false, exhausted = false;
+    auto finalize = [&]() {
+#pragma unroll
+        for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * g.count + e] = x[i];
+        if (y) {
+            double F[D], Cp[D], uu[D];
+            gather_F<NV>(g, e, xfull, nf, F, Cp);
+#pragma unroll
+            for (int i = 0; i < D; ++i) uu[i] = u ? u[g.zoff + (size_t)i * g.count + e] : 0.0;
+            write_slots<NV>(g, e, nf, g.w[e], x, Cp, uu, y);
+        }
+    };
+    for (;;) {
+        const bool need = !active && !exhausted;
+        const unsigned long long mask = __ballot(need);
+        if (!__any(active || need)) break;
+        // refill only once enough lanes are idle (the init path then runs for many lanes at once)
+        if (mask && (__popcll(mask) >= refill || !__any(active))) {
+            const int leader = __ffsll((long long)mask) - 1;
+            int b = 0;
+            if (lane == leader) b = atomicAdd(queue, __popcll(mask));
+            b = __shfl(b, leader, 64);
+            if (need) {
+                const int my = b + __popcll(mask & ((1ull << lane) - 1ull));
+                if (my >= g.count) {
+                    exhausted = true;
+                } else {
+                    e = my;
+                    double F[D], Cp[D];
+                    gather_F<NV>(g, e, xfull, nf, F, Cp);
+                    const double w = g.w[e];
+#pragma unroll
+                    for (int i = 0; i < D; ++i) {
+                        v[i] = F[i] + (u ? u[g.zoff + (size_t)i * g.count + e] : 0.0) / w;
+                        x[i] = v[i];
+                    }
+                    vol = g.vol[e];
+                    if (L.start(g.mat, g.mu, g.lambda, g.k, vol, v, x)) finalize();
+                    else active = true;
+                }
+            }
+        }
+        if (active && L.iterate(g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail)) {
+            finalize();
+            active = false;
+        }
+    }
+    if (fail && ctrl) ctrl->fail = 1;
 }
 
 // r = w(P x - z): prim2 += |r|^2, dual2 += |w P (x - x_last)|^2, u += r
@@ -776,9 +847,26 @@ inline int grid_for(long long n) { long long b = (n + kBlock - 1) / kBlock; retu
 
 // ============================================================================ launchers
 void launch_local_z(const GroupDev& g, const double* xfull, const double* u, double* z, double* y, int nf,
-                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s) {
+                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s, int* queue) {
     if (g.count == 0) return;
     const int nb = blocks_for(g.count);
+    if (g.kind == 0 && g.mat != 0 && !red && queue) {   // hyperelastic, no partials: work queue
+        static int resident = 0;
+        if (!resident) {
+            int dev = 0, cus = 0, per = 0;
+            AA_HIP(hipGetDevice(&dev));
+            AA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_local_z_hq<4>, kBlock, 0));
+            resident = std::max(1, cus * std::max(1, per));
+        }
+        AA_HIP(hipMemsetAsync(queue, 0, sizeof(int), s));
+        static int refill = -1;
+        if (refill < 0) { const char* r = std::getenv("AA_LQ_REFILL"); refill = r ? std::atoi(r) : 60; }
+        hipLaunchKernelGGL(k_local_z_hq<4>, dim3(std::min(nb, resident)), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
+                           ctrl, queue, refill);
+        AA_CHECK_LAUNCH();
+        return;
+    }
     if (g.kind == 1) hipLaunchKernelGGL((k_local_z<3, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
     else if (g.mat == 0) hipLaunchKernelGGL((k_local_z<4, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
     else hipLaunchKernelGGL((k_local_z<4, 1>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);

@@ -56,8 +56,9 @@ struct ElasticLaunch;  // fwd
 enum LocalMode { LZ_NORMAL = 0, LZ_REDO = 1, LZ_INIT = 2 };
 
 // z = prox(P x + u/w); prim partials; optional y = w(w z + c - u). gate: !done (and reject for REDO)
+// queue: one device int; hyperelastic groups without partials then run as a persistent work queue
 void launch_local_z(const GroupDev& g, const double* xfull, const double* u, double* z, double* y, int nf,
-                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s);
+                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s, int* queue = nullptr);
 // r = w(P x - z); prim2/dual2 partials; u += r (UX variant update_u fused with the residual)
 void launch_resid_update_u(const GroupDev& g, const double* xfull, const double* xlast, const double* z, double* u,
                            int nf, Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s);
