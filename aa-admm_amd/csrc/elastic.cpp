@@ -345,18 +345,37 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
         red_blocks_ += blocks_for(cnt);
     }
     Z_ = zoff;
-    Yslots_ = yrow;
     if (P == 1) { nbg_ = red_blocks_; zmax = Z_; }
     {
-        std::vector<int> ptr(nf_ + 1, 0), row;
+        // vertex slots in node order: the element kernels scatter each vertex contribution to its
+        // node's run (spos), the rhs kernel streams every node's run contiguously
+        std::vector<int> ptr(nf_ + 1, 0);
+        std::vector<std::vector<int>> spos(groups_.size());
+        std::vector<long long> gfirst(groups_.size());
+        for (size_t gi = 0; gi < groups_.size(); ++gi) {
+            spos[gi].assign((size_t)groups_[gi].d.nv * groups_[gi].d.count, -1);
+            gfirst[gi] = groups_[gi].d.yrow;
+        }
+        long long pos = 0;
         for (int q = 0; q < nf_; ++q) {
             auto& r = dtr[q];
             std::sort(r.begin(), r.end());
-            if (!r.empty() && r.back() > 0x7fffffffLL) throw Error(ERR_ARG, "initialize: too many element vertices");
-            for (long long e : r) row.push_back((int)e);
-            ptr[q + 1] = (int)row.size();
+            for (long long key : r) {   // key = group's first slot + t * nv + a
+                const size_t gi = (size_t)(std::upper_bound(gfirst.begin(), gfirst.end(), key) - gfirst.begin()) - 1;
+                const long long local = key - gfirst[gi];
+                const int nv = groups_[gi].d.nv, cnt = groups_[gi].d.count;
+                spos[gi][(size_t)(local % nv) * cnt + (size_t)(local / nv)] = (int)pos++;
+            }
+            if (pos > 0x7fffffffLL) throw Error(ERR_ARG, "initialize: too many element vertices");
+            ptr[q + 1] = (int)pos;
+            std::vector<long long>().swap(r);
         }
-        dt_ptr_.upload(ptr, s()); dt_row_.upload(row, s());
+        dt_ptr_.upload(ptr, s());
+        for (size_t gi = 0; gi < groups_.size(); ++gi) {
+            groups_[gi].spos.upload(spos[gi], s());
+            groups_[gi].d.spos = groups_[gi].spos.p;
+        }
+        Yslots_ = pos;
     }
     // ---- state and work buffers
     std::vector<double> xs(3 * (size_t)n), ms(n);
@@ -413,19 +432,19 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     double lz = 0, rs = 0;
     for (auto& g : groups_) {
         const double per = 4.0 * g.d.nv + 8.0 * g.d.ncol * g.d.nv + 8.0;
-        lz += g.d.count * (per + 2 * 8.0 * g.d.dim + 24.0 * g.d.nv);   // u in, z out, vertex slots out
+        lz += g.d.count * (per + 2 * 8.0 * g.d.dim + 28.0 * g.d.nv);   // u in, z out, slot positions + slots out
         rs += g.d.count * (per + 3 * 8.0 * g.d.dim);
     }
     kstats_["local_z"].bytes = lz + 24.0 * n;
     kstats_["resid"].bytes = rs + 48.0 * n;
     kstats_["solve"].bytes = solver_.bytes_per_solve();
-    kstats_["rhs"].bytes = 28.0 * (double)dt_row_.n + 48.0 * nf_;   // slot index + 3 doubles per slot; Mxbar, b
+    kstats_["rhs"].bytes = 24.0 * (double)Yslots_ + 4.0 * nf_ + 48.0 * nf_;   // 3 doubles per slot; ptr, Mxbar, b
     // Z variant: u = W^-1 grad E(z) and the vertex slots (reads idx, G, w, z; writes u, slots),
     // prim (reads idx, G, w, z, u; writes block partials)
     double gy = 0, pr = 0;
     for (auto& g : groups_) {
         const double per = 4.0 * g.d.nv + 8.0 * g.d.ncol * g.d.nv + 8.0;
-        gy += g.d.count * (per + 8.0 * 2 * g.d.dim + 24.0 * g.d.nv);
+        gy += g.d.count * (per + 8.0 * 2 * g.d.dim + 28.0 * g.d.nv);
         pr += g.d.count * (per + 8.0 * 2 * g.d.dim);
     }
     kstats_["grad"].bytes = gy + 24.0 * n;
@@ -521,7 +540,7 @@ void ElasticSolver::prologue() {
     const long long nx = 3LL * nf_;
     if (st_.variant == AA_VARIANT_UX) {
         local_z_all(xfull_.p, u_.p, z_.p, y_.p, LZ_INIT, false);
-        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
+        launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
         solver_.solve(b_.p, xfull_.p, nullptr, 0, s());
         {
             int off = 0;
@@ -538,7 +557,7 @@ void ElasticSolver::prologue() {
         }
     } else {
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 2, 0, ctrl_.p, s());
-        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
+        launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
         solver_.solve(b_.p, xfull_.p, nullptr, 0, s());
         local_z_all(xfull_.p, u_.p, z_.p, nullptr, LZ_INIT, false);
         launch_copy(dz_.p, z_.p, Z_, nullptr, 0, s());
@@ -561,7 +580,7 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
         reduce_partials();
     }
     ev_begin("rhs");
-    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s(), xfull_.p, xlast_.p,
+    launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s(), xfull_.p, xlast_.p,
                ga_, nbg_);
     ev_end("rhs");
     ev_begin("solve");
@@ -601,7 +620,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
     for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, accel ? 1 : 0, 0, c, s());
     ev_end("grad");
     ev_begin("rhs");
-    launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+    launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
     ev_end("rhs");
     ev_begin("solve");
     solver_.solve(b_.p, xfull_.p, c, 0, s());
@@ -624,7 +643,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         launch_copy(z_.p, dz_.p, Z_, c, 1, s());
         launch_copy(aa_cur_.p, dz_.p, Z_, c, 1, s());   // accelerator.replace(curr_z)
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 0, 1, c, s());
-        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());
+        launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());
         solver_.solve(b_.p, xfull_.p, c, 1, s());
         prim_all(xfull_.p, z_.p, nullptr, 1);
         reduce_partials();
@@ -649,7 +668,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
         ev_begin("comb");
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, dz_.p, u_.p, y_.p, nf_, 2, 0, c, s());
-        launch_rhs(nf_, dt_ptr_.p, dt_row_.p, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
+        launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
         solver_.solve(b_.p, cxfull_.p, c, 0, s());
         local_z_all(cxfull_.p, u_.p, cz_.p, nullptr, LZ_NORMAL, false);
         prim_all(cxfull_.p, cz_.p, dz_.p, 0);

@@ -56,7 +56,7 @@ private:
         std::vector<double> vol, w;
     };
     struct DevGroup {
-        DevBuf<int> idx;
+        DevBuf<int> idx, spos;
         DevBuf<double> G, w, vol;
         GroupDev d{};
     };
@@ -80,7 +80,7 @@ private:
     // device
     std::vector<DevGroup> groups_;
     DirectSolver solver_;
-    DevBuf<int> dt_ptr_, dt_row_;
+    DevBuf<int> dt_ptr_;
     DevBuf<double> xs_, vs_, mass_, xfull_, xlast_, xbar_, Mxbar_, b_, cxfull_;
     DevBuf<double> z_, u_, y_, du_, dz_, dx_, lastz_, cz_;
     DevBuf<double> aa_cur_, aa_dF_, aa_dG_, aa_red_, aa_red_g_;

@@ -94,8 +94,8 @@ __device__ __forceinline__ void gather_P(const GroupDev& g, int e, const double*
 
 // Per-vertex right-hand-side contributions of one element: with y_c = w (w z_c - w Cp_c - u_c)
 // (the element's rows of W z + C - u, Solver.cpp:105/175), vertex a of a free node receives
-// f_a = sum_c G[c][a] y_c, written to slot (yrow + e*NV + a); the rhs kernel then only sums
-// the slots of each node (no coefficient array, no per-column gathers).
+// f_a = sum_c G[c][a] y_c, scattered to its node's run of slots (spos, node order); the rhs
+// kernel then streams each node's run (no coefficient array, no gathers).
 template <int NV>
 __device__ __forceinline__ void write_slots(const GroupDev& g, int e, int nf, double w, const double* zz,
                                             const double* Cp, const double* uu, double* __restrict__ y) {
@@ -105,14 +105,15 @@ __device__ __forceinline__ void write_slots(const GroupDev& g, int e, int nf, do
     for (int i = 0; i < 3 * NC; ++i) yc[i] = w * (w * zz[i] - w * Cp[i] - uu[i]);
 #pragma unroll
     for (int a = 0; a < NV; ++a) {
-        if (g.idx[(size_t)a * g.count + e] >= nf) continue;   // pinned: no rhs row
+        const int pos = g.spos[(size_t)a * g.count + e];
+        if (pos < 0) continue;   // pinned: no rhs row
         double f0 = 0, f1 = 0, f2 = 0;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
             f0 += gc * yc[3 * c]; f1 += gc * yc[3 * c + 1]; f2 += gc * yc[3 * c + 2];
         }
-        double* o = y + 3 * (size_t)(g.yrow + (long long)e * NV + a);
+        double* o = y + 3 * (size_t)pos;
         o[0] = f0; o[1] = f1; o[2] = f2;
     }
 }
@@ -375,12 +376,10 @@ __global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ 
             const size_t r = 3 * (size_t)row[k];
             s0 += v * y[r]; s1 += v * y[r + 1]; s2 += v * y[r + 2];
         }
-    } else {   // vertex slots (write_slots): plain sums
+    } else {   // vertex slots (write_slots): the node's run, contiguous
+        const double* q = y + 3 * (size_t)ptr[i];
 #pragma unroll 4
-        for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
-            const size_t r = 3 * (size_t)row[k];
-            s0 += y[r]; s1 += y[r + 1]; s2 += y[r + 2];
-        }
+        for (int k = ptr[i]; k < ptr[i + 1]; ++k, q += 3) { s0 += q[0]; s1 += q[1]; s2 += q[2]; }
     }
     b[3 * (size_t)i + 0] = Mxbar[3 * (size_t)i + 0] + pdt2 * s0;
     b[3 * (size_t)i + 1] = Mxbar[3 * (size_t)i + 1] + pdt2 * s1;

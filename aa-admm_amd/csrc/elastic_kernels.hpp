@@ -16,6 +16,7 @@ struct GroupDev {
     long long zoff;      // z/u offset: component c of element e at zoff + c*count + e
     long long yrow;      // first vertex slot of this group in the slot array y (slot e*nv + a, 3 doubles)
     const int* idx;      // [nv][count] internal node ids
+    const int* spos;     // [nv][count] position of the vertex's rhs slot (node order), -1 = pinned
     const double* G;     // [(c*nv + a)][count]  F[:,c] = sum_a G[c][a] x_a
     const double* w;     // [count] ADMM weights sqrt(k*vol)
     const double* vol;   // [count]
