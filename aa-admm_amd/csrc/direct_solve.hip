@@ -60,6 +60,19 @@ __device__ __forceinline__ void front_row(const Task& t, int q, const long long*
     }
 }
 
+// front row q of a supernode given by its fields (the split-K tiles assemble their own slices)
+__device__ __forceinline__ void front_row_at(int beg, int p, int ell_w, long long ell_off, int q,
+                                             const long long* __restrict__ ell, const double* __restrict__ B,
+                                             const double* __restrict__ U, double& a0, double& a1, double& a2) {
+    a0 = a1 = a2 = 0;
+    if (q < p) { const size_t o = 3 * (size_t)(beg + q); a0 = B[o]; a1 = B[o + 1]; a2 = B[o + 2]; }
+    const long long* e = ell + ell_off + (size_t)q * ell_w;
+    for (int k = 0; k < ell_w; ++k) {
+        const long long o = e[k];
+        if (o >= 0) { a0 += U[o]; a1 += U[o + 1]; a2 += U[o + 2]; }
+    }
+}
+
 // assembly of the front vectors of wave-mode supernodes into Fg
 __global__ __launch_bounds__(256) void k_asm(const Task* __restrict__ tasks, int first, const long long* __restrict__ ell,
                                              const double* __restrict__ B, const double* __restrict__ U,
@@ -268,16 +281,18 @@ using FRed = DirectSolver::FRed;
 constexpr int kFwdTileCols = 128;
 
 __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tiles, int first, const double* __restrict__ Gc,
-                                                  const double* __restrict__ Fg, double* __restrict__ part,
-                                                  const FRed* __restrict__ reds, int* __restrict__ cnt,
-                                                  double* __restrict__ Y, double* __restrict__ U,
+                                                  const long long* __restrict__ ell, const double* __restrict__ B,
+                                                  double* __restrict__ part, const FRed* __restrict__ reds,
+                                                  int* __restrict__ cnt, double* __restrict__ Y, double* __restrict__ U,
                                                   const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     __shared__ double f[3 * kFwdTileCols];
     __shared__ double red[3][3 * 64];
     const FTile t = tiles[first + blockIdx.x];
     const int tid = threadIdx.x;
-    for (int i = tid; i < 3 * t.nc; i += 256) f[i] = Fg[t.foff + 3 * (size_t)t.c0 + i];
+    // this tile's slice of the front f_P = b_P + extend-add of the children's update vectors
+    for (int i = tid; i < t.nc; i += 256)
+        front_row_at(t.beg, t.p, t.ell_w, t.ell_off, t.c0 + i, ell, B, U, f[3 * i], f[3 * i + 1], f[3 * i + 2]);
     __syncthreads();
     const int lane = tid & 63, w = tid >> 6;
     const int r = t.r0 + lane;
@@ -313,9 +328,10 @@ __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tile
             const size_t yo = 3 * (size_t)(rd.beg + rr);
             Y[yo] = b0; Y[yo + 1] = b1; Y[yo + 2] = b2;
         } else {
-            const double* fb = Fg + rd.foff + 3 * (size_t)rr;
+            double f0, f1, f2;
+            front_row_at(rd.beg, rd.p, rd.ell_w, rd.ell_off, rr, ell, B, U, f0, f1, f2);
             double* u = U + rd.uoff + 3 * (size_t)(rr - rd.p);
-            u[0] = fb[0] - b0; u[1] = fb[1] - b1; u[2] = fb[2] - b2;
+            u[0] = f0 - b0; u[1] = f1 - b1; u[2] = f2 - b2;
         }
     }
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -726,12 +742,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         (void)bwave;
         L.bblock = br > 128 ? 256 : (br > 64 ? 128 : 64);
         L.asm_first = (int)tasks.size();
-        for (int sn : l) {
-            if (p[sn] <= kWaveP) continue;
-            foff[sn] = fo;
-            fo += 3LL * (p[sn] + nb[sn]);
-            for (int r0 = 0; r0 < p[sn] + nb[sn]; r0 += 256) tasks.push_back(mk(sn, r0, std::min(256, p[sn] + nb[sn] - r0), 1));
-        }
+        // (the split-K tiles assemble their own front slices: no assembly tasks)
         L.asm_count = (int)tasks.size() - L.asm_first;
         L.fwd_first = (int)tasks.size();
         for (int sn : l) {
@@ -752,13 +763,13 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             for (int r0 = 0; r0 < R; r0 += 64) {
                 FRed rd{};
                 rd.beg = beg[sn]; rd.p = p[sn]; rd.r0 = r0; rd.nr = std::min(64, R - r0);
-                rd.uoff = uoff[sn]; rd.foff = foff[sn]; rd.poff = poff;
+                rd.uoff = uoff[sn]; rd.ell_off = ell_off[sn]; rd.ell_w = ell_w[sn]; rd.poff = poff;
                 for (int c0 = 0; c0 < p[sn]; c0 += kFwdTileCols) {
                     if (r0 + 63 < c0) break;
                     FTile ft{};
                     ft.beg = beg[sn]; ft.p = p[sn]; ft.R = R; ft.c0 = c0; ft.r0 = r0;
                     ft.nc = std::min(kFwdTileCols, p[sn] - c0);
-                    ft.goff = goff[sn]; ft.foff = foff[sn]; ft.poff = poff;
+                    ft.goff = goff[sn]; ft.ell_off = ell_off[sn]; ft.ell_w = ell_w[sn]; ft.poff = poff;
                     ft.rid = (int)freds.size();
                     poff += 3 * 64;
                     ftiles.push_back(ft);
@@ -862,8 +873,8 @@ void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject
 #define FWD(BL) hipLaunchKernelGGL(k_fwd<BL>, dim3(L.fwd_count), dim3(BL), L.lds_fwd, s, T, L.fwd_first, Gr_.p, Gc_.p, ell_.p, b, Y_.p, U_.p, Fg_.p, ctrl, gate_reject)
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
         if (L.ft_count) {
-            hipLaunchKernelGGL(k_fwd_tile, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, Fg_.p, bpart_.p,
-                               freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
+            hipLaunchKernelGGL(k_fwd_tile, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b,
+                               bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
         }
 #undef FWD
     }

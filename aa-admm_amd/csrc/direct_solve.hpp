@@ -69,8 +69,8 @@ public:
     struct BRed { int beg, c0, nc, nt; long long poff; };
     // split-K forward of large supernodes: tile (64 rows from r0, nc columns from c0) and the
     // per-row-block reduction of its nt partials
-    struct FTile { int beg, p, R, c0, r0, nc, rid, pad; long long goff, foff, poff; };
-    struct FRed { int beg, p, r0, nr, nt, pad; long long uoff, foff, poff; };
+    struct FTile { int beg, p, R, c0, r0, nc, rid, ell_w; long long goff, ell_off, poff; };
+    struct FRed { int beg, p, r0, nr, nt, ell_w; long long uoff, ell_off, poff; };
 
 private:
     struct Level {
