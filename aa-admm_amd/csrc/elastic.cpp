@@ -653,8 +653,11 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         const int m = st_.anderson_m;
         launch_copy(dx_.p, xfull_.p, nx, c, 0, s());
         launch_copy(du_.p, u_.p, Z_, c, 0, s());
+        // default_z = update_z(curr_x, curr_u) (Solver.cpp:196-199); the same pass writes the
+        // rhs slots of the combined-residual solve below, w (w default_z + C - curr_u)
+        // (Solver.cpp:220): curr_u is final for this iteration and the AA step does not touch it
         ev_begin("local_z");
-        local_z_all(xfull_.p, u_.p, dz_.p, nullptr, LZ_NORMAL, false);
+        local_z_all(xfull_.p, u_.p, dz_.p, y_.p, LZ_NORMAL, false);
         ev_end("local_z");
         Seg2 G{dz_.p, Z_, nullptr, 0};
         Seg2 out{z_.p, Z_, nullptr, 0};
@@ -667,7 +670,6 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         ev_end("aa");
         // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
         ev_begin("comb");
-        for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, dz_.p, u_.p, y_.p, nf_, 2, 0, c, s());
         launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
         solver_.solve(b_.p, cxfull_.p, c, 0, s());
         local_z_all(cxfull_.p, u_.p, cz_.p, nullptr, LZ_NORMAL, false);
