@@ -84,6 +84,27 @@ struct BvhBuilder {
             for (int d = 0; d < 3; ++d) { clo[d] = std::min(clo[d], cen[3 * (size_t)t + d]); chi[d] = std::max(chi[d], cen[3 * (size_t)t + d]); }
         }
         for (int d = 0; d < 3; ++d) { nd.lo[d] = down(lo[d]); nd.hi[d] = up(hi[d]); }
+        {   // slab: area-weighted mean normal of the subtree, range of n . v over its vertices
+            double N[3] = {0, 0, 0};
+            for (int i = b; i < e; ++i) {
+                const double* A = V + 3 * (size_t)F[3 * (size_t)ids[i]];
+                const double* Bv = V + 3 * (size_t)F[3 * (size_t)ids[i] + 1];
+                const double* C = V + 3 * (size_t)F[3 * (size_t)ids[i] + 2];
+                const double u[3] = {Bv[0] - A[0], Bv[1] - A[1], Bv[2] - A[2]}, w[3] = {C[0] - A[0], C[1] - A[1], C[2] - A[2]};
+                N[0] += u[1] * w[2] - u[2] * w[1]; N[1] += u[2] * w[0] - u[0] * w[2]; N[2] += u[0] * w[1] - u[1] * w[0];
+            }
+            const double l = std::sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+            for (int d = 0; d < 3; ++d) nd.nrm[d] = l > 0 ? (float)(N[d] / l) : 0.0f;
+            double dl = DBL_MAX, dh = -DBL_MAX;
+            for (int i = b; i < e; ++i)
+                for (int a = 0; a < 3; ++a) {
+                    const double* P = V + 3 * (size_t)F[3 * (size_t)ids[i] + a];
+                    const double dd = (double)nd.nrm[0] * P[0] + (double)nd.nrm[1] * P[1] + (double)nd.nrm[2] * P[2];
+                    dl = std::min(dl, dd); dh = std::max(dh, dd);
+                }
+            if (l > 0) { nd.dlo = down(dl); nd.dhi = up(dh); }
+            else { nd.dlo = -FLT_MAX; nd.dhi = FLT_MAX; }   // degenerate patch: no slab bound
+        }
         const int me = (int)nodes->size();
         if (me >= (1 << 29)) throw Error(ERR_ARG, "add_ref_surface: too many BVH nodes");
         nodes->push_back(nd);

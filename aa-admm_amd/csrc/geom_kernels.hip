@@ -233,7 +233,13 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
     const double tx = px < l0 ? l0 - px : (px > h0 ? px - h0 : 0.0);
     const double ty = py < l1 ? l1 - py : (py > h1 ? py - h1 : 0.0);
     const double tz = pz < l2 ? l2 - pz : (pz > h2 ? pz - h2 : 0.0);
-    return tx * tx + ty * ty + tz * tz;
+    const double b = tx * tx + ty * ty + tz * tz;
+    // slab lower bound |n.p - [dlo, dhi]| (n unit to fp32 accuracy: shrunk by 1e-6 to stay below)
+    const double dn = (double)nd.nrm[0] * px + (double)nd.nrm[1] * py + (double)nd.nrm[2] * pz;
+    const double lo = nd.dlo, hi = nd.dhi;
+    const double t = dn < lo ? lo - dn : (dn > hi ? dn - hi : 0.0);
+    const double sl = t * t * (1.0 - 1e-6);
+    return b > sl ? b : sl;
 }
 
 // exact closest point on the surface. Stackless depth-first traversal over escape links
@@ -254,9 +260,10 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         const double d2 = (px - qx) * (px - qx) + (py - qy) * (py - qy) + (pz - qz) * (pz - qz);
         if (d2 < best) { best = d2; best_t = t; cx = qx; cy = qy; cz = qz; }
     };
-    if (warm >= 0 && warm < S.n_tris) {
-        test_tri(warm);
-    } else {   // cold start: greedy descent
+    if (warm >= 0 && warm < S.n_tris) test_tri(warm);
+    {   // greedy descent to the nearest-box leaf: a tight bound even when the point slid far
+        // from its previous triangle (the warm bound alone then lets the traversal open every
+        // box within that distance)
         int i = 0;
         for (;;) {
             const BvhNode& nd = S.nodes[i];

@@ -16,13 +16,17 @@ constexpr int kGeoMaxK = 8;   // largest plane supported on device (face valence
 // the left child of node i is i+1; `a` is the right child (inner) or the first triangle
 // (leaf), `b` = -(triangle count) for a leaf, 0 otherwise; `skip` is the first node after
 // this node's subtree (the escape link of a stackless traversal).
-// 32-B BVH node: box in fp32 rounded OUTWARD (never prunes a box the fp64 box would keep, so
-// the closest point is unchanged), a = right child (inner) or first triangle (leaf),
-// sn = escape link (node after the subtree, low 29 bits) | leaf triangle count << 29 (0 = inner)
+// 64-B BVH node: box in fp32 rounded OUTWARD (never prunes a box the fp64 box would keep),
+// a = right child (inner) or first triangle (leaf), sn = escape link (node after the subtree,
+// low 29 bits) | leaf triangle count << 29 (0 = inner), and a slab: the subtree's mean unit
+// normal n and the range [dlo, dhi] of n . v over its vertices (rounded outward). The slab
+// bounds the distance to every triangle of the subtree from below like the box does, and is
+// far tighter for sloped, thin patches seen from afar (a point well off the surface).
 struct BvhNode {
     float lo[3], hi[3];
     int a;
     unsigned sn;
+    float nrm[3], dlo, dhi, pad[3];
 };
 __host__ __device__ inline int bvh_skip(const BvhNode& n) { return (int)(n.sn & 0x1fffffffu); }
 __host__ __device__ inline int bvh_count(const BvhNode& n) { return (int)(n.sn >> 29); }
