@@ -127,7 +127,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
         const double* F = Fg + t.foff;
         for (int rr = w; rr < t.nr; rr += BLOCK / 64) {
             const int r = t.r0 + rr;
-            const double* row = Gr + t.goff + (size_t)r * p;
+            const double* row = Gr + t.goff + (size_t)r * t.ldr;
             const int cmax = r < p ? r + 1 : p;
             double a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll 4
@@ -173,10 +173,11 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
         if (tid >= t.nr) return;
         const int j = t.r0 + tid;
         const double* G = Gr + t.goff + j;
+        const int ld = t.ldr;
         double a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll 8
         for (int r = j; r < R; ++r) {
-            const double g = G[(size_t)r * p];
+            const double g = G[(size_t)r * ld];
             a0 += g * v[3 * r]; a1 += g * v[3 * r + 1]; a2 += g * v[3 * r + 2];
         }
         const size_t o = 3 * (size_t)(t.beg + j);
@@ -207,11 +208,12 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
     }
 }
 
-// Backward sweep of the large supernodes (R > kWaveR) as a split-K GEMV: tile = 64 columns
-// (lanes) x kBwdTileRows rows (4 waves x 32 rows) of the row-major G, the tile's slice of
-// [y_P ; -x_B] staged in LDS, one 64 x 3 partial per tile; the last tile of a column block to finish
-// sums the block's partials in tile order (deterministic; hand-off protocol above). Gives (columns/64) x (rows/128) workgroups per
-// supernode instead of one wave per column with a serial loop over all R rows.
+// Backward sweep of the large supernodes (R > kWaveR) as a split-K GEMV: tile = 128 columns
+// (2 per lane, one 16-B load each: rows of G are padded to an even length) x kBwdTileRows rows
+// (4 waves x 32 rows) of the row-major G, the tile's slice of [y_P ; -x_B] staged in LDS, one
+// 128 x 3 partial per tile; the last tile of a column block to finish sums the block's partials
+// in tile order (deterministic; hand-off protocol above). Gives (columns/128) x (rows/128)
+// workgroups per supernode instead of one wave per column with a serial loop over all R rows.
 using BTile = DirectSolver::BTile;
 using BRed = DirectSolver::BRed;
 constexpr int kBwdTileRows = 128;
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
                                                   const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     __shared__ double v[3 * kBwdTileRows];
-    __shared__ double red[3][3 * 64];
+    __shared__ double red[3][6 * 64];
     const BTile t = tiles[first + blockIdx.x];
     const int tid = threadIdx.x;
     for (int i = tid; i < t.nr; i += 256) {
@@ -238,36 +240,47 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
     }
     __syncthreads();
     const int lane = tid & 63, w = tid >> 6;
-    const int c = t.c0 + lane;
+    const int c = t.c0 + 2 * lane;   // columns c, c+1 (c+1 may be the zero pad column)
     constexpr int per = kBwdTileRows / 4;
     const int i0 = w * per, i1 = min(i0 + per, t.nr);
-    double a0 = 0, a1 = 0, a2 = 0;
+    double a[6] = {0, 0, 0, 0, 0, 0};
     if (c < t.p) {
-        const double* G = Gr + t.goff + (size_t)t.r0 * t.p + c;
+        const double2* G = reinterpret_cast<const double2*>(Gr + t.goff + (size_t)t.r0 * t.ldr + c);
+        const int ld2 = t.ldr / 2;
 #pragma unroll 8
         for (int i = i0; i < i1; ++i) {
-            const double g = G[(size_t)i * t.p];
-            a0 += g * v[3 * i]; a1 += g * v[3 * i + 1]; a2 += g * v[3 * i + 2];
+            const double2 g = G[(size_t)i * ld2];
+            const double v0 = v[3 * i], v1 = v[3 * i + 1], v2 = v[3 * i + 2];
+            a[0] += g.x * v0; a[1] += g.x * v1; a[2] += g.x * v2;
+            a[3] += g.y * v0; a[4] += g.y * v1; a[5] += g.y * v2;
         }
     }
-    if (w > 0) { red[w - 1][3 * lane] = a0; red[w - 1][3 * lane + 1] = a1; red[w - 1][3 * lane + 2] = a2; }
+    if (w > 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[w - 1][6 * lane + k] = a[k];
     __syncthreads();
     if (w != 0) return;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { a0 += red[k][3 * lane]; a1 += red[k][3 * lane + 1]; a2 += red[k][3 * lane + 2]; }
-    double* o = part + t.poff + 3 * lane;
-    st_sc1(o, a0); st_sc1(o + 1, a1); st_sc1(o + 2, a2);
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a[k] += red[q][6 * lane + k];
+    double* o = part + t.poff + 6 * lane;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) st_sc1(o + k, a[k]);
     const BRed rd = reds[t.rid];
     if (!arrive_last(cnt + t.rid, rd.nt, lane)) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // last tile of the column block: sum its partials in tile order (deterministic)
-    if (lane < rd.nc) {
-        double b0 = 0, b1 = 0, b2 = 0;
-        const double* q = part + rd.poff + 3 * lane;
-#pragma unroll 8
-        for (int k = 0; k < rd.nt; ++k, q += 3 * 64) { b0 += q[0]; b1 += q[1]; b2 += q[2]; }
-        const size_t xo = 3 * (size_t)(rd.beg + rd.c0 + lane);
-        X[xo] = b0; X[xo + 1] = b1; X[xo + 2] = b2;
+    if (2 * lane < rd.nc) {
+        double b[6] = {0, 0, 0, 0, 0, 0};
+        const double* q = part + rd.poff + 6 * lane;
+#pragma unroll 4
+        for (int k = 0; k < rd.nt; ++k, q += 6 * 64)
+#pragma unroll
+            for (int m = 0; m < 6; ++m) b[m] += q[m];
+        const size_t xo = 3 * (size_t)(rd.beg + rd.c0 + 2 * lane);
+        X[xo] = b[0]; X[xo + 1] = b[1]; X[xo + 2] = b[2];
+        if (2 * lane + 1 < rd.nc) { X[xo + 3] = b[3]; X[xo + 4] = b[4]; X[xo + 5] = b[5]; }
     }
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -443,11 +456,12 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             const int seg = (int)((it >> 20) & 0xfffff), j = (int)(it & 0xfffff), p = nd.p, R = p + nd.nb;
             const double* v = lds + nd.lds;
             const double* G = Gr + nd.goff + j;
+            const int ld = nd.ldr;
             const int r1 = min(R, (seg + 1) * kSubSegRows);
             double a0 = 0, a1 = 0, a2 = 0;
 #pragma unroll 8
             for (int r = max(j, seg * kSubSegRows); r < r1; ++r) {
-                const double g = G[(size_t)r * p];
+                const double g = G[(size_t)r * ld];
                 a0 += g * v[3 * r]; a1 += g * v[3 * r + 1]; a2 += g * v[3 * r + 2];
             }
             double* q = lds + nd.slot + 3 * (sub_seg_off(seg, p) + j);
@@ -490,6 +504,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         for (int sn = 0; sn < nn_; ++sn) inc[sn] = (*node_part)[sn] == my_part || (*node_part)[sn] == -1;
     std::vector<int> beg(nn_), p(nn_), nb(nn_), bnd_off(nn_), bnd, pull_off(nn_);
     std::vector<long long> goff(nn_), uoff(nn_), foff(nn_, -1);
+    std::vector<int> ldr(nn_, 0);
     long long go = 0, uo = 0, fo = 0;
     double dense = 0, offd = 0, bsum = 0, piv = 0;
     int rows_total = 0;
@@ -498,13 +513,14 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         const int ps = F.end[sn] - F.beg[sn], nbs = (int)F.bnd[sn].size();
         beg[sn] = F.beg[sn]; p[sn] = ps; nb[sn] = nbs;
         goff[sn] = go; uoff[sn] = uo;
+        ldr[sn] = ps + (ps & 1);   // row-major rows padded to even length (16-B loads in k_bwd_tile)
         bnd_off[sn] = (int)bnd.size();
         pull_off[sn] = rows_total;
         if (!inc[sn]) continue;
         bnd.insert(bnd.end(), F.bnd[sn].begin(), F.bnd[sn].end());
         rows_total += ps + nbs;
         nnz_L_ += (size_t)ps * (ps + 1) / 2 + (size_t)ps * nbs;
-        go += (long long)(ps + nbs) * ps;
+        go += (long long)(ps + nbs) * (ps + (ps & 1));
         uo += 3LL * nbs;
         dense += 0.5 * ps * (ps + 1.0);
         offd += (double)ps * nbs;
@@ -516,14 +532,16 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
 #pragma omp parallel for schedule(dynamic, 1)
     for (int sn = 0; sn < nn_; ++sn) {
         if (!inc[sn]) continue;
-        const int ps = p[sn], nbs = nb[sn], R = ps + nbs;
+        const int ps = p[sn], nbs = nb[sn], R = ps + nbs, ld = ldr[sn];
         double* gr = Gr.data() + goff[sn];
         const std::vector<double>& Li = F.Linv[sn];
         const std::vector<double>& LB = F.LBP[sn];
+        for (int r = 0; r < R; ++r)
+            for (int c = ps; c < ld; ++c) gr[(size_t)r * ld + c] = 0.0;   // pad column
         for (int r = 0; r < ps; ++r)
-            for (int c = 0; c < ps; ++c) gr[(size_t)r * ps + c] = c <= r ? Li[(size_t)r * ps + c] : 0.0;
+            for (int c = 0; c < ps; ++c) gr[(size_t)r * ld + c] = c <= r ? Li[(size_t)r * ps + c] : 0.0;
         for (int a = 0; a < nbs; ++a) {
-            double* m = gr + (size_t)(ps + a) * ps;
+            double* m = gr + (size_t)(ps + a) * ld;
             for (int c = 0; c < ps; ++c) m[c] = 0.0;
             for (int k = 0; k < ps; ++k) {
                 const double l = LB[(size_t)a * ps + k];
@@ -534,7 +552,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         }
         double* gc = Gc.data() + goff[sn];
         for (int r = 0; r < R; ++r)
-            for (int c = 0; c < ps; ++c) gc[(size_t)c * R + r] = gr[(size_t)r * ps + c];
+            for (int c = 0; c < ps; ++c) gc[(size_t)c * R + r] = gr[(size_t)r * ld + c];
     }
     // children lists and ELL pull lists (front row q of a parent <- child update entries, fixed order)
     // (partitioned: the children of the top that belong to other GPUs' parts contribute nothing
@@ -639,7 +657,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                         fused[v] = 1;
                         SubNode nd{};
                         nd.p = p[v]; nd.nb = nb[v]; nd.beg = beg[v]; nd.bnd_off = bnd_off[v]; nd.ell_w = ell_w[v];
-                        nd.lds = 0; nd.goff = goff[v]; nd.uoff = uoff[v]; nd.ell_off = ell_off[v];
+                        nd.lds = 0; nd.goff = goff[v]; nd.uoff = uoff[v]; nd.ell_off = ell_off[v]; nd.ldr = ldr[v];
                         snodes.push_back(nd);
                     }
                     // forward: f_P offsets, assembly items, row items
@@ -721,7 +739,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         t.node = sn; t.r0 = r0; t.nr = nr; t.mode = mode;
         t.p = p[sn]; t.nb = nb[sn]; t.beg = beg[sn]; t.bnd_off = bnd_off[sn];
         t.ell_w = ell_w[sn];
-        t.goff = goff[sn]; t.uoff = uoff[sn]; t.foff = foff[sn]; t.ell_off = ell_off[sn];
+        t.goff = goff[sn]; t.uoff = uoff[sn]; t.foff = foff[sn]; t.ell_off = ell_off[sn]; t.ldr = ldr[sn];
         return t;
     };
     levels_.clear();
@@ -796,16 +814,16 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
             if (R <= kWaveR) continue;
-            for (int c0 = 0; c0 < p[sn]; c0 += 64) {
+            for (int c0 = 0; c0 < p[sn]; c0 += 128) {
                 BRed rd{};
-                rd.beg = beg[sn]; rd.c0 = c0; rd.nc = std::min(64, p[sn] - c0); rd.poff = poff;
+                rd.beg = beg[sn]; rd.c0 = c0; rd.nc = std::min(128, p[sn] - c0); rd.poff = poff;
                 for (int r0 = c0; r0 < R; r0 += kBwdTileRows) {
                     BTile bt{};
                     bt.beg = beg[sn]; bt.p = p[sn]; bt.nb = nb[sn]; bt.bnd_off = bnd_off[sn];
                     bt.c0 = c0; bt.r0 = r0; bt.nr = std::min(kBwdTileRows, R - r0);
-                    bt.goff = goff[sn]; bt.poff = poff;
+                    bt.goff = goff[sn]; bt.poff = poff; bt.ldr = ldr[sn];
                     bt.rid = (int)breds.size();
-                    poff += 3 * 64;
+                    poff += 6 * 64;
                     btiles.push_back(bt);
                     ++rd.nt;
                 }

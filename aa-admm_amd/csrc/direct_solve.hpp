@@ -51,21 +51,21 @@ public:
     struct Task {
         int node, r0, nr, mode;
         int p, nb, beg, bnd_off;
-        int ell_w, pad0, pad1, pad2;
+        int ell_w, ldr, pad1, pad2;   // ldr: row stride of the row-major G (p padded to even)
         long long goff, uoff, foff, ell_off;
     };
 
     // Bottom subtrees (all supernodes up to a cut height) are solved whole by one workgroup
     // each: their levels are separated by workgroup barriers instead of kernel boundaries.
     struct SubNode {   // a supernode inside a fused subtree; lds = its vector's offset in LDS,
-        int p, nb, beg, bnd_off, ell_w, lds, slot, pad1;   // slot = its backward segment partials
+        int p, nb, beg, bnd_off, ell_w, lds, slot, ldr;   // slot = its backward segment partials
         long long goff, uoff, ell_off;
     };
     struct SubLevel { int n0, fa0, nfa, fr0, nfr, bv0, nbv, bc0, nbc, bs0, nbs, pad; };   // item ranges
     struct SubTree { int lvl0, nlvl; };
     // split-K backward of large supernodes: a tile (64 columns from c0, nr rows from r0) and the
     // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
-    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid; long long goff, poff; };
+    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid, ldr, pad; long long goff, poff; };
     struct BRed { int beg, c0, nc, nt; long long poff; };
     // split-K forward of large supernodes: tile (64 rows from r0, nc columns from c0) and the
     // per-row-block reduction of its nt partials
