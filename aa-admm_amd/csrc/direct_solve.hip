@@ -46,305 +46,286 @@ __device__ __forceinline__ double wsum(double v) {
     return v;
 }
 
-// front row q of a supernode: [b_P ; 0]_q + the children's update entries landing on it
-// (ELL pull list: t.ell_w offsets into U per row, -1 = none; fixed order -> deterministic)
-__device__ __forceinline__ void front_row(const Task& t, int q, const long long* __restrict__ ell,
-                                          const double* __restrict__ B, const double* __restrict__ U, double& a0,
-                                          double& a1, double& a2) {
-    a0 = a1 = a2 = 0;
-    if (q < t.p) { const size_t o = 3 * (size_t)(t.beg + q); a0 = B[o]; a1 = B[o + 1]; a2 = B[o + 2]; }
+// Right-hand-side sets. NR = 3: one solve (the x, y, z columns of A_s X = B). NR = 6: two
+// independent solves batched into one pass, so the factor is streamed from HBM once for both
+// (the Z variant's main solve and the previous iteration's combined-residual solve). The
+// caller's vectors b and x stay 3-interleaved per node, one array per set (P0, P1); the
+// solver's own vectors (Y, U, split-K partials, LDS) are NR-interleaved, and every offset the
+// host built for 3 columns is scaled by NR / 3 on the device. Each column's sums run in the
+// same order for NR = 3 and 6, so a batched solve is bit-identical to two single ones.
+template <int NR>
+__device__ __forceinline__ void ld_ext(const double* __restrict__ P0, const double* __restrict__ P1, size_t node,
+                                       double* a) {
+    const size_t o = 3 * node;
+    a[0] = P0[o]; a[1] = P0[o + 1]; a[2] = P0[o + 2];
+    if constexpr (NR == 6) { a[3] = P1[o]; a[4] = P1[o + 1]; a[5] = P1[o + 2]; }
+}
+template <int NR>
+__device__ __forceinline__ void st_ext(double* P0, double* P1, size_t node, const double* a) {
+    const size_t o = 3 * node;
+    P0[o] = a[0]; P0[o + 1] = a[1]; P0[o + 2] = a[2];
+    if constexpr (NR == 6) { P1[o] = a[3]; P1[o + 1] = a[4]; P1[o + 2] = a[5]; }
+}
+template <int NR>
+__device__ __forceinline__ void zero(double* a) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) a[k] = 0;
+}
+
+// front row q of a supernode (any record with beg, p, ell_w, ell_off): [b_P ; 0]_q + the
+// children's update entries landing on it (ELL pull list: ell_w offsets into U per row, -1 =
+// none; fixed order -> deterministic)
+template <int NR, class N>
+__device__ __forceinline__ void front_row(const N& t, int q, const long long* __restrict__ ell,
+                                          const double* __restrict__ B0, const double* __restrict__ B1,
+                                          const double* __restrict__ U, double* a) {
+    zero<NR>(a);
+    if (q < t.p) ld_ext<NR>(B0, B1, (size_t)(t.beg + q), a);
     const long long* e = ell + t.ell_off + (size_t)q * t.ell_w;
     for (int k = 0; k < t.ell_w; ++k) {
         const long long o = e[k];
-        if (o >= 0) { a0 += U[o]; a1 += U[o + 1]; a2 += U[o + 2]; }
+        if (o >= 0) {
+            const double* u = U + (NR / 3) * o;
+#pragma unroll
+            for (int j = 0; j < NR; ++j) a[j] += u[j];
+        }
     }
 }
 
-// front row q of a supernode given by its fields (the split-K tiles assemble their own slices)
-__device__ __forceinline__ void front_row_at(int beg, int p, int ell_w, long long ell_off, int q,
-                                             const long long* __restrict__ ell, const double* __restrict__ B,
-                                             const double* __restrict__ U, double& a0, double& a1, double& a2) {
-    a0 = a1 = a2 = 0;
-    if (q < p) { const size_t o = 3 * (size_t)(beg + q); a0 = B[o]; a1 = B[o + 1]; a2 = B[o + 2]; }
-    const long long* e = ell + ell_off + (size_t)q * ell_w;
-    for (int k = 0; k < ell_w; ++k) {
-        const long long o = e[k];
-        if (o >= 0) { a0 += U[o]; a1 += U[o + 1]; a2 += U[o + 2]; }
-    }
-}
-
-// assembly of the front vectors of wave-mode supernodes into Fg
-__global__ __launch_bounds__(256) void k_asm(const Task* __restrict__ tasks, int first, const long long* __restrict__ ell,
-                                             const double* __restrict__ B, const double* __restrict__ U,
-                                             double* __restrict__ Fg, const Ctrl* ctrl, int gate_reject) {
-    if (solve_gated(ctrl, gate_reject)) return;
-    const Task t = tasks[first + blockIdx.x];
-    if ((int)threadIdx.x >= t.nr) return;
-    const int q = t.r0 + threadIdx.x;
-    double a0, a1, a2;
-    front_row(t, q, ell, B, U, a0, a1, a2);
-    double* f = Fg + t.foff + 3 * (size_t)q;
-    f[0] = a0; f[1] = a1; f[2] = a2;
-}
-
-// forward sweep of one tree level: y_P = Linv f_P (rows r < p), u = f_B - M f_P (rows r >= p)
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, int first, const double* __restrict__ Gr,
-                                               const double* __restrict__ Gc, const long long* __restrict__ ell,
-                                               const double* __restrict__ B, double* __restrict__ Y,
-                                               double* __restrict__ U, const double* __restrict__ Fg,
-                                               const Ctrl* ctrl, int gate_reject) {
+// forward sweep of one tree level: y_P = Linv f_P (rows r < p), u = f_B - M f_P (rows r >= p);
+// thread per row, f_P in LDS, column-major G (lanes read consecutive rows)
+template <int BLOCK, int NR>
+__global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, int first, const double* __restrict__ Gc,
+                                               const long long* __restrict__ ell, const double* __restrict__ B0,
+                                               const double* __restrict__ B1, double* __restrict__ Y,
+                                               double* __restrict__ U, const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Task t = tasks[first + blockIdx.x];
     const int p = t.p, R = p + t.nb;
     const int tid = threadIdx.x;
-    if (t.mode == 0) {   // thread per row, f_P in LDS, column-major G (lanes read consecutive rows)
-        double* f = lds;
-        for (int c = tid; c < p; c += BLOCK) front_row(t, c, ell, B, U, f[3 * c], f[3 * c + 1], f[3 * c + 2]);
-        __syncthreads();
-        if (tid >= t.nr) return;
-        const int r = t.r0 + tid;
-        const double* G = Gc + t.goff + r;
-        const int cmax = r < p ? r + 1 : p;
-        double a0 = 0, a1 = 0, a2 = 0;
+    double* f = lds;
+    for (int c = tid; c < p; c += BLOCK) front_row<NR>(t, c, ell, B0, B1, U, f + NR * c);
+    __syncthreads();
+    if (tid >= t.nr) return;
+    const int r = t.r0 + tid;
+    const double* G = Gc + t.goff + r;
+    const int cmax = r < p ? r + 1 : p;
+    double a[NR];
+    zero<NR>(a);
 #pragma unroll 8
-        for (int c = 0; c < cmax; ++c) {
-            const double v = G[(size_t)c * R];
-            a0 += v * f[3 * c]; a1 += v * f[3 * c + 1]; a2 += v * f[3 * c + 2];
-        }
-        if (r < p) {
-            const size_t o = 3 * (size_t)(t.beg + r);
-            Y[o] = a0; Y[o + 1] = a1; Y[o + 2] = a2;
-        } else {
-            double f0, f1, f2;
-            front_row(t, r, ell, B, U, f0, f1, f2);
-            double* u = U + t.uoff + 3 * (size_t)(r - p);
-            u[0] = f0 - a0; u[1] = f1 - a1; u[2] = f2 - a2;
-        }
-    } else {             // wave per row, lanes across the row of the row-major G, f from Fg
-        const int lane = tid & 63, w = tid >> 6;
-        const double* F = Fg + t.foff;
-        for (int rr = w; rr < t.nr; rr += BLOCK / 64) {
-            const int r = t.r0 + rr;
-            const double* row = Gr + t.goff + (size_t)r * t.ldr;
-            const int cmax = r < p ? r + 1 : p;
-            double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 4
-            for (int c = lane; c < cmax; c += 64) {
-                const double v = row[c];
-                a0 += v * F[3 * c]; a1 += v * F[3 * c + 1]; a2 += v * F[3 * c + 2];
-            }
-            a0 = wsum(a0); a1 = wsum(a1); a2 = wsum(a2);
-            if (lane == 0) {
-                if (r < p) {
-                    const size_t o = 3 * (size_t)(t.beg + r);
-                    Y[o] = a0; Y[o + 1] = a1; Y[o + 2] = a2;
-                } else {
-                    double* u = U + t.uoff + 3 * (size_t)(r - p);
-                    u[0] = F[3 * r] - a0; u[1] = F[3 * r + 1] - a1; u[2] = F[3 * r + 2] - a2;
-                }
-            }
-        }
+    for (int c = 0; c < cmax; ++c) {
+        const double v = G[(size_t)c * R];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
+    }
+    if (r < p) {
+        double* y = Y + NR * (size_t)(t.beg + r);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) y[k] = a[k];
+    } else {
+        double fr[NR];
+        front_row<NR>(t, r, ell, B0, B1, U, fr);
+        double* u = U + (NR / 3) * t.uoff + NR * (size_t)(r - p);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) u[k] = fr[k] - a[k];
     }
 }
 
-// backward sweep of one tree level: x_P = Linv^T y_P - M^T x_B (columns j of G)
-template <int BLOCK>
+// [y_P ; -x_B]_r of a supernode (backward input vector)
+template <int NR, class N>
+__device__ __forceinline__ void bwd_row(const N& t, int r, const int* __restrict__ bnd, const double* __restrict__ Y,
+                                        const double* __restrict__ X0, const double* __restrict__ X1, double* v) {
+    if (r < t.p) {
+        const double* y = Y + NR * (size_t)(t.beg + r);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) v[k] = y[k];
+    } else {
+        ld_ext<NR>(X0, X1, (size_t)bnd[t.bnd_off + r - t.p], v);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) v[k] = -v[k];
+    }
+}
+
+// backward sweep of one tree level: x_P = Linv^T y_P - M^T x_B (columns j of G); thread per
+// column, [y_P ; -x_B] in LDS, row-major G (lanes read consecutive columns)
+template <int BLOCK, int NR>
 __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, int first, const double* __restrict__ Gr,
-                                               const double* __restrict__ Gc, const int* __restrict__ bnd,
-                                               const double* __restrict__ Y, double* __restrict__ X,
-                                               const Ctrl* ctrl, int gate_reject) {
+                                               const int* __restrict__ bnd, const double* __restrict__ Y,
+                                               double* __restrict__ X0, double* __restrict__ X1, const Ctrl* ctrl,
+                                               int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Task t = tasks[first + blockIdx.x];
-    const int p = t.p, R = p + t.nb;
-    const int* bi = bnd + t.bnd_off;
+    const int R = t.p + t.nb;
     const int tid = threadIdx.x;
-    if (t.mode == 0) {   // thread per column, [y_P ; -x_B] in LDS, row-major G (lanes read consecutive columns)
-        double* v = lds;
-        for (int r = tid; r < R; r += BLOCK) {
-            const size_t o = r < p ? 3 * (size_t)(t.beg + r) : 3 * (size_t)bi[r - p];
-            const double sg = r < p ? 1.0 : -1.0;
-            const double* src = r < p ? Y : X;
-            v[3 * r] = sg * src[o]; v[3 * r + 1] = sg * src[o + 1]; v[3 * r + 2] = sg * src[o + 2];
-        }
-        __syncthreads();
-        if (tid >= t.nr) return;
-        const int j = t.r0 + tid;
-        const double* G = Gr + t.goff + j;
-        const int ld = t.ldr;
-        double a0 = 0, a1 = 0, a2 = 0;
+    double* v = lds;
+    for (int r = tid; r < R; r += BLOCK) bwd_row<NR>(t, r, bnd, Y, X0, X1, v + NR * r);
+    __syncthreads();
+    if (tid >= t.nr) return;
+    const int j = t.r0 + tid;
+    const double* G = Gr + t.goff + j;
+    const int ld = t.ldr;
+    double a[NR];
+    zero<NR>(a);
 #pragma unroll 8
-        for (int r = j; r < R; ++r) {
-            const double g = G[(size_t)r * ld];
-            a0 += g * v[3 * r]; a1 += g * v[3 * r + 1]; a2 += g * v[3 * r + 2];
-        }
-        const size_t o = 3 * (size_t)(t.beg + j);
-        X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
-    } else {             // wave per column, lanes down the column of the column-major G
-        const int lane = tid & 63, w = tid >> 6;
-        for (int jj = w; jj < t.nr; jj += BLOCK / 64) {
-            const int j = t.r0 + jj;
-            const double* col = Gc + t.goff + (size_t)j * R;
-            double a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll 4
-            for (int r = j + lane; r < R; r += 64) {
-                const double g = col[r];
-                if (r < p) {
-                    const size_t o = 3 * (size_t)(t.beg + r);
-                    a0 += g * Y[o]; a1 += g * Y[o + 1]; a2 += g * Y[o + 2];
-                } else {
-                    const size_t o = 3 * (size_t)bi[r - p];
-                    a0 -= g * X[o]; a1 -= g * X[o + 1]; a2 -= g * X[o + 2];
-                }
-            }
-            a0 = wsum(a0); a1 = wsum(a1); a2 = wsum(a2);
-            if (lane == 0) {
-                const size_t o = 3 * (size_t)(t.beg + j);
-                X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
-            }
-        }
+    for (int r = j; r < R; ++r) {
+        const double g = G[(size_t)r * ld];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
     }
+    st_ext<NR>(X0, X1, (size_t)(t.beg + j), a);
 }
 
 // Backward sweep of the large supernodes (R > kWaveR) as a split-K GEMV: tile = 128 columns
 // (2 per lane, one 16-B load each: rows of G are padded to an even length) x kBwdTileRows rows
 // (4 waves x 32 rows) of the row-major G, the tile's slice of [y_P ; -x_B] staged in LDS, one
-// 128 x 3 partial per tile; the last tile of a column block to finish sums the block's partials
+// 128 x NR partial per tile; the last tile of a column block to finish sums the block's partials
 // in tile order (deterministic; hand-off protocol above). Gives (columns/128) x (rows/128)
 // workgroups per supernode instead of one wave per column with a serial loop over all R rows.
 using BTile = DirectSolver::BTile;
 using BRed = DirectSolver::BRed;
 constexpr int kBwdTileRows = 128;
 
+template <int NR>
 __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tiles, int first, const double* __restrict__ Gr,
                                                   const int* __restrict__ bnd, const double* __restrict__ Y,
-                                                  double* __restrict__ X, double* __restrict__ part,
-                                                  const BRed* __restrict__ reds, int* __restrict__ cnt,
-                                                  const Ctrl* ctrl, int gate_reject) {
+                                                  double* __restrict__ X0, double* __restrict__ X1,
+                                                  double* __restrict__ part, const BRed* __restrict__ reds,
+                                                  int* __restrict__ cnt, const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
-    __shared__ double v[3 * kBwdTileRows];
-    __shared__ double red[3][6 * 64];
+    constexpr int W = 2 * NR;   // accumulators per lane: columns c and c + 1
+    __shared__ double v[NR * kBwdTileRows];
+    __shared__ double red[3][W * 64];
     const BTile t = tiles[first + blockIdx.x];
     const int tid = threadIdx.x;
-    for (int i = tid; i < t.nr; i += 256) {
-        const int r = t.r0 + i;
-        if (r < t.p) {
-            const size_t o = 3 * (size_t)(t.beg + r);
-            v[3 * i] = Y[o]; v[3 * i + 1] = Y[o + 1]; v[3 * i + 2] = Y[o + 2];
-        } else {
-            const size_t o = 3 * (size_t)bnd[t.bnd_off + r - t.p];
-            v[3 * i] = -X[o]; v[3 * i + 1] = -X[o + 1]; v[3 * i + 2] = -X[o + 2];
-        }
-    }
+    for (int i = tid; i < t.nr; i += 256) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
     __syncthreads();
     const int lane = tid & 63, w = tid >> 6;
     const int c = t.c0 + 2 * lane;   // columns c, c+1 (c+1 may be the zero pad column)
     constexpr int per = kBwdTileRows / 4;
     const int i0 = w * per, i1 = min(i0 + per, t.nr);
-    double a[6] = {0, 0, 0, 0, 0, 0};
+    double a[W];
+    zero<W>(a);
     if (c < t.p) {
         const double2* G = reinterpret_cast<const double2*>(Gr + t.goff + (size_t)t.r0 * t.ldr + c);
         const int ld2 = t.ldr / 2;
 #pragma unroll 8
         for (int i = i0; i < i1; ++i) {
             const double2 g = G[(size_t)i * ld2];
-            const double v0 = v[3 * i], v1 = v[3 * i + 1], v2 = v[3 * i + 2];
-            a[0] += g.x * v0; a[1] += g.x * v1; a[2] += g.x * v2;
-            a[3] += g.y * v0; a[4] += g.y * v1; a[5] += g.y * v2;
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                const double vk = v[NR * i + k];
+                a[k] += g.x * vk;
+                a[NR + k] += g.y * vk;
+            }
         }
     }
     if (w > 0)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) red[w - 1][6 * lane + k] = a[k];
+        for (int k = 0; k < W; ++k) red[w - 1][W * lane + k] = a[k];
     __syncthreads();
     if (w != 0) return;
 #pragma unroll
     for (int q = 0; q < 3; ++q)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) a[k] += red[q][6 * lane + k];
-    double* o = part + t.poff + 6 * lane;
+        for (int k = 0; k < W; ++k) a[k] += red[q][W * lane + k];
+    double* o = part + (NR / 3) * t.poff + W * lane;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) st_sc1(o + k, a[k]);
+    for (int k = 0; k < W; ++k) st_sc1(o + k, a[k]);
     const BRed rd = reds[t.rid];
     if (!arrive_last(cnt + t.rid, rd.nt, lane)) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // last tile of the column block: sum its partials in tile order (deterministic)
     if (2 * lane < rd.nc) {
-        double b[6] = {0, 0, 0, 0, 0, 0};
-        const double* q = part + rd.poff + 6 * lane;
+        double b[W];
+        zero<W>(b);
+        const double* q = part + (NR / 3) * rd.poff + W * lane;
 #pragma unroll 4
-        for (int k = 0; k < rd.nt; ++k, q += 6 * 64)
+        for (int k = 0; k < rd.nt; ++k, q += W * 64)
 #pragma unroll
-            for (int m = 0; m < 6; ++m) b[m] += q[m];
-        const size_t xo = 3 * (size_t)(rd.beg + rd.c0 + 2 * lane);
-        X[xo] = b[0]; X[xo + 1] = b[1]; X[xo + 2] = b[2];
-        if (2 * lane + 1 < rd.nc) { X[xo + 3] = b[3]; X[xo + 4] = b[4]; X[xo + 5] = b[5]; }
+            for (int m = 0; m < W; ++m) b[m] += q[m];
+        const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane);
+        st_ext<NR>(X0, X1, xo, b);
+        if (2 * lane + 1 < rd.nc) st_ext<NR>(X0, X1, xo + 1, b + NR);
     }
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Forward sweep of the large supernodes (p > kWaveP) as a split-K GEMV on the column-major G:
 // tile = 64 rows (lanes) x kFwdTileCols columns (4 waves x 32), the tile's slice of the
-// assembled front f_P staged in LDS, one 64 x 3 partial per tile; the last tile of a row block to finish sums
-// its partials in tile order and writes y_P (rows < p) or the update vector u = f_B - M f_P.
+// assembled front f_P staged in LDS, one 64 x NR partial per tile; the last tile of a row block
+// to finish sums its partials in tile order and writes y_P (rows < p) or the update vector
+// u = f_B - M f_P.
 using FTile = DirectSolver::FTile;
 using FRed = DirectSolver::FRed;
 constexpr int kFwdTileCols = 128;
 
+template <int NR>
 __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tiles, int first, const double* __restrict__ Gc,
-                                                  const long long* __restrict__ ell, const double* __restrict__ B,
-                                                  double* __restrict__ part, const FRed* __restrict__ reds,
-                                                  int* __restrict__ cnt, double* __restrict__ Y, double* __restrict__ U,
-                                                  const Ctrl* ctrl, int gate_reject) {
+                                                  const long long* __restrict__ ell, const double* __restrict__ B0,
+                                                  const double* __restrict__ B1, double* __restrict__ part,
+                                                  const FRed* __restrict__ reds, int* __restrict__ cnt,
+                                                  double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
+                                                  int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
-    __shared__ double f[3 * kFwdTileCols];
-    __shared__ double red[3][3 * 64];
+    __shared__ double f[NR * kFwdTileCols];
+    __shared__ double red[3][NR * 64];
     const FTile t = tiles[first + blockIdx.x];
     const int tid = threadIdx.x;
     // this tile's slice of the front f_P = b_P + extend-add of the children's update vectors
-    for (int i = tid; i < t.nc; i += 256)
-        front_row_at(t.beg, t.p, t.ell_w, t.ell_off, t.c0 + i, ell, B, U, f[3 * i], f[3 * i + 1], f[3 * i + 2]);
+    for (int i = tid; i < t.nc; i += 256) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i);
     __syncthreads();
     const int lane = tid & 63, w = tid >> 6;
     const int r = t.r0 + lane;
     constexpr int per = kFwdTileCols / 4;
     const int i0 = w * per, i1 = min(i0 + per, t.nc);
-    double a0 = 0, a1 = 0, a2 = 0;
+    double a[NR];
+    zero<NR>(a);
     if (r < t.R) {
         const double* G = Gc + t.goff + (size_t)t.c0 * t.R + r;
 #pragma unroll 8
         for (int i = i0; i < i1; ++i) {
             const double g = G[(size_t)i * t.R];
-            a0 += g * f[3 * i]; a1 += g * f[3 * i + 1]; a2 += g * f[3 * i + 2];
+#pragma unroll
+            for (int k = 0; k < NR; ++k) a[k] += g * f[NR * i + k];
         }
     }
-    if (w > 0) { red[w - 1][3 * lane] = a0; red[w - 1][3 * lane + 1] = a1; red[w - 1][3 * lane + 2] = a2; }
+    if (w > 0)
+#pragma unroll
+        for (int k = 0; k < NR; ++k) red[w - 1][NR * lane + k] = a[k];
     __syncthreads();
     if (w != 0) return;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { a0 += red[k][3 * lane]; a1 += red[k][3 * lane + 1]; a2 += red[k][3 * lane + 2]; }
-    double* o = part + t.poff + 3 * lane;
-    st_sc1(o, a0); st_sc1(o + 1, a1); st_sc1(o + 2, a2);
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int k = 0; k < NR; ++k) a[k] += red[q][NR * lane + k];
+    double* o = part + (NR / 3) * t.poff + NR * lane;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) st_sc1(o + k, a[k]);
     const FRed rd = reds[t.rid];
     if (!arrive_last(cnt + t.rid, rd.nt, lane)) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // last tile of the row block: sum its partials in tile order (deterministic)
     if (lane < rd.nr) {
-        double b0 = 0, b1 = 0, b2 = 0;
-        const double* q = part + rd.poff + 3 * lane;
+        double b[NR];
+        zero<NR>(b);
+        const double* q = part + (NR / 3) * rd.poff + NR * lane;
 #pragma unroll 8
-        for (int k = 0; k < rd.nt; ++k, q += 3 * 64) { b0 += q[0]; b1 += q[1]; b2 += q[2]; }
+        for (int k = 0; k < rd.nt; ++k, q += NR * 64)
+#pragma unroll
+            for (int m = 0; m < NR; ++m) b[m] += q[m];
         const int rr = rd.r0 + lane;
         if (rr < rd.p) {
-            const size_t yo = 3 * (size_t)(rd.beg + rr);
-            Y[yo] = b0; Y[yo + 1] = b1; Y[yo + 2] = b2;
+            double* y = Y + NR * (size_t)(rd.beg + rr);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) y[k] = b[k];
         } else {
-            double f0, f1, f2;
-            front_row_at(rd.beg, rd.p, rd.ell_w, rd.ell_off, rr, ell, B, U, f0, f1, f2);
-            double* u = U + rd.uoff + 3 * (size_t)(rr - rd.p);
-            u[0] = f0 - b0; u[1] = f1 - b1; u[2] = f2 - b2;
+            double fr[NR];
+            front_row<NR>(rd, rr, ell, B0, B1, U, fr);
+            double* u = U + (NR / 3) * rd.uoff + NR * (size_t)(rr - rd.p);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) u[k] = fr[k] - b[k];
         }
     }
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -354,27 +335,17 @@ using SubNode = DirectSolver::SubNode;
 using SubLevel = DirectSolver::SubLevel;
 using SubTree = DirectSolver::SubTree;
 
-__device__ __forceinline__ void sub_front_row(const SubNode& t, int q, const long long* __restrict__ ell,
-                                              const double* __restrict__ B, const double* __restrict__ U, double& a0,
-                                              double& a1, double& a2) {
-    a0 = a1 = a2 = 0;
-    if (q < t.p) { const size_t o = 3 * (size_t)(t.beg + q); a0 = B[o]; a1 = B[o + 1]; a2 = B[o + 2]; }
-    const long long* e = ell + t.ell_off + (size_t)q * t.ell_w;
-    for (int k = 0; k < t.ell_w; ++k) {
-        const long long o = e[k];
-        if (o >= 0) { a0 += U[o]; a1 += U[o + 1]; a2 += U[o + 2]; }
-    }
-}
-
 // forward sweep of a whole bottom subtree (one workgroup), its levels bottom-up
-template <int BLOCK>
+template <int BLOCK, int NR>
 __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
                                                  const SubNode* __restrict__ nodes, const int* __restrict__ items,
                                                  const double* __restrict__ Gc, const long long* __restrict__ ell,
-                                                 const double* __restrict__ B, double* __restrict__ Y,
-                                                 double* __restrict__ U, const Ctrl* ctrl, int gate_reject) {
+                                                 const double* __restrict__ B0, const double* __restrict__ B1,
+                                                 double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
+                                                 int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int K = NR / 3;
     const SubTree T = trees[blockIdx.x];
     const int tid = threadIdx.x;
     for (int l = 0; l < T.nlvl; ++l) {
@@ -383,31 +354,34 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             const int it = items[L.fa0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
             const int c = it & 0xffff;
-            double* f = lds + nd.lds + 3 * c;
-            sub_front_row(nd, c, ell, B, U, f[0], f[1], f[2]);
+            front_row<NR>(nd, c, ell, B0, B1, U, lds + K * nd.lds + NR * c);
         }
         __syncthreads();
         for (int i = tid; i < L.nfr; i += BLOCK) {          // rows of G . f_P
             const int it = items[L.fr0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
             const int r = it & 0xffff, p = nd.p, R = p + nd.nb;
-            const double* f = lds + nd.lds;
+            const double* f = lds + K * nd.lds;
             const double* G = Gc + nd.goff + r;
             const int cmax = r < p ? r + 1 : p;
-            double a0 = 0, a1 = 0, a2 = 0;
+            double a[NR];
+            zero<NR>(a);
 #pragma unroll 8
             for (int c = 0; c < cmax; ++c) {
                 const double v = G[(size_t)c * R];
-                a0 += v * f[3 * c]; a1 += v * f[3 * c + 1]; a2 += v * f[3 * c + 2];
+#pragma unroll
+                for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
             }
             if (r < p) {
-                const size_t o = 3 * (size_t)(nd.beg + r);
-                Y[o] = a0; Y[o + 1] = a1; Y[o + 2] = a2;
+                double* y = Y + NR * (size_t)(nd.beg + r);
+#pragma unroll
+                for (int k = 0; k < NR; ++k) y[k] = a[k];
             } else {
-                double f0, f1, f2;
-                sub_front_row(nd, r, ell, B, U, f0, f1, f2);
-                double* u = U + nd.uoff + 3 * (size_t)(r - p);
-                u[0] = f0 - a0; u[1] = f1 - a1; u[2] = f2 - a2;
+                double fr[NR];
+                front_row<NR>(nd, r, ell, B0, B1, U, fr);
+                double* u = U + K * nd.uoff + NR * (size_t)(r - p);
+#pragma unroll
+                for (int k = 0; k < NR; ++k) u[k] = fr[k] - a[k];
             }
         }
         __syncthreads();
@@ -426,15 +400,16 @@ __device__ __forceinline__ int sub_seg_off(int seg, int p) {   // partial slots 
     return o;
 }
 
-template <int BLOCK>
+template <int BLOCK, int NR>
 __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
                                                  const SubNode* __restrict__ nodes, const int* __restrict__ items,
                                                  const long long* __restrict__ items2,
                                                  const double* __restrict__ Gr, const int* __restrict__ bnd,
-                                                 const double* __restrict__ Y, double* __restrict__ X,
-                                                 const Ctrl* ctrl, int gate_reject) {
+                                                 const double* __restrict__ Y, double* __restrict__ X0,
+                                                 double* __restrict__ X1, const Ctrl* ctrl, int gate_reject) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int K = NR / 3;
     const SubTree T = trees[blockIdx.x];
     const int tid = threadIdx.x;
     for (int l = T.nlvl - 1; l >= 0; --l) {
@@ -443,29 +418,28 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             const int it = items[L.bv0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
             const int r = it & 0xffff;
-            const size_t o = r < nd.p ? 3 * (size_t)(nd.beg + r) : 3 * (size_t)bnd[nd.bnd_off + r - nd.p];
-            const double sg = r < nd.p ? 1.0 : -1.0;
-            const double* src = r < nd.p ? Y : X;
-            double* v = lds + nd.lds + 3 * r;
-            v[0] = sg * src[o]; v[1] = sg * src[o + 1]; v[2] = sg * src[o + 2];
+            bwd_row<NR>(nd, r, bnd, Y, X0, X1, lds + K * nd.lds + NR * r);
         }
         __syncthreads();
         for (int i = tid; i < L.nbs; i += BLOCK) {          // segment partials of G^T . v
             const long long it = items2[L.bs0 + i];
             const SubNode nd = nodes[L.n0 + (int)(it >> 40)];
             const int seg = (int)((it >> 20) & 0xfffff), j = (int)(it & 0xfffff), p = nd.p, R = p + nd.nb;
-            const double* v = lds + nd.lds;
+            const double* v = lds + K * nd.lds;
             const double* G = Gr + nd.goff + j;
             const int ld = nd.ldr;
             const int r1 = min(R, (seg + 1) * kSubSegRows);
-            double a0 = 0, a1 = 0, a2 = 0;
+            double a[NR];
+            zero<NR>(a);
 #pragma unroll 8
             for (int r = max(j, seg * kSubSegRows); r < r1; ++r) {
                 const double g = G[(size_t)r * ld];
-                a0 += g * v[3 * r]; a1 += g * v[3 * r + 1]; a2 += g * v[3 * r + 2];
+#pragma unroll
+                for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
             }
-            double* q = lds + nd.slot + 3 * (sub_seg_off(seg, p) + j);
-            q[0] = a0; q[1] = a1; q[2] = a2;
+            double* q = lds + K * nd.slot + NR * (sub_seg_off(seg, p) + j);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) q[k] = a[k];
         }
         __syncthreads();
         for (int i = tid; i < L.nbc; i += BLOCK) {          // columns: sum of their segments
@@ -474,27 +448,27 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             const int j = it & 0xffff, p = nd.p, R = p + nd.nb;
             const int nseg = (R + kSubSegRows - 1) / kSubSegRows, s0 = j / kSubSegRows;
             int off = sub_seg_off(s0, p);
-            double a0 = 0, a1 = 0, a2 = 0;
+            double a[NR];
+            zero<NR>(a);
             for (int seg = s0; seg < nseg; ++seg) {
-                const double* q = lds + nd.slot + 3 * (off + j);
-                a0 += q[0]; a1 += q[1]; a2 += q[2];
+                const double* q = lds + K * nd.slot + NR * (off + j);
+#pragma unroll
+                for (int k = 0; k < NR; ++k) a[k] += q[k];
                 off += min(p, (seg + 1) * kSubSegRows);
             }
-            const size_t o = 3 * (size_t)(nd.beg + j);
-            X[o] = a0; X[o + 1] = a1; X[o + 2] = a2;
+            st_ext<NR>(X0, X1, (size_t)(nd.beg + j), a);
         }
         __syncthreads();
     }
 }
 
-constexpr int kWaveRowsPerTask = 8;   // wave-mode rows per 256-thread task (2 per wave)
-constexpr int kMaxLdsMode0 = 96 * 1024;
-
 }  // namespace
 
 void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part, int my_part,
-                         int top_beg, Comm* comm) {
+                         int top_beg, Comm* comm, int max_sets) {
     n_ = F.n;
+    max_sets_ = max_sets >= 2 ? 2 : 1;
+    const int KS = max_sets_;   // LDS / workspace scale of the widest solve
     nn_ = F.n_nodes;
     comm_ = (node_part && comm && comm->size() > 1) ? comm : nullptr;
     top_beg_ = comm_ ? top_beg : n_;
@@ -503,9 +477,9 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     if (comm_)
         for (int sn = 0; sn < nn_; ++sn) inc[sn] = (*node_part)[sn] == my_part || (*node_part)[sn] == -1;
     std::vector<int> beg(nn_), p(nn_), nb(nn_), bnd_off(nn_), bnd, pull_off(nn_);
-    std::vector<long long> goff(nn_), uoff(nn_), foff(nn_, -1);
+    std::vector<long long> goff(nn_), uoff(nn_);
     std::vector<int> ldr(nn_, 0);
-    long long go = 0, uo = 0, fo = 0;
+    long long go = 0, uo = 0;
     double dense = 0, offd = 0, bsum = 0, piv = 0;
     int rows_total = 0;
     nnz_L_ = 0;
@@ -620,10 +594,10 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         for (int rt : r) {
             std::vector<long long> lf(H + 1, 0), lb(H + 1, 0), nodes_at(H + 1, 0);
             for (int v : collect(rt)) {
-                lf[F.height[v]] += 24LL * p[v];
+                lf[F.height[v]] += 24LL * KS * p[v];
                 long long slots = 0;
                 for (int sg = 0; sg < (p[v] + nb[v] + 63) / 64; ++sg) slots += std::min(p[v], (sg + 1) * 64);
-                lb[F.height[v]] += 24LL * (p[v] + nb[v]) + 24LL * slots;
+                lb[F.height[v]] += 24LL * KS * (p[v] + nb[v] + slots);
                 nodes_at[F.height[v]] += 1;
                 if (p[v] + nb[v] > kMaxItemRow) ok = false;
             }
@@ -734,12 +708,12 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     std::vector<FTile> ftiles;
     std::vector<FRed> freds;
     long long poff = 0;
-    auto mk = [&](int sn, int r0, int nr, int mode) {
+    auto mk = [&](int sn, int r0, int nr) {
         Task t{};
-        t.node = sn; t.r0 = r0; t.nr = nr; t.mode = mode;
+        t.node = sn; t.r0 = r0; t.nr = nr;
         t.p = p[sn]; t.nb = nb[sn]; t.beg = beg[sn]; t.bnd_off = bnd_off[sn];
         t.ell_w = ell_w[sn];
-        t.goff = goff[sn]; t.uoff = uoff[sn]; t.foff = foff[sn]; t.ell_off = ell_off[sn]; t.ldr = ldr[sn];
+        t.goff = goff[sn]; t.uoff = uoff[sn]; t.ell_off = ell_off[sn]; t.ldr = ldr[sn];
         return t;
     };
     levels_.clear();
@@ -759,14 +733,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         L.fblock = fr > 128 ? 256 : (fr > 64 ? 128 : 64);
         (void)bwave;
         L.bblock = br > 128 ? 256 : (br > 64 ? 128 : 64);
-        L.asm_first = (int)tasks.size();
-        // (the split-K tiles assemble their own front slices: no assembly tasks)
-        L.asm_count = (int)tasks.size() - L.asm_first;
         L.fwd_first = (int)tasks.size();
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
             if (p[sn] <= kWaveP) {
-                for (int r0 = 0; r0 < R; r0 += L.fblock) tasks.push_back(mk(sn, r0, std::min(L.fblock, R - r0), 0));
+                for (int r0 = 0; r0 < R; r0 += L.fblock) tasks.push_back(mk(sn, r0, std::min(L.fblock, R - r0)));
                 L.lds_fwd = std::max(L.lds_fwd, 24 * p[sn]);
             }
         }
@@ -802,7 +773,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
             if (R <= kWaveR) {
-                for (int j0 = 0; j0 < p[sn]; j0 += L.bblock) tasks.push_back(mk(sn, j0, std::min(L.bblock, p[sn] - j0), 0));
+                for (int j0 = 0; j0 < p[sn]; j0 += L.bblock) tasks.push_back(mk(sn, j0, std::min(L.bblock, p[sn] - j0)));
                 L.lds_bwd = std::max(L.lds_bwd, 24 * R);
             }
         }
@@ -833,7 +804,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         L.bt_count = (int)btiles.size() - L.bt_first;
         L.br_count = (int)breds.size() - L.br_first;
         max_lds = std::max(max_lds, std::max(L.lds_fwd, L.lds_bwd));
-        kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.asm_count ? 1 : 0) + (L.bt_count ? 1 : 0) +
+        kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.bt_count ? 1 : 0) +
                     (L.ft_count ? 1 : 0);
         levels_.push_back(L);
         if (stats) {
@@ -860,60 +831,77 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     fcnt_.alloc(std::max<size_t>(freds.size(), 1)); fcnt_.zero(s);
     bcnt_.alloc(std::max<size_t>(breds.size(), 1)); bcnt_.zero(s);
     breds_.upload(breds, s);
-    bpart_.alloc(std::max<long long>(poff, 3));
-    Y_.alloc(3 * (size_t)n_);
-    U_.alloc(std::max<long long>(uo, 3));
-    Fg_.alloc(std::max<long long>(fo, 3));
-    if (std::max(sub_lds_f_, sub_lds_b_) > 64 * 1024)
-        for (const void* k : {(const void*)k_fwd_sub<256>, (const void*)k_fwd_sub<512>, (const void*)k_fwd_sub<1024>,
-                              (const void*)k_bwd_sub<256>, (const void*)k_bwd_sub<512>, (const void*)k_bwd_sub<1024>})
+    bpart_.alloc(std::max<long long>(KS * poff, 3));
+    Y_.alloc(3 * KS * (size_t)n_);
+    U_.alloc(std::max<long long>(KS * uo, 3));
+    // (LDS figures above are per 3 columns; a 6-column solve needs twice as much)
+    if (KS * std::max(sub_lds_f_, sub_lds_b_) > 64 * 1024)
+        for (const void* k : {(const void*)k_fwd_sub<256, 3>, (const void*)k_fwd_sub<512, 3>, (const void*)k_fwd_sub<1024, 3>,
+                              (const void*)k_bwd_sub<256, 3>, (const void*)k_bwd_sub<512, 3>, (const void*)k_bwd_sub<1024, 3>,
+                              (const void*)k_fwd_sub<256, 6>, (const void*)k_fwd_sub<512, 6>, (const void*)k_fwd_sub<1024, 6>,
+                              (const void*)k_bwd_sub<256, 6>, (const void*)k_bwd_sub<512, 6>, (const void*)k_bwd_sub<1024, 6>})
             AA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    if (max_lds > 64 * 1024) {   // large fronts: opt in to more than the default 64 KiB of LDS
-        for (const void* k : {(const void*)k_fwd<64>, (const void*)k_fwd<128>, (const void*)k_fwd<256>,
-                              (const void*)k_bwd<64>, (const void*)k_bwd<128>, (const void*)k_bwd<256>})
+    if (KS * max_lds > 64 * 1024) {   // large fronts: opt in to more than the default 64 KiB of LDS
+        for (const void* k : {(const void*)k_fwd<64, 3>, (const void*)k_fwd<128, 3>, (const void*)k_fwd<256, 3>,
+                              (const void*)k_bwd<64, 3>, (const void*)k_bwd<128, 3>, (const void*)k_bwd<256, 3>,
+                              (const void*)k_fwd<64, 6>, (const void*)k_fwd<128, 6>, (const void*)k_fwd<256, 6>,
+                              (const void*)k_bwd<64, 6>, (const void*)k_bwd<128, 6>, (const void*)k_bwd<256, 6>})
             AA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
     // algorithmic bytes of one solve: the factor once per sweep (dense triangles + boundary
     // blocks, fp64), b/y/x (24 B per node each way) and the update vectors (write + read)
     bytes_ = 2.0 * 8.0 * (dense + offd) + 4.0 * 24.0 * piv + 3.0 * 24.0 * bsum;
+    bytes2_ = 2.0 * 8.0 * (dense + offd) + 2.0 * (4.0 * 24.0 * piv + 3.0 * 24.0 * bsum);
     AA_HIP(hipStreamSynchronize(s));
 }
 
-void DirectSolver::solve(double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
+void DirectSolver::solve(const double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
+    solve_nr<3>(b, x, nullptr, nullptr, ctrl, gate_reject, s);
+}
+
+void DirectSolver::solve2(const double* b0, double* x0, const double* b1, double* x1, const Ctrl* ctrl, int gate_reject,
+                          hipStream_t s) {
+    if (max_sets_ < 2) throw Error(ERR_STATE, "DirectSolver::solve2 needs build(..., max_sets = 2)");
+    solve_nr<6>(b0, x0, b1, x1, ctrl, gate_reject, s);
+}
+
+template <int NR>
+void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, double* x1, const Ctrl* ctrl,
+                            int gate_reject, hipStream_t s) {
+    constexpr int K = NR / 3;
     const Task* T = tasks_.p;
-#define SUBF(BL) hipLaunchKernelGGL(k_fwd_sub<BL>, dim3(n_sub_), dim3(BL), sub_lds_f_, s, sub_trees_.p, sub_levels_.p, \
-                                    sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b, Y_.p, U_.p, ctrl, gate_reject)
+#define SUBF(BL) hipLaunchKernelGGL((k_fwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_f_, s, sub_trees_.p, \
+                                    sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
     if (n_sub_) switch (sub_block_) { case 1024: SUBF(1024); break; case 512: SUBF(512); break; default: SUBF(256); break; }
 #undef SUBF
     for (auto& L : levels_) {
-        if (L.asm_count)
-            hipLaunchKernelGGL(k_asm, dim3(L.asm_count), dim3(256), 0, s, T, L.asm_first, ell_.p, b, U_.p, Fg_.p, ctrl, gate_reject);
-#define FWD(BL) hipLaunchKernelGGL(k_fwd<BL>, dim3(L.fwd_count), dim3(BL), L.lds_fwd, s, T, L.fwd_first, Gr_.p, Gc_.p, ell_.p, b, Y_.p, U_.p, Fg_.p, ctrl, gate_reject)
+#define FWD(BL) hipLaunchKernelGGL((k_fwd<BL, NR>), dim3(L.fwd_count), dim3(BL), K * L.lds_fwd, s, T, L.fwd_first, Gc_.p, \
+                                   ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
-        if (L.ft_count) {
-            hipLaunchKernelGGL(k_fwd_tile, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b,
-                               bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
-        }
 #undef FWD
+        if (L.ft_count)
+            hipLaunchKernelGGL(k_fwd_tile<NR>, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b0, b1,
+                               bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
     }
     // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
     // and in the update vectors); their sum over the GPUs is the full forward result. When the
     // solve is gated off the stale rows are summed too -- harmless, the next forward rewrites
     // them and the backward sweep is gated alike on every GPU.
     if (comm_ && top_beg_ < n_)
-        comm_->allreduce_sum(Y_.p + 3 * (size_t)top_beg_, Y_.p + 3 * (size_t)top_beg_, 3 * (size_t)(n_ - top_beg_), s);
+        comm_->allreduce_sum(Y_.p + NR * (size_t)top_beg_, Y_.p + NR * (size_t)top_beg_, NR * (size_t)(n_ - top_beg_), s);
     for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
         const Level& L = *it;
-#define BWD(BL) hipLaunchKernelGGL(k_bwd<BL>, dim3(L.bwd_count), dim3(BL), L.lds_bwd, s, T, L.bwd_first, Gr_.p, Gc_.p, bnd_.p, Y_.p, x, ctrl, gate_reject)
+#define BWD(BL) hipLaunchKernelGGL((k_bwd<BL, NR>), dim3(L.bwd_count), dim3(BL), K * L.lds_bwd, s, T, L.bwd_first, Gr_.p, \
+                                   bnd_.p, Y_.p, x0, x1, ctrl, gate_reject)
         if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
-        if (L.bt_count) {
-            hipLaunchKernelGGL(k_bwd_tile, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p, x,
-                               bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
-        }
+        if (L.bt_count)
+            hipLaunchKernelGGL(k_bwd_tile<NR>, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p,
+                               x0, x1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
     }
-#define SUBB(BL) hipLaunchKernelGGL(k_bwd_sub<BL>, dim3(n_sub_), dim3(BL), sub_lds_b_, s, sub_trees_.p, sub_levels_.p, \
-                                    sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x, ctrl, gate_reject)
+#define SUBB(BL) hipLaunchKernelGGL((k_bwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_b_, s, sub_trees_.p, \
+                                    sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, \
+                                    ctrl, gate_reject)
     if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }
 #undef SUBB
     AA_CHECK_LAUNCH();

@@ -15,7 +15,8 @@
 // large ones are spread over many workgroups (wave per row, lanes across the row). Every
 // product reads a coalesced copy of G_s (row-major for lane-across-row, column-major for
 // thread-per-row); sums are in a fixed order (no atomics): deterministic. Three right-hand
-// sides (x, y, z coordinates) are processed together.
+// sides (x, y, z coordinates) are processed together -- or six: solve2() runs two independent
+// solves in one pass over the factor (bit-identical to two solve() calls).
 #pragma once
 #include <vector>
 
@@ -36,23 +37,28 @@ public:
     // (-1 = shared top separator, rows [top_beg, n)); only the supernodes of `my_part` and of
     // the top are stored and solved here, and the top rows of the forward result are summed
     // over the GPUs between the two sweeps.
+    // max_sets = 2 sizes the workspaces and the fused subtrees' LDS budget for solve2().
     void build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part = nullptr, int my_part = -1,
-               int top_beg = -1, Comm* comm = nullptr);
+               int top_beg = -1, Comm* comm = nullptr, int max_sets = 1);
     // x (n x 3, stride 3 doubles) = A^-1 b ; b is read only. gate: skip when ctrl->done (or !reject).
-    void solve(double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s);
+    void solve(const double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s);
+    // x0 = A^-1 b0 and x1 = A^-1 b1 in one pass (needs build(..., max_sets = 2))
+    void solve2(const double* b0, double* x0, const double* b1, double* x1, const Ctrl* ctrl, int gate_reject,
+                hipStream_t s);
     int n() const { return n_; }
     size_t nnz_L() const { return nnz_L_; }
     double bytes_per_solve() const { return bytes_; }
+    double bytes_per_solve2() const { return bytes2_; }
     int kernels_per_solve() const { return kernels_; }
 
     // One workgroup's share of a level: rows [r0, r0 + nr) of supernode `node` (forward) or
-    // its columns (backward). mode 0: thread per row, 1: wave per row. The supernode's
-    // metadata rides along so a workgroup needs one (scalar) load before its first product.
+    // its columns (backward), a thread per row. The supernode's metadata rides along so a
+    // workgroup needs one (scalar) load before its first product.
     struct Task {
-        int node, r0, nr, mode;
+        int node, r0, nr, pad0;
         int p, nb, beg, bnd_off;
         int ell_w, ldr, pad1, pad2;   // ldr: row stride of the row-major G (p padded to even)
-        long long goff, uoff, foff, ell_off;
+        long long goff, uoff, ell_off, pad3;
     };
 
     // Bottom subtrees (all supernodes up to a cut height) are solved whole by one workgroup
@@ -75,7 +81,6 @@ public:
 private:
     struct Level {
         int fwd_first = 0, fwd_count = 0, bwd_first = 0, bwd_count = 0;
-        int asm_first = 0, asm_count = 0;     // assembly tasks of the wave-mode supernodes
         int bt_first = 0, bt_count = 0, br_first = 0, br_count = 0;   // split-K backward tiles
         int ft_first = 0, ft_count = 0, fr_first = 0, frd_count = 0;  // split-K forward tiles
         int fblock = 256, bblock = 256, lds_fwd = 0, lds_bwd = 0;
@@ -83,10 +88,14 @@ private:
     int n_ = 0, nn_ = 0, kernels_ = 0, top_beg_ = 0;
     Comm* comm_ = nullptr;
     size_t nnz_L_ = 0;
-    double bytes_ = 0;
+    double bytes_ = 0, bytes2_ = 0;
+    int max_sets_ = 1;
+    template <int NR>
+    void solve_nr(const double* b0, double* x0, const double* b1, double* x1, const Ctrl* ctrl, int gate_reject,
+                  hipStream_t s);
     DevBuf<int> bnd_;
     DevBuf<long long> ell_;   // per front row, ell_w pull offsets into U (-1 = none)
-    DevBuf<double> Gr_, Gc_, Y_, U_, Fg_;
+    DevBuf<double> Gr_, Gc_, Y_, U_;
     DevBuf<Task> tasks_;
     DevBuf<BTile> btiles_;
     DevBuf<BRed> breds_;

@@ -271,7 +271,11 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     } catch (const std::runtime_error& e) {
         throw Error(ERR_NUMERIC, e.what());
     }
-    solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_);
+    // Z variant with Anderson: the combined-residual solve is batched with the next iteration's
+    // solve (enqueue_iteration_z); AA_Z_PIPELINE=0 restores the sequential order
+    pipe_z_ = st_.variant == AA_VARIANT_Z && st_.acceleration_type == 1;
+    if (const char* e = std::getenv("AA_Z_PIPELINE")) pipe_z_ = pipe_z_ && e[0] != '0';
+    solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_, pipe_z_ ? 2 : 1);
 
     // ---- element ownership (partitioned): an element touching a node of part r belongs to
     // rank r (it cannot touch another part: the separators split the mesh); elements whose free
@@ -388,7 +392,8 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     mass_.upload(ms, s());
     xfull_.alloc(3 * (size_t)n); xlast_.alloc(3 * (size_t)n); cxfull_.alloc(3 * (size_t)n);
     xfull_.zero(s()); xlast_.zero(s()); cxfull_.zero(s());
-    xbar_.alloc(3 * (size_t)nf_); Mxbar_.alloc(3 * (size_t)nf_); b_.alloc(3 * (size_t)nf_); dx_.alloc(3 * (size_t)nf_);
+    xbar_.alloc(3 * (size_t)nf_); Mxbar_.alloc(3 * (size_t)nf_); b_.alloc(3 * (size_t)nf_);
+    if (pipe_z_) b2_.alloc(3 * (size_t)nf_); dx_.alloc(3 * (size_t)nf_);
     z_.alloc(Z_); u_.alloc(Z_); y_.alloc(3 * std::max<long long>(1, Yslots_)); du_.alloc(Z_);
     if (st_.variant == AA_VARIANT_Z) { dz_.alloc(Z_); lastz_.alloc(Z_); cz_.alloc(Z_); }
     // residual block partials [a | b], padded to the largest rank's block count (zeros beyond
@@ -437,7 +442,8 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     }
     kstats_["local_z"].bytes = lz + 24.0 * n;
     kstats_["resid"].bytes = rs + 48.0 * n;
-    kstats_["solve"].bytes = solver_.bytes_per_solve();
+    kstats_["solve"].bytes = pipe_z_ ? solver_.bytes_per_solve2() : solver_.bytes_per_solve();
+    kstats_["solve1"].bytes = solver_.bytes_per_solve();
     kstats_["rhs"].bytes = 24.0 * (double)Yslots_ + 4.0 * nf_ + 48.0 * nf_;   // 3 doubles per slot; ptr, Mxbar, b
     // Z variant: u = W^-1 grad E(z) and the vertex slots (reads idx, G, w, z; writes u, slots),
     // prim (reads idx, G, w, z, u; writes block partials)
@@ -613,18 +619,42 @@ void ElasticSolver::enqueue_iteration_ux(bool accel) {
 }
 
 // admm_anderson_xzu/src/Solver.cpp:122-251
-void ElasticSolver::enqueue_iteration_z(bool accel) {
+//
+// Pipelined combined residual (pipe_z_): the "for drawing figures" pass of iteration k
+// (Solver.cpp:217-233: x_c = A^-1 b(default_z_k, u_k), z_c = update_z(x_c), comb_k) needs a
+// solve that does not depend on iteration k+1, and iteration k+1's main solve does not depend
+// on it -- so the two run as one two-set solve (DirectSolver::solve2, the factor streamed once).
+// comb_k's update_z / residual / break test follow that solve, before iteration k+1 records or
+// changes anything the test depends on: its inputs are default_z (dz_), default_u (du_, equal
+// to curr_u_k: the Anderson step leaves u alone) and x_c, none of which iteration k+1 writes
+// before that point. A break at comb_k (done = 2) rolls back the one speculative write that
+// survives the step, x (restored from default_x = curr_x_k); everything after is gated off.
+// The last iteration's pass runs alone (enqueue_comb_tail_z). Results are bit-identical to
+// the unpipelined order (same kernels, same operands; the batched solve sums each column in
+// the same order).
+void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
     const long long nx = 3LL * nf_;
     Ctrl* c = ctrl_.p;
+    const bool pipe = accel && pipe_z_;
     ev_begin("grad");
     for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, accel ? 1 : 0, 0, c, s());
     ev_end("grad");
     ev_begin("rhs");
     launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
     ev_end("rhs");
-    ev_begin("solve");
-    solver_.solve(b_.p, xfull_.p, c, 0, s());
-    ev_end("solve");
+    if (pipe && it > 0) {
+        ev_begin("solve");
+        solver_.solve2(b_.p, xfull_.p, b2_.p, cxfull_.p, c, 0, s());
+        ev_end("solve");
+        ev_begin("comb");
+        comb_finish_z(CTL_COMB_ZP);
+        launch_copy(xfull_.p, dx_.p, nx, c, 2, s());   // break at comb_{k-1}: x back to curr_x_{k-1}
+        ev_end("comb");
+    } else {
+        ev_begin(pipe ? "solve1" : "solve");
+        solver_.solve(b_.p, xfull_.p, c, 0, s());
+        ev_end(pipe ? "solve1" : "solve");
+    }
     auto prim_all = [&](const double* xf, const double* z, const double* zref, int redo) {
         int off = 0;
         for (auto& g : groups_) {
@@ -654,7 +684,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         launch_copy(dx_.p, xfull_.p, nx, c, 0, s());
         launch_copy(du_.p, u_.p, Z_, c, 0, s());
         // default_z = update_z(curr_x, curr_u) (Solver.cpp:196-199); the same pass writes the
-        // rhs slots of the combined-residual solve below, w (w default_z + C - curr_u)
+        // rhs slots of the combined-residual solve, w (w default_z + C - curr_u)
         // (Solver.cpp:220): curr_u is final for this iteration and the AA step does not touch it
         ev_begin("local_z");
         local_z_all(xfull_.p, u_.p, dz_.p, y_.p, LZ_NORMAL, false);
@@ -669,21 +699,58 @@ void ElasticSolver::enqueue_iteration_z(bool accel) {
         launch_aa_mix(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, out, m, s());
         ev_end("aa");
         // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
+        if (pipe) {   // its rhs now (the next iteration overwrites the slots); the rest next iteration
+            ev_begin("rhs");
+            launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b2_.p, c, 0, s());
+            ev_end("rhs");
+            return;
+        }
         ev_begin("comb");
         launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
         solver_.solve(b_.p, cxfull_.p, c, 0, s());
-        local_z_all(cxfull_.p, u_.p, cz_.p, nullptr, LZ_NORMAL, false);
-        prim_all(cxfull_.p, cz_.p, dz_.p, 0);
+        comb_finish_z(CTL_COMB_Z);
         ev_end("comb");
-    } else {
-        launch_copy(lastz_.p, z_.p, Z_, c, 0, s());
-        ev_begin("local_z");
-        local_z_all(xfull_.p, u_.p, z_.p, nullptr, LZ_NORMAL, false);
-        ev_end("local_z");
-        prim_all(xfull_.p, z_.p, lastz_.p, 0);
+        return;
     }
+    launch_copy(lastz_.p, z_.p, Z_, c, 0, s());
+    ev_begin("local_z");
+    local_z_all(xfull_.p, u_.p, z_.p, nullptr, LZ_NORMAL, false);
+    ev_end("local_z");
+    prim_all(xfull_.p, z_.p, lastz_.p, 0);
     reduce_partials();
     launch_control(CTL_COMB_Z, c, ga_, gb_, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+}
+
+// comb pass after its solve: z_c = update_z(x_c, curr_u) into cz_, dual = W (z_c - default_z),
+// prim = D x_c - W z_c - C, comb = |prim|^2 + |dual|^2 and the break test (Solver.cpp:224-246).
+// Reads du_ (= curr_u of the iteration the pass belongs to) -- also when pipelined, where u_
+// already holds the next iteration's u.
+void ElasticSolver::comb_finish_z(int op) {
+    Ctrl* c = ctrl_.p;
+    local_z_all(cxfull_.p, du_.p, cz_.p, nullptr, LZ_NORMAL, false);
+    int off = 0;
+    for (auto& g : groups_) {
+        launch_prim_z(g.d, cxfull_.p, cz_.p, dz_.p, nf_, 0, c, pa_, pb_, off, s());
+        off += blocks_for(g.d.count);
+    }
+    reduce_partials();
+    launch_control(op, c, ga_, gb_, nbg_, 1, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+}
+
+// the last iteration's combined-residual pass (pipelined Z variant)
+void ElasticSolver::enqueue_comb_tail_z() {
+    ev_begin("comb");
+    solver_.solve(b2_.p, cxfull_.p, ctrl_.p, 0, s());
+    comb_finish_z(CTL_COMB_Z);
+    ev_end("comb");
+}
+
+void ElasticSolver::enqueue_iterations(int iters, bool accel) {
+    for (int it = 0; it < iters; ++it) {
+        if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
+        else enqueue_iteration_z(accel, it);
+    }
+    if (st_.variant != AA_VARIANT_UX && accel && pipe_z_ && iters > 0) enqueue_comb_tail_z();
 }
 
 void ElasticSolver::epilogue_enqueue(bool accel) {
@@ -721,19 +788,13 @@ void ElasticSolver::step() {
     if (use_graph_ && st_.admm_iters > 0) {
         if (!gexec_) {   // pointers and control flow are fixed after initialize: capture once
             AA_HIP(hipStreamBeginCapture(s(), hipStreamCaptureModeThreadLocal));
-            for (int it = 0; it < st_.admm_iters; ++it) {
-                if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
-                else enqueue_iteration_z(accel);
-            }
+            enqueue_iterations(st_.admm_iters, accel);
             AA_HIP(hipStreamEndCapture(s(), &graph_));
             AA_HIP(hipGraphInstantiate(&gexec_, graph_, nullptr, nullptr, 0));
         }
         AA_HIP(hipGraphLaunch(gexec_, s()));
     } else {
-        for (int it = 0; it < st_.admm_iters; ++it) {
-            if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
-            else enqueue_iteration_z(accel);
-        }
+        enqueue_iterations(st_.admm_iters, accel);
     }
     epilogue_enqueue(accel);
     gather_state(xs_);
@@ -779,10 +840,7 @@ double ElasticSolver::bench_iterations(int iters) {
     hipEvent_t e0, e1;
     AA_HIP(hipEventCreate(&e0)); AA_HIP(hipEventCreate(&e1));
     AA_HIP(hipEventRecord(e0, s()));
-    for (int it = 0; it < iters; ++it) {
-        if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
-        else enqueue_iteration_z(accel);
-    }
+    enqueue_iterations(iters, accel);
     AA_HIP(hipEventRecord(e1, s()));
     AA_HIP(hipEventSynchronize(e1));
     instrument_ = false;

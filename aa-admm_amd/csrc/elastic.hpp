@@ -81,7 +81,7 @@ private:
     std::vector<DevGroup> groups_;
     DirectSolver solver_;
     DevBuf<int> dt_ptr_;
-    DevBuf<double> xs_, vs_, mass_, xfull_, xlast_, xbar_, Mxbar_, b_, cxfull_;
+    DevBuf<double> xs_, vs_, mass_, xfull_, xlast_, xbar_, Mxbar_, b_, b2_, cxfull_;
     DevBuf<double> z_, u_, y_, du_, dz_, dx_, lastz_, cz_;
     DevBuf<double> aa_cur_, aa_dF_, aa_dG_, aa_red_, aa_red_g_;
     // residual block partials: this rank's [a | b] (pa_, pb_) and their sums over the ranks
@@ -111,6 +111,7 @@ private:
     hipGraph_t graph_ = nullptr;
     hipGraphExec_t gexec_ = nullptr;
     bool use_graph_ = true;
+    bool pipe_z_ = false;   // Z variant + Anderson: comb solve batched with the next solve
     void drop_graph();
 
     // kernel-class event timing (bench only)
@@ -123,7 +124,10 @@ private:
     void upload_pins();
     void prologue();
     void enqueue_iteration_ux(bool accel);
-    void enqueue_iteration_z(bool accel);
+    void enqueue_iteration_z(bool accel, int it);
+    void comb_finish_z(int op);
+    void enqueue_comb_tail_z();
+    void enqueue_iterations(int iters, bool accel);
     void epilogue_enqueue(bool accel);
     void fetch_results();
     int nb_elems() const { return red_blocks_; }

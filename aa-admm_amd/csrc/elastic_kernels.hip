@@ -424,14 +424,17 @@ __global__ __launch_bounds__(kBlock) void k_control(int op, Ctrl* ctrl, const do
             ctrl->nrec = k + 1;
             break;
         }
-        case CTL_COMB_Z: {
+        case CTL_COMB_Z:
+        case CTL_COMB_ZP: {
             const double comb = a + b;
             ctrl->iters_run += 1;
             ctrl->comb = comb;
             const int k = ctrl->nrec;
             if (k < ctrl->cap) { hist_prim[k] = ctrl->prim; hist_comb[k] = comb; hist_rej[k] = ctrl->reject; }
             ctrl->nrec = k + 1;
-            if (comb < kCombEps) ctrl->done = 1;
+            // ZP: decided one iteration late (pipelined): done = 2 asks for the speculative
+            // next iteration's x to be rolled back (launch_copy gate 2)
+            if (comb < kCombEps) ctrl->done = op == CTL_COMB_ZP ? 2 : 1;
             break;
         }
     }
@@ -439,7 +442,11 @@ __global__ __launch_bounds__(kBlock) void k_control(int op, Ctrl* ctrl, const do
 
 __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ dst, const double* __restrict__ src,
                                                  long long n, const Ctrl* ctrl, int gate_reject) {
-    if (gated(ctrl, gate_reject)) return;
+    if (gate_reject == 2) {   // only after a pipelined break (CTL_COMB_ZP)
+        if (!ctrl || ctrl->done != 2) return;
+    } else if (gated(ctrl, gate_reject)) {
+        return;
+    }
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
         dst[i] = src[i];
 }

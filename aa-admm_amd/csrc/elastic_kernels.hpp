@@ -83,7 +83,7 @@ void launch_restore_ux(double* u, double* x, double* cur, const double* du, cons
                        long long nx, const Ctrl* ctrl, hipStream_t s);
 // control steps
 enum CtlOp { CTL_PRIM_CHECK = 0, CTL_PRIM_FINAL = 1, CTL_COMB_UX = 2, CTL_PRIM_CHECK_Z = 3, CTL_PRIM_FINAL_Z = 4,
-             CTL_COMB_Z = 5 };
+             CTL_COMB_Z = 5, CTL_COMB_ZP = 6 };
 void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b, int nblocks, int accel,
                     double* hist_prim, double* hist_comb, int* hist_rej, hipStream_t s);
 // dst = src (gate: !done, and reject if gate_reject)

@@ -3,6 +3,8 @@ the oracle. Tolerances: residual curves judged relative to comb
 time step over the recorded iterations -- closed-form element paths (tri, linear tet) 1e-9,
 L-BFGS prox paths (NeoHookean / StVK) 1e-6 -- final positions 1e-9 / 1e-6 relative, and the
 Anderson reject flags must agree over the first 20 iterations."""
+import dataclasses
+
 import numpy as np
 import pytest
 
@@ -106,3 +108,24 @@ def test_gpu_full_size_drop_c4(pkg, ctx):
     assert abs(vbar[1] - g_dt) <= 1e-9 * abs(g_dt), vbar
     assert abs(vbar[0]) <= 1e-9 * abs(g_dt) and abs(vbar[2]) <= 1e-9 * abs(g_dt), vbar
     assert h["comb"][-1] < 1e-4 * h["comb"][0], (h["comb"][0], h["comb"][-1])
+
+
+@pytest.mark.parametrize("builder", [
+    lambda: scenes.tet_drop(12, 4, 6, iters=40, n_steps=2),                       # no break
+    lambda: dataclasses.replace(scenes.tet_drop(4, 2, 2, squash=1.0, iters=30, n_steps=2), gravity=0.0),
+    lambda: dataclasses.replace(scenes.tet_drop(6, 2, 3, squash=0.98, iters=200, n_steps=1), gravity=0.0),
+    lambda: scenes.beams(2, iters=40, n_steps=2, variant=scenes.VARIANT_X),      # rejects
+])
+def test_gpu_z_pipelined_comb_bit_identical(builder, pkg, ctx, monkeypatch):
+    """Z variant + Anderson: the combined-residual solve batched with the next iteration's solve
+    (two-set DirectSolver::solve2, break decided one iteration late and x rolled back) gives
+    bit-identical histories and positions to the sequential order (AA_Z_PIPELINE=0) -- including
+    runs that stop at comb < 1e-20 (Solver.cpp:243-246) early or mid-step."""
+    sc = builder()
+    monkeypatch.setenv("AA_Z_PIPELINE", "0")
+    seq, _ = pkg.capi.run_scene(ctx, sc)
+    monkeypatch.setenv("AA_Z_PIPELINE", "1")
+    pipe, _ = pkg.capi.run_scene(ctx, sc)
+    for a, b in zip(seq, pipe):
+        for k in ("prim", "comb", "reject", "x", "v"):
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
