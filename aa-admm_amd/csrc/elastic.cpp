@@ -411,7 +411,9 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     if (accel) {
         const int m = st_.anderson_m;
         const long long dim = st_.variant == AA_VARIANT_UX ? Z_ + 3LL * nf_ : Z_;
-        aa_cur_.alloc(dim);
+        // the Z variant mixes z in place: the accelerator's current iterate is z itself (z == the
+        // last Anderson output or, after a reject, default_z -- accelerator.replace)
+        if (st_.variant == AA_VARIANT_UX) aa_cur_.alloc(dim);
         aa_dF_.alloc((size_t)m * Z_); aa_dF_.zero(s());
         aa_dG_.alloc((size_t)m * dim); aa_dG_.zero(s());
         // same grid on every rank (the largest rank's) so the partial layouts line up
@@ -569,7 +571,7 @@ void ElasticSolver::prologue() {
         launch_copy(dz_.p, z_.p, Z_, nullptr, 0, s());
         launch_copy(dx_.p, xfull_.p, nx, nullptr, 0, s());
         launch_copy(du_.p, u_.p, Z_, nullptr, 0, s());
-        if (accel) launch_copy(aa_cur_.p, z_.p, Z_, nullptr, 0, s());
+        // (Z variant: the accelerator's current iterate is z_ itself)
     }
 }
 
@@ -671,7 +673,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         launch_copy(u_.p, du_.p, Z_, c, 1, s());
         launch_copy(xfull_.p, dx_.p, nx, c, 1, s());
         launch_copy(z_.p, dz_.p, Z_, c, 1, s());
-        launch_copy(aa_cur_.p, dz_.p, Z_, c, 1, s());   // accelerator.replace(curr_z)
+        // accelerator.replace(curr_z): the accelerator's iterate is z_ (restored above)
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 0, 1, c, s());
         launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());
         solver_.solve(b_.p, xfull_.p, c, 1, s());
@@ -693,10 +695,10 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         Seg2 out{z_.p, Z_, nullptr, 0};
         Seg2 none{nullptr, 0, nullptr, 0};
         ev_begin("aa");
-        launch_aa_reduce(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, none, m, s());
+        launch_aa_reduce(G, z_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, none, m, s());
         reduce_aa();
         launch_aa_solve(c, aag_, aa_blocks_, m, s());
-        launch_aa_mix(G, aa_cur_.p, Z_, aa_dF_.p, aa_dG_.p, c, out, m, s());
+        launch_aa_mix(G, z_.p, Z_, aa_dF_.p, aa_dG_.p, c, out, m, s());   // in place (out == cur)
         ev_end("aa");
         // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
         if (pipe) {   // its rhs now (the next iteration overwrites the slots); the rest next iteration

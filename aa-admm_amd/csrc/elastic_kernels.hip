@@ -387,11 +387,13 @@ __global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ 
 }
 
 // ------------------------------------------------------------------ control (one block)
-__global__ __launch_bounds__(kBlock) void k_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b,
+// 1024 threads: the kernel is latency-bound on summing a few thousand block partials
+constexpr int kCtlBlock = 1024;
+__global__ __launch_bounds__(kCtlBlock) void k_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b,
                                                     int nb, int accel, double* hist_prim, double* hist_comb,
                                                     int* hist_rej) {
     if (ctrl->done) return;
-    __shared__ double sm[kBlock / 64];
+    __shared__ double sm[kCtlBlock / 64];
     double a = 0, b = 0;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) { a += red_a[i]; if (red_b) b += red_b[i]; }
     a = block_sum(a, sm);
@@ -522,7 +524,9 @@ __global__ __launch_bounds__(kBlock) void k_finalize(int n, int nf, const double
 __device__ __forceinline__ double seg_get(const Seg2& s, long long i) { return i < s.na ? s.a[i] : s.b[i - s.na]; }
 __device__ __forceinline__ void seg_set(const Seg2& s, long long i, double v) { if (i < s.na) s.a[i] = v; else s.b[i - s.na] = v; }
 
-// pass 1: dF_j += F, dG_j += G and the partial sums for |dF_j|^2, dF_j.F, dF_j.dF_c, dF_c.F
+// pass 1: the partial sums for |dF_j|^2, dF_j.F, dF_j.dF_c, dF_c.F with dF_j = dF_j + F formed on
+// the fly (read only: k_aa_mix forms dF_j + F and dG_j + G again and stores them, so the history
+// columns are written once per iteration; the arithmetic is unchanged)
 template <int MM>
 __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __restrict__ cur, long long eff,
                                                       double* __restrict__ dF, double* __restrict__ dG, Ctrl* ctrl,
@@ -557,25 +561,27 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < dim; i += (long long)gridDim.x * blockDim.x) {
         const double g = seg_get(G, i);
         if (copy_to.a) seg_set(copy_to, i, g);
-        if (iter == 0) continue;
-        dG[(size_t)col * dim + i] += g;
-        if (i < eff) {
-            const double f = g - cur[i];
-            const double dfj = dF[(size_t)col * eff + i] + f;
-            dF[(size_t)col * eff + i] = dfj;
-            if (i >= G.na) {
-                const long long j = i - G.na;
-                if (!((j >= mask.lo1 && j < mask.hi1) || (j >= mask.lo2 && j < mask.hi2))) continue;
-            }
-            acc[0] += dfj * dfj;
-            acc[1] += dfj * f;
+        if (iter == 0 || i >= eff) continue;
+        // every load of the element first (cur, dF_j, the other history columns), then the
+        // products: a load used right away serialises the loop on its latency
+        const double ci = cur[i];
+        const double dfo = dF[(size_t)col * eff + i];
+        double dfc[MM];
 #pragma unroll
-            for (int c = 0; c < MM; ++c) {
-                if (c < mk && c != col) {
-                    const double dfc = dF[(size_t)c * eff + i];
-                    acc[2 + c] += dfj * dfc;
-                    acc[2 + MM + c] += dfc * f;
-                }
+        for (int c = 0; c < MM; ++c) dfc[c] = (c < mk && c != col) ? dF[(size_t)c * eff + i] : 0.0;
+        if (i >= G.na) {
+            const long long j = i - G.na;
+            if (!((j >= mask.lo1 && j < mask.hi1) || (j >= mask.lo2 && j < mask.hi2))) continue;
+        }
+        const double f = g - ci;
+        const double dfj = dfo + f;
+        acc[0] += dfj * dfj;
+        acc[1] += dfj * f;
+#pragma unroll
+        for (int c = 0; c < MM; ++c) {
+            if (c < mk && c != col) {
+                acc[2 + c] += dfj * dfc[c];
+                acc[2 + MM + c] += dfc[c] * f;
             }
         }
     }
@@ -738,11 +744,13 @@ __device__ void cod_solve_block(int n, CodLds& S, const double* b, double* x) {
 #undef QR
 }
 
+// 1024 threads: summing up to 2048 x NVAL block partials is latency-bound
+constexpr int kSolveBlock = 1024;
 template <int MM>
-__global__ __launch_bounds__(kBlock) void k_aa_solve(Ctrl* ctrl, const double* red, int nb) {
+__global__ __launch_bounds__(kSolveBlock) void k_aa_solve(Ctrl* ctrl, const double* red, int nb) {
     if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
     constexpr int NVAL = 2 + 2 * MM;
-    constexpr int NCH = kBlock / NVAL;          // block partials are split into NCH chunks per value
+    constexpr int NCH = kSolveBlock / NVAL;     // block partials are split into NCH chunks per value
     __shared__ double tot[NVAL];
     __shared__ double part[NCH * NVAL];
     const int iter = ctrl->aa_iter;
@@ -778,33 +786,47 @@ __global__ __launch_bounds__(kBlock) void k_aa_solve(Ctrl* ctrl, const double* r
     const int mk = iter < m ? iter : m;
     const double eps = 1e-14;
     const double s = fmax(eps, sqrt(tot[0]));
+    // the normal-equation matrix and the column scales live in Ctrl (device memory) between
+    // iterations; they are staged through LDS here so the serial parts below never wait on a
+    // global load (thread 0 reading back what it just stored cost ~25 us per call)
+    __shared__ double sM[kMaxM * kMaxM], ssc[kMaxM];
+    for (int q = threadIdx.x; q < mk * mk; q += blockDim.x) sM[(q / mk) * m + q % mk] = ctrl->M[(q / mk) * m + q % mk];
+    if ((int)threadIdx.x < mk) ssc[threadIdx.x] = ctrl->scale[threadIdx.x];
+    __syncthreads();
     if (threadIdx.x == 0) {
-        ctrl->scale[col] = s;
+        ssc[col] = s;
         if (mk == 1) {
             sx[0] = 0;
             const double sq = tot[0] / (s * s);
-            ctrl->M[0] = sq;
+            sM[0] = sq;
             const double dn = sqrt(sq);
             if (dn > eps) sx[0] = (tot[1] / s) / (dn * dn);
         } else {
             for (int c = 0; c < mk; ++c) {
                 if (c == col) continue;
                 const double v = tot[2 + c] / s;
-                ctrl->M[c * m + col] = v;
-                ctrl->M[col * m + c] = v;
+                sM[c * m + col] = v;
+                sM[col * m + c] = v;
                 sb[c] = tot[2 + MM + c];
             }
-            ctrl->M[col * m + col] = tot[0] / (s * s);
+            sM[col * m + col] = tot[0] / (s * s);
             sb[col] = tot[1] / s;
             for (int c = 0; c < mk; ++c)
-                for (int r = 0; r < mk; ++r) S.A[c * mk + r] = ctrl->M[c * m + r];
+                for (int r = 0; r < mk; ++r) S.A[c * mk + r] = sM[c * m + r];
         }
         s_mk = mk;
     }
     __syncthreads();
     if (s_mk > 1) cod_solve_block(s_mk, S, sb, sx);
+    // write back in parallel: row/column col of M, scale[col], the coefficients
+    if ((int)threadIdx.x < mk) {
+        const int c = threadIdx.x;
+        ctrl->M[c * m + col] = sM[c * m + col];
+        ctrl->M[col * m + c] = sM[col * m + c];
+        ctrl->coef[c] = sx[c] / ssc[c];
+        if (c == col) ctrl->scale[col] = s;
+    }
     if (threadIdx.x != 0) return;
-    for (int c = 0; c < mk; ++c) ctrl->coef[c] = sx[c] / ctrl->scale[c];
     ctrl->aa_first = 0;
     ctrl->aa_j = col;
     ctrl->aa_jn = (col + 1) % m;
@@ -814,35 +836,49 @@ __global__ __launch_bounds__(kBlock) void k_aa_solve(Ctrl* ctrl, const double* r
     ctrl->aa_iter = iter + 1;
 }
 
-// pass 2: u = G - dG theta/scale, normalise dF_j, start the next column with -F / -G
+// pass 2: dG_j += G, dF_j = (dF_j + F) / scale, u = G - dG theta/scale, start the next column with
+// -F / -G. With out.a == cur (the Z variant mixes z in place) the output is written once.
 template <int MM>
-__global__ __launch_bounds__(kBlock) void k_aa_mix(Seg2 G, double* __restrict__ cur, long long eff,
+__global__ __launch_bounds__(kBlock) void k_aa_mix(Seg2 G, double* cur, long long eff,
                                                    double* __restrict__ dF, double* __restrict__ dG, Ctrl* ctrl,
                                                    Seg2 out) {
     if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
     const long long dim = G.na + G.nb;
     const int first = ctrl->aa_first, j = ctrl->aa_j, jn = ctrl->aa_jn, mk = ctrl->aa_mk;
     const double s = ctrl->aa_s;
+    const bool inplace = out.a == cur && out.nb == 0;
     double coef[MM];
 #pragma unroll
     for (int c = 0; c < MM; ++c) coef[c] = c < mk ? ctrl->coef[c] : 0.0;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < dim; i += (long long)gridDim.x * blockDim.x) {
+        // loads first (G, cur, dF_j, the dG columns), then the arithmetic and the stores
         const double g = seg_get(G, i);
-        const double f = i < eff ? g - cur[i] : 0.0;
+        const bool in_eff = i < eff;
+        const double ci = in_eff ? cur[i] : 0.0;
+        const double dfo = (!first && in_eff) ? dF[(size_t)j * eff + i] : 0.0;
+        double dgc[MM];
+#pragma unroll
+        for (int c = 0; c < MM; ++c) dgc[c] = (!first && c < mk) ? dG[(size_t)c * dim + i] : 0.0;
+        const double f = in_eff ? g - ci : 0.0;
         double res;
         if (first) {
             res = g;
         } else {
-            double acc = 0;
+            double acc = 0, dgj = 0;
 #pragma unroll
             for (int c = 0; c < MM; ++c)
-                if (c < mk) acc += dG[(size_t)c * dim + i] * coef[c];
+                if (c < mk) {
+                    double d = dgc[c];
+                    if (c == j) { d += g; dgj = d; }
+                    acc += d * coef[c];
+                }
+            dG[(size_t)j * dim + i] = dgj;
             res = g - acc;
-            if (i < eff) dF[(size_t)j * eff + i] = dF[(size_t)j * eff + i] / s;
+            if (in_eff) dF[(size_t)j * eff + i] = (dfo + f) / s;
         }
         if (i < eff) dF[(size_t)jn * eff + i] = -f;
         dG[(size_t)jn * dim + i] = -g;
-        seg_set(out, i, res);
+        if (!inplace) seg_set(out, i, res);
         cur[i] = res;
     }
 }
@@ -926,7 +962,7 @@ void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const
 
 void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b, int nblocks, int accel,
                     double* hist_prim, double* hist_comb, int* hist_rej, hipStream_t s) {
-    hipLaunchKernelGGL(k_control, dim3(1), dim3(kBlock), 0, s, op, ctrl, red_a, red_b, nblocks, accel, hist_prim, hist_comb, hist_rej);
+    hipLaunchKernelGGL(k_control, dim3(1), dim3(kCtlBlock), 0, s, op, ctrl, red_a, red_b, nblocks, accel, hist_prim, hist_comb, hist_rej);
     AA_CHECK_LAUNCH();
 }
 
@@ -986,9 +1022,9 @@ void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, doub
 
 void launch_aa_solve(Ctrl* ctrl, const double* red, int nblocks, int m, hipStream_t s) {
     switch (mm_bucket(m)) {
-        case 8: hipLaunchKernelGGL(k_aa_solve<8>, dim3(1), dim3(kBlock), 0, s, ctrl, red, nblocks); break;
-        case 16: hipLaunchKernelGGL(k_aa_solve<16>, dim3(1), dim3(kBlock), 0, s, ctrl, red, nblocks); break;
-        default: hipLaunchKernelGGL(k_aa_solve<32>, dim3(1), dim3(kBlock), 0, s, ctrl, red, nblocks); break;
+        case 8: hipLaunchKernelGGL(k_aa_solve<8>, dim3(1), dim3(kSolveBlock), 0, s, ctrl, red, nblocks); break;
+        case 16: hipLaunchKernelGGL(k_aa_solve<16>, dim3(1), dim3(kSolveBlock), 0, s, ctrl, red, nblocks); break;
+        default: hipLaunchKernelGGL(k_aa_solve<32>, dim3(1), dim3(kSolveBlock), 0, s, ctrl, red, nblocks); break;
     }
     AA_CHECK_LAUNCH();
 }
