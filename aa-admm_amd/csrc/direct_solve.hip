@@ -187,7 +187,7 @@ using BTile = DirectSolver::BTile;
 using BRed = DirectSolver::BRed;
 constexpr int kBwdTileRows = 128;
 
-template <int NR>
+template <int NR, int kBwdPrefetch>
 __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tiles, int first, const double* __restrict__ Gr,
                                                   const int* __restrict__ bnd, const double* __restrict__ Y,
                                                   double* __restrict__ X0, double* __restrict__ X1,
@@ -199,19 +199,37 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
     __shared__ double red[3][W * 64];
     const BTile t = tiles[first + blockIdx.x];
     const int tid = threadIdx.x;
-    for (int i = tid; i < t.nr; i += 256) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
-    __syncthreads();
     const int lane = tid & 63, w = tid >> 6;
     const int c = t.c0 + 2 * lane;   // columns c, c+1 (c+1 may be the zero pad column)
     constexpr int per = kBwdTileRows / 4;
     const int i0 = w * per, i1 = min(i0 + per, t.nr);
+    // the first kBwdPrefetch rows of this lane's G slice are loaded before the vector slice is
+    // staged, so their latency overlaps the gathers of bwd_row and the barrier
+    const double2* G = reinterpret_cast<const double2*>(Gr + t.goff + (size_t)t.r0 * t.ldr + c);
+    const int ld2 = t.ldr / 2;
+    double2 gp[kBwdPrefetch > 0 ? kBwdPrefetch : 1];
+    if (c < t.p) {
+#pragma unroll
+        for (int q = 0; q < kBwdPrefetch; ++q)
+            if (i0 + q < i1) gp[q] = G[(size_t)(i0 + q) * ld2];
+    }
+    for (int i = tid; i < t.nr; i += 256) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
+    __syncthreads();
     double a[W];
     zero<W>(a);
     if (c < t.p) {
-        const double2* G = reinterpret_cast<const double2*>(Gr + t.goff + (size_t)t.r0 * t.ldr + c);
-        const int ld2 = t.ldr / 2;
+#pragma unroll
+        for (int q = 0; q < kBwdPrefetch; ++q) {
+            if (i0 + q >= i1) break;
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                const double vk = v[NR * (i0 + q) + k];
+                a[k] += gp[q].x * vk;
+                a[NR + k] += gp[q].y * vk;
+            }
+        }
 #pragma unroll 8
-        for (int i = i0; i < i1; ++i) {
+        for (int i = i0 + kBwdPrefetch; i < i1; ++i) {
             const double2 g = G[(size_t)i * ld2];
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
@@ -261,7 +279,7 @@ using FTile = DirectSolver::FTile;
 using FRed = DirectSolver::FRed;
 constexpr int kFwdTileCols = 128;
 
-template <int NR>
+template <int NR, int kFwdPrefetch>
 __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tiles, int first, const double* __restrict__ Gc,
                                                   const long long* __restrict__ ell, const double* __restrict__ B0,
                                                   const double* __restrict__ B1, double* __restrict__ part,
@@ -273,19 +291,33 @@ __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tile
     __shared__ double red[3][NR * 64];
     const FTile t = tiles[first + blockIdx.x];
     const int tid = threadIdx.x;
-    // this tile's slice of the front f_P = b_P + extend-add of the children's update vectors
-    for (int i = tid; i < t.nc; i += 256) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i);
-    __syncthreads();
     const int lane = tid & 63, w = tid >> 6;
     const int r = t.r0 + lane;
     constexpr int per = kFwdTileCols / 4;
     const int i0 = w * per, i1 = min(i0 + per, t.nc);
+    // the first kFwdPrefetch columns of this lane's G slice are loaded before the front slice is
+    // assembled, so their latency overlaps the extend-add gathers and the barrier
+    const double* G = Gc + t.goff + (size_t)t.c0 * t.R + r;
+    double gp[kFwdPrefetch > 0 ? kFwdPrefetch : 1];
+    if (r < t.R) {
+#pragma unroll
+        for (int q = 0; q < kFwdPrefetch; ++q)
+            if (i0 + q < i1) gp[q] = G[(size_t)(i0 + q) * t.R];
+    }
+    // this tile's slice of the front f_P = b_P + extend-add of the children's update vectors
+    for (int i = tid; i < t.nc; i += 256) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i);
+    __syncthreads();
     double a[NR];
     zero<NR>(a);
     if (r < t.R) {
-        const double* G = Gc + t.goff + (size_t)t.c0 * t.R + r;
+#pragma unroll
+        for (int q = 0; q < kFwdPrefetch; ++q) {
+            if (i0 + q >= i1) break;
+#pragma unroll
+            for (int k = 0; k < NR; ++k) a[k] += gp[q] * f[NR * (i0 + q) + k];
+        }
 #pragma unroll 8
-        for (int i = i0; i < i1; ++i) {
+        for (int i = i0 + kFwdPrefetch; i < i1; ++i) {
             const double g = G[(size_t)i * t.R];
 #pragma unroll
             for (int k = 0; k < NR; ++k) a[k] += g * f[NR * i + k];
@@ -572,6 +604,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     const bool stats = std::getenv("AA_SOLVE_STATS") != nullptr;
     const char* sb = std::getenv("AA_SUB_BLOCK");
     sub_block_ = sb ? std::atoi(sb) : 1024;
+    const char* pf = std::getenv("AA_TILE_PREFETCH");
+    tile_pf_ = pf ? std::atoi(pf) : 1;
     const int min_sub = ms ? std::atoi(ms) : 256;
     constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
     static_assert(kSubSegRows == 64, "LDS accounting below assumes 64-row segments");
@@ -879,9 +913,11 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
                                    ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
-        if (L.ft_count)
-            hipLaunchKernelGGL(k_fwd_tile<NR>, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b0, b1,
+        if (L.ft_count) {
+            auto kf = tile_pf_ ? k_fwd_tile<NR, 16> : k_fwd_tile<NR, 0>;
+            hipLaunchKernelGGL(kf, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b0, b1,
                                bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
+        }
     }
     // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
     // and in the update vectors); their sum over the GPUs is the full forward result. When the
@@ -895,9 +931,11 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
                                    bnd_.p, Y_.p, x0, x1, ctrl, gate_reject)
         if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
-        if (L.bt_count)
-            hipLaunchKernelGGL(k_bwd_tile<NR>, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p,
+        if (L.bt_count) {
+            auto kb = tile_pf_ ? k_bwd_tile<NR, 8> : k_bwd_tile<NR, 0>;
+            hipLaunchKernelGGL(kb, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p,
                                x0, x1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
+        }
     }
 #define SUBB(BL) hipLaunchKernelGGL((k_bwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_b_, s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, \

@@ -106,6 +106,7 @@ private:
     std::vector<Level> levels_;
     // fused bottom subtrees
     int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1, sub_block_ = 256;
+    int tile_pf_ = 1;   // split-K tiles prefetch their first G rows/columns before staging (AA_TILE_PREFETCH)
     DevBuf<SubNode> sub_nodes_;
     DevBuf<SubLevel> sub_levels_;
     DevBuf<SubTree> sub_trees_;
