@@ -566,9 +566,13 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
         // products: a load used right away serialises the loop on its latency
         const double ci = cur[i];
         const double dfo = dF[(size_t)col * eff + i];
-        double dfc[MM];
+        // (wide windows keep the loads in the product loop: MM doubles more would cost occupancy)
+        constexpr bool kPre = MM <= 16;
+        double dfc[kPre ? MM : 1];
+        if constexpr (kPre) {
 #pragma unroll
-        for (int c = 0; c < MM; ++c) dfc[c] = (c < mk && c != col) ? dF[(size_t)c * eff + i] : 0.0;
+            for (int c = 0; c < MM; ++c) dfc[c] = (c < mk && c != col) ? dF[(size_t)c * eff + i] : 0.0;
+        }
         if (i >= G.na) {
             const long long j = i - G.na;
             if (!((j >= mask.lo1 && j < mask.hi1) || (j >= mask.lo2 && j < mask.hi2))) continue;
@@ -580,8 +584,11 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
 #pragma unroll
         for (int c = 0; c < MM; ++c) {
             if (c < mk && c != col) {
-                acc[2 + c] += dfj * dfc[c];
-                acc[2 + MM + c] += dfc[c] * f;
+                double d;
+                if constexpr (kPre) d = dfc[c];
+                else d = dF[(size_t)c * eff + i];
+                acc[2 + c] += dfj * d;
+                acc[2 + MM + c] += d * f;
             }
         }
     }
@@ -856,9 +863,12 @@ __global__ __launch_bounds__(kBlock) void k_aa_mix(Seg2 G, double* cur, long lon
         const bool in_eff = i < eff;
         const double ci = in_eff ? cur[i] : 0.0;
         const double dfo = (!first && in_eff) ? dF[(size_t)j * eff + i] : 0.0;
-        double dgc[MM];
+        constexpr bool kPre = MM <= 16;   // as in k_aa_reduce
+        double dgc[kPre ? MM : 1];
+        if constexpr (kPre) {
 #pragma unroll
-        for (int c = 0; c < MM; ++c) dgc[c] = (!first && c < mk) ? dG[(size_t)c * dim + i] : 0.0;
+            for (int c = 0; c < MM; ++c) dgc[c] = (!first && c < mk) ? dG[(size_t)c * dim + i] : 0.0;
+        }
         const double f = in_eff ? g - ci : 0.0;
         double res;
         if (first) {
@@ -868,7 +878,9 @@ __global__ __launch_bounds__(kBlock) void k_aa_mix(Seg2 G, double* cur, long lon
 #pragma unroll
             for (int c = 0; c < MM; ++c)
                 if (c < mk) {
-                    double d = dgc[c];
+                    double d;
+                    if constexpr (kPre) d = dgc[c];
+                    else d = dG[(size_t)c * dim + i];
                     if (c == j) { d += g; dgj = d; }
                     acc += d * coef[c];
                 }

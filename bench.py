@@ -383,11 +383,14 @@ def main():
     if roof is not None:   # HBM bytes per solve from the committed PMC passes (tools/gpu_pmc.sh)
         pmc = os.path.join(REPO, "profiles", f"r1_{args.config}_pmc.json")
         if os.path.exists(pmc) and comm is None:
-            sp = json.load(open(pmc)).get("solve_per_launch") or {}
+            # the PMC group of the same solve the roofline times: two-set (6 RHS) when pipelined
+            key = "solve2_per_launch" if pipelined else "solve_per_launch"
+            sp = json.load(open(pmc)).get(key) or {}
             if sp.get("traffic_B"):
                 roof["traffic"] = sp["traffic_B"]
-                roof["traffic_source"] = (f"profiles/r1_{args.config}_pmc.json: FETCH_SIZE (x2, calibrated on k_copy) "
-                                          f"+ WRITE_SIZE over one solve's {sp['kernels']} kernels, separate --pmc passes")
+                roof["traffic_source"] = (f"profiles/r1_{args.config}_pmc.json {key}: FETCH_SIZE (x2, calibrated on "
+                                          f"k_copy) + WRITE_SIZE over the solve's {sp['kernels']} kernels, separate "
+                                          "--pmc passes")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         print("[bench] timing the reference CPU baseline", file=sys.stderr, flush=True)

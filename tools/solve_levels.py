@@ -1,4 +1,7 @@
-"""Per-launch durations of the last global solve in a rocprofv3 kernel trace (NO_GRAPH runs)."""
+"""Per-launch durations of the last global solve in a rocprofv3 kernel trace (NO_GRAPH runs).
+
+    python tools/solve_levels.py run_kernel_trace.csv [3|6]
+"""
 import csv
 import re
 import sys
@@ -6,7 +9,18 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 names = [r["Kernel_Name"] for r in rows]
-idx = set(i for i, n in enumerate(names) if "k_fwd" in n or "k_bwd" in n or "k_asm" in n)
+# optional argv[2]: right-hand sides of the solve to show (3 = one solve, 6 = the two-set solve)
+want = sys.argv[2] if len(sys.argv) > 2 else None
+
+
+def nr_of(n):
+    m = re.search(r"k_[a-z_0-9]+<([^>]*)>", n)
+    nr = [a.strip() for a in m.group(1).split(",") if a.strip() in ("3", "6")] if m else []
+    return nr[0] if nr else None
+
+
+idx = set(i for i, n in enumerate(names)
+          if ("k_fwd" in n or "k_bwd" in n or "k_asm" in n) and (want is None or nr_of(n) == want))
 end = max(idx)
 start = end
 while start - 1 in idx:
