@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libaa_admm.so")
+LIB_PATH = os.environ.get("AA_ADMM_LIB") or os.path.join(HERE, "libaa_admm.so")   # override: A/B builds
 
 AA_LINEAR, AA_NEOHOOKEAN, AA_STVK = 0, 1, 2
 AA_VARIANT_Z, AA_VARIANT_UX = 0, 1

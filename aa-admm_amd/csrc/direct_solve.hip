@@ -179,15 +179,14 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
 
 // Backward sweep of the large supernodes (R > kWaveR) as a split-K GEMV: tile = 128 columns
 // (2 per lane, one 16-B load each: rows of G are padded to an even length) x kBwdTileRows rows
-// (4 waves x 32 rows) of the row-major G, the tile's slice of [y_P ; -x_B] staged in LDS, one
+// (4 waves x kBwdTileRows/4 rows; kBwdTileRows = DirectSolver::tile_w_, 128 or 256) of the
+// row-major G, the tile's slice of [y_P ; -x_B] staged in LDS, one
 // 128 x NR partial per tile; the last tile of a column block to finish sums the block's partials
-// in tile order (deterministic; hand-off protocol above). Gives (columns/128) x (rows/128)
+// in tile order (deterministic; hand-off protocol above). Gives (columns/128) x (rows/kBwdTileRows)
 // workgroups per supernode instead of one wave per column with a serial loop over all R rows.
 using BTile = DirectSolver::BTile;
 using BRed = DirectSolver::BRed;
-constexpr int kBwdTileRows = 128;
-
-template <int NR, int kBwdPrefetch>
+template <int NR, int kBwdPrefetch, int kBwdTileRows>
 __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tiles, int first, const double* __restrict__ Gr,
                                                   const int* __restrict__ bnd, const double* __restrict__ Y,
                                                   double* __restrict__ X0, double* __restrict__ X1,
@@ -271,15 +270,13 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
 }
 
 // Forward sweep of the large supernodes (p > kWaveP) as a split-K GEMV on the column-major G:
-// tile = 64 rows (lanes) x kFwdTileCols columns (4 waves x 32), the tile's slice of the
+// tile = 64 rows (lanes) x kFwdTileCols columns (4 waves; 128 or 256), the tile's slice of the
 // assembled front f_P staged in LDS, one 64 x NR partial per tile; the last tile of a row block
 // to finish sums its partials in tile order and writes y_P (rows < p) or the update vector
 // u = f_B - M f_P.
 using FTile = DirectSolver::FTile;
 using FRed = DirectSolver::FRed;
-constexpr int kFwdTileCols = 128;
-
-template <int NR, int kFwdPrefetch>
+template <int NR, int kFwdPrefetch, int kFwdTileCols>
 __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tiles, int first, const double* __restrict__ Gc,
                                                   const long long* __restrict__ ell, const double* __restrict__ B0,
                                                   const double* __restrict__ B1, double* __restrict__ part,
@@ -606,6 +603,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     sub_block_ = sb ? std::atoi(sb) : 1024;
     const char* pf = std::getenv("AA_TILE_PREFETCH");
     tile_pf_ = pf ? std::atoi(pf) : 1;
+    // split-K tile width (forward columns / backward rows): 256 for the two-set solves of the Z
+    // variant (C4: two-set solve 860 -> 800 us), 128 for one-set solvers (their smaller
+    // supernodes lose ~4 % with 256-wide tiles); AA_SOLVE_TILE overrides
+    const char* tw = std::getenv("AA_SOLVE_TILE");
+    tile_w_ = tw ? (std::atoi(tw) >= 256 ? 256 : 128) : (max_sets_ >= 2 ? 256 : 128);
     const int min_sub = ms ? std::atoi(ms) : 256;
     constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
     static_assert(kSubSegRows == 64, "LDS accounting below assumes 64-row segments");
@@ -776,7 +778,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             }
         }
         L.fwd_count = (int)tasks.size() - L.fwd_first;
-        // large supernodes: split-K forward tiles (64 rows x kFwdTileCols columns; tiles entirely
+        // large supernodes: split-K forward tiles (64 rows x tile_w_ columns; tiles entirely
         // above the diagonal of L_PP^-1 are zero and skipped), one reduction task per row block
         L.ft_first = (int)ftiles.size();
         L.fr_first = (int)freds.size();
@@ -787,11 +789,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 FRed rd{};
                 rd.beg = beg[sn]; rd.p = p[sn]; rd.r0 = r0; rd.nr = std::min(64, R - r0);
                 rd.uoff = uoff[sn]; rd.ell_off = ell_off[sn]; rd.ell_w = ell_w[sn]; rd.poff = poff;
-                for (int c0 = 0; c0 < p[sn]; c0 += kFwdTileCols) {
+                for (int c0 = 0; c0 < p[sn]; c0 += tile_w_) {
                     if (r0 + 63 < c0) break;
                     FTile ft{};
                     ft.beg = beg[sn]; ft.p = p[sn]; ft.R = R; ft.c0 = c0; ft.r0 = r0;
-                    ft.nc = std::min(kFwdTileCols, p[sn] - c0);
+                    ft.nc = std::min(tile_w_, p[sn] - c0);
                     ft.goff = goff[sn]; ft.ell_off = ell_off[sn]; ft.ell_w = ell_w[sn]; ft.poff = poff;
                     ft.rid = (int)freds.size();
                     poff += 3 * 64;
@@ -812,7 +814,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             }
         }
         L.bwd_count = (int)tasks.size() - L.bwd_first;
-        // large supernodes: split-K tiles (64 columns x kBwdTileRows rows; the tiles above the
+        // large supernodes: split-K tiles (128 columns x tile_w_ rows; the tiles above the
         // diagonal of L_PP^-1 are all zero and skipped) and one reduction task per column block
         L.bt_first = (int)btiles.size();
         L.br_first = (int)breds.size();
@@ -822,10 +824,10 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             for (int c0 = 0; c0 < p[sn]; c0 += 128) {
                 BRed rd{};
                 rd.beg = beg[sn]; rd.c0 = c0; rd.nc = std::min(128, p[sn] - c0); rd.poff = poff;
-                for (int r0 = c0; r0 < R; r0 += kBwdTileRows) {
+                for (int r0 = c0; r0 < R; r0 += tile_w_) {
                     BTile bt{};
                     bt.beg = beg[sn]; bt.p = p[sn]; bt.nb = nb[sn]; bt.bnd_off = bnd_off[sn];
-                    bt.c0 = c0; bt.r0 = r0; bt.nr = std::min(kBwdTileRows, R - r0);
+                    bt.c0 = c0; bt.r0 = r0; bt.nr = std::min(tile_w_, R - r0);
                     bt.goff = goff[sn]; bt.poff = poff; bt.ldr = ldr[sn];
                     bt.rid = (int)breds.size();
                     poff += 6 * 64;
@@ -914,7 +916,8 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
         if (L.ft_count) {
-            auto kf = tile_pf_ ? k_fwd_tile<NR, 16> : k_fwd_tile<NR, 0>;
+            auto kf = tile_w_ == 256 ? (tile_pf_ ? k_fwd_tile<NR, 16, 256> : k_fwd_tile<NR, 0, 256>)
+                                     : (tile_pf_ ? k_fwd_tile<NR, 16, 128> : k_fwd_tile<NR, 0, 128>);
             hipLaunchKernelGGL(kf, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b0, b1,
                                bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
         }
@@ -932,7 +935,8 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
         if (L.bt_count) {
-            auto kb = tile_pf_ ? k_bwd_tile<NR, 8> : k_bwd_tile<NR, 0>;
+            auto kb = tile_w_ == 256 ? (tile_pf_ ? k_bwd_tile<NR, 8, 256> : k_bwd_tile<NR, 0, 256>)
+                                     : (tile_pf_ ? k_bwd_tile<NR, 8, 128> : k_bwd_tile<NR, 0, 128>);
             hipLaunchKernelGGL(kb, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p,
                                x0, x1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
         }

@@ -107,6 +107,7 @@ private:
     // fused bottom subtrees
     int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1, sub_block_ = 256;
     int tile_pf_ = 1;   // split-K tiles prefetch their first G rows/columns before staging (AA_TILE_PREFETCH)
+    int tile_w_ = 128;  // split-K tile width: forward columns / backward rows (128 or 256)
     DevBuf<SubNode> sub_nodes_;
     DevBuf<SubLevel> sub_levels_;
     DevBuf<SubTree> sub_trees_;
