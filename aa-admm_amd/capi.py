@@ -24,17 +24,20 @@ EXPORTS = [
     "aa_settings_default", "aa_elastic_create", "aa_elastic_destroy", "aa_elastic_add_nodes", "aa_elastic_add_tets",
     "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
+    "aa_elastic_get_times", "aa_elastic_set_iterations",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats",
     "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_destroy", "aa_comm_info",
     "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
-    "aa_geom_create", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
+    "aa_geom_create", "aa_geom_create_kind", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
     "aa_geom_add_closeness", "aa_geom_setup", "aa_geom_solve", "aa_geom_get_solution", "aa_geom_get_history",
     "aa_geom_runtime_info", "aa_geom_closest_points", "aa_geom_bench_iterations", "aa_geom_kernel_stats",
+    "aa_test_prox", "aa_test_cod_solve", "aa_test_geom_project",
 ]
 
 # Geometry constraint types (Geometry/Constraint.h) and SPD solver types (SolverCommon.h)
 AA_CON_PLANE, AA_CON_ANGLE, AA_CON_EDGE, AA_CON_CLOSENESS, AA_CON_POINT_TO_REF, AA_CON_REF_SURFACE = range(6)
 AA_SPD_LDLT, AA_SPD_LLT = 0, 1
+AA_GEOM_ALM, AA_GEOM_PLAIN = 0, 1   # ALMGeometrySolver<3> / GeometrySolver<3>
 
 
 class Lame(C.Structure):
@@ -52,10 +55,10 @@ class Settings(C.Structure):
     """admm::Solver::Settings (Solver.hpp:45-67) + the variant."""
     _fields_ = [("timestep_s", C.c_double), ("verbose", C.c_int), ("admm_iters", C.c_int), ("gravity", C.c_double),
                 ("constraint_w", C.c_double), ("anderson_m", C.c_int), ("penalty", C.c_double),
-                ("acceleration_type", C.c_int), ("variant", C.c_int)]
+                ("acceleration_type", C.c_int), ("variant", C.c_int), ("eps_rel", C.c_double)]
 
     def __init__(self, **kw):
-        super().__init__(1.0 / 30.0, 1, 500, -9.8, -1.0, 2, 1.0, NOACC, AA_VARIANT_UX)
+        super().__init__(1.0 / 30.0, 1, 500, -9.8, -1.0, 2, 1.0, NOACC, AA_VARIANT_UX, 0.0)
         for k, v in kw.items():
             setattr(self, k, v)
 
@@ -265,6 +268,17 @@ class Solver:
         k = min(n.value, cap)
         return dict(prim=p[:k].copy(), comb=c[:k].copy(), reject=r[:k].copy())
 
+    def times(self, cap=100000):
+        """Device-clock ms from the start of the last step to the end of each recorded iteration."""
+        t = np.zeros(cap)
+        n = C.c_int()
+        _chk(lib().aa_elastic_get_times(self.h, _dp(t), C.c_int(cap), C.byref(n)))
+        return t[:min(n.value, cap)].copy()
+
+    def set_iterations(self, admm_iters, eps_rel=0.0):
+        """Settings::admm_iters and the run-to-epsilon stop of later steps (no re-factor)."""
+        _chk(lib().aa_elastic_set_iterations(self.h, C.c_int(admm_iters), C.c_double(eps_rel)))
+
     def runtime(self) -> Runtime:
         rt = Runtime()
         _chk(lib().aa_elastic_runtime(self.h, C.byref(rt)))
@@ -332,14 +346,15 @@ class GeomRuntime(C.Structure):
 
 
 class GeomSolver:
-    """Mirror of ALMGeometrySolver<3>: add_hard/soft constraints, add_*laplacian, add_closeness,
-    setup_ADMM, solve_ADMM, get_solution, function_values_ / elapsed_time_."""
+    """Mirror of ALMGeometrySolver<3> (kind AA_GEOM_ALM) or GeometrySolver<3> (AA_GEOM_PLAIN):
+    add_hard/soft constraints, add_*laplacian, add_closeness, setup_ADMM, solve_ADMM,
+    get_solution, function_values_ / elapsed_time_."""
 
-    def __init__(self, ctx: Context):
+    def __init__(self, ctx: Context, kind=AA_GEOM_ALM):
         self.ctx = ctx
         self.h = C.c_void_p()
         self.n = 0
-        _chk(lib().aa_geom_create(ctx.h, C.byref(self.h)))
+        _chk(lib().aa_geom_create_kind(ctx.h, C.c_int(kind), C.byref(self.h)))
 
     def close(self):
         if self.h:
@@ -430,7 +445,7 @@ class GeomSolver:
 
 def geom_from_scene(ctx: Context, sc, comm=None) -> GeomSolver:
     """Binds a geom_scenes.GeomScene the way optimize_mesh (PlanarityOpt.cpp / WireMeshOpt.cpp) does."""
-    g = GeomSolver(ctx)
+    g = GeomSolver(ctx, AA_GEOM_PLAIN if getattr(sc, "solver", "alm") == "plain" else AA_GEOM_ALM)
     if comm is not None:
         g.set_comm(comm)
     sids = [g.add_ref_surface(V, F) for V, F in sc.surfaces]
@@ -458,3 +473,39 @@ def run_geom(ctx: Context, sc, comm=None):
     h = g.history()
     h["x"] = g.solution()
     return h, g
+
+
+# ------------------------------------------------------------------------------------------
+# element-level test hooks (aa_test_*): the device prox / COD / projection functions
+# ------------------------------------------------------------------------------------------
+
+def hook_prox(ctx: Context, op, prm4, X):
+    """op 0 linear tet, 1 NeoHookean, 2 StVK (prm4 = E, nu, h), 3 / 4 tri H / X prox (prm4[2:] =
+    limits); X (n, 9|6). Returns (out, L-BFGS iterations)."""
+    X = np.ascontiguousarray(X, np.float64)
+    n = X.shape[0]
+    out, it = np.zeros_like(X), np.zeros(n, np.int32)
+    p = np.ascontiguousarray(prm4, np.float64)
+    _chk(lib().aa_test_prox(ctx.h, C.c_int(op), _dp(p), _dp(X), C.c_int(n), _dp(out), _ip(it)))
+    return out, it
+
+
+def hook_cod_solve(ctx: Context, M, b):
+    Mc = np.asfortranarray(M, np.float64).ravel(order="F").copy()
+    bb = np.ascontiguousarray(b, np.float64)
+    th = np.zeros(len(bb))
+    _chk(lib().aa_test_cod_solve(ctx.h, C.c_int(len(bb)), _dp(Mc), _dp(bb), _dp(th)))
+    return th
+
+
+def hook_geom_project(ctx: Context, ctype, k, params, P):
+    """P (n, cols, 3) transformed points; params (2,) (angle min/max or edge length)."""
+    P = np.ascontiguousarray(P, np.float64)
+    out = np.zeros_like(P)
+    prm = np.zeros(2)
+    if params is not None:
+        a = np.atleast_1d(np.asarray(params, np.float64))
+        prm[:len(a)] = a
+    _chk(lib().aa_test_geom_project(ctx.h, C.c_int(ctype), C.c_int(k), _dp(prm), _dp(P), C.c_int(P.shape[0]), _dp(out)))
+    return out
+

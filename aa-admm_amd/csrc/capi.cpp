@@ -92,6 +92,7 @@ int aa_settings_default(aa_settings* s) {
         s->penalty = 1.0;
         s->acceleration_type = 0;
         s->variant = AA_VARIANT_UX;
+        s->eps_rel = 0.0;
     });
 }
 
@@ -183,6 +184,18 @@ int aa_elastic_get_history(aa_elastic h, double* prim, double* comb, int* reject
     });
 }
 
+int aa_elastic_set_iterations(aa_elastic h, int admm_iters, double eps_rel) {
+    return guarded([&] { NEED(h, "null handle"); h->s->set_iterations(admm_iters, eps_rel); });
+}
+
+int aa_elastic_get_times(aa_elastic h, double* time_ms, int cap, int* n) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        int k = h->s->times(time_ms, cap);
+        if (n) *n = k;
+    });
+}
+
 int aa_elastic_runtime(aa_elastic h, aa_runtime* out) {
     return guarded([&] { NEED(h && out, "null argument"); *out = h->s->runtime(); });
 }
@@ -256,13 +269,16 @@ int aa_elastic_kernel_stats(aa_elastic h, const char* name, double* avg_ms, doub
 }
 
 // ---- Geometry (ALMGeometrySolver<3>) -------------------------------------------------------
-int aa_geom_create(aa_ctx ctx, aa_geom* out) {
+int aa_geom_create(aa_ctx ctx, aa_geom* out) { return aa_geom_create_kind(ctx, AA_GEOM_ALM, out); }
+
+int aa_geom_create_kind(aa_ctx ctx, int kind, aa_geom* out) {
     return guarded([&] {
         NEED(ctx && out, "aa_geom_create: null argument");
+        NEED(kind == AA_GEOM_ALM || kind == AA_GEOM_PLAIN, "aa_geom_create_kind: unknown solver kind");
         AA_HIP(hipSetDevice(ctx->c.device));
         auto* h = new aa_geom_s;
         h->ctx = ctx;
-        h->s = new aa::GeomSolver(&ctx->c);
+        h->s = new aa::GeomSolver(&ctx->c, kind == AA_GEOM_PLAIN);
         *out = h;
     });
 }
@@ -351,3 +367,56 @@ int aa_geom_kernel_stats(aa_geom h, const char* name, double* avg_ms, double* by
 }
 
 }  // extern "C"
+
+// ---- element-level test hooks (tests only): device prox / COD / projections on host arrays ----
+namespace {
+template <class F>
+int with_device_arrays(aa_ctx ctx, F&& f) {
+    return guarded([&] {
+        NEED(ctx, "null context");
+        AA_HIP(hipSetDevice(ctx->c.device));
+        f(ctx->c.stream);
+        AA_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+}  // namespace
+
+extern "C" int aa_test_prox(aa_ctx ctx, int op, const double* prm4, const double* in, int n, double* out, int* iters) {
+    return with_device_arrays(ctx, [&](hipStream_t s) {
+        NEED(prm4 && in && out && n >= 0 && op >= 0 && op <= 4, "aa_test_prox: bad argument");
+        const int D = op >= 3 ? 6 : 9;
+        aa::DevBuf<double> di, dout((size_t)D * std::max(n, 1));
+        aa::DevBuf<int> dit(std::max(n, 1));
+        di.upload(in, (size_t)D * n, s);
+        aa::launch_test_prox(op, prm4, di.p, n, dout.p, dit.p, s);
+        AA_HIP(hipMemcpyAsync(out, dout.p, sizeof(double) * D * n, hipMemcpyDeviceToHost, s));
+        if (iters) AA_HIP(hipMemcpyAsync(iters, dit.p, sizeof(int) * n, hipMemcpyDeviceToHost, s));
+        AA_HIP(hipStreamSynchronize(s));
+    });
+}
+
+extern "C" int aa_test_cod_solve(aa_ctx ctx, int k, const double* M, const double* b, double* theta) {
+    return with_device_arrays(ctx, [&](hipStream_t s) {
+        NEED(M && b && theta && k >= 1 && k <= aa::kMaxM, "aa_test_cod_solve: bad argument");
+        aa::DevBuf<double> dM, db, dx(k);
+        dM.upload(M, (size_t)k * k, s);
+        db.upload(b, k, s);
+        aa::launch_test_cod(k, dM.p, db.p, dx.p, s);
+        AA_HIP(hipMemcpyAsync(theta, dx.p, sizeof(double) * k, hipMemcpyDeviceToHost, s));
+        AA_HIP(hipStreamSynchronize(s));
+    });
+}
+
+extern "C" int aa_test_geom_project(aa_ctx ctx, int type, int k, const double* prm2, const double* in, int n,
+                                    double* out) {
+    return with_device_arrays(ctx, [&](hipStream_t s) {
+        NEED(prm2 && in && out && n >= 0 && k >= 2, "aa_test_geom_project: bad argument");
+        const int C = (type == aa::GEO_ANGLE || type == aa::GEO_EDGE) ? k - 1 : k;
+        aa::DevBuf<double> di, dout((size_t)3 * C * std::max(n, 1));
+        di.upload(in, (size_t)3 * C * n, s);
+        aa::launch_test_geo_project(type, k, prm2, di.p, n, dout.p, s);
+        AA_HIP(hipMemcpyAsync(out, dout.p, sizeof(double) * 3 * C * n, hipMemcpyDeviceToHost, s));
+        AA_HIP(hipStreamSynchronize(s));
+    });
+}
+

@@ -494,10 +494,13 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
 }  // namespace
 
 void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part, int my_part,
-                         int top_beg, Comm* comm, int max_sets) {
+                         int top_beg, Comm* comm, int max_sets, bool wide) {
     n_ = F.n;
     max_sets_ = max_sets >= 2 ? 2 : 1;
-    const int KS = max_sets_;   // LDS / workspace scale of the widest solve
+    // LDS scale the layout (fused-subtree cut, tile width) is planned for: the two-set budget
+    // whenever `wide`, so a one-set solver built wide sums every column in the same order as a
+    // two-set one (bit-identical AA_Z_PIPELINE=0 / 1)
+    const int KS = (wide || max_sets_ >= 2) ? 2 : 1;
     nn_ = F.n_nodes;
     comm_ = (node_part && comm && comm->size() > 1) ? comm : nullptr;
     top_beg_ = comm_ ? top_beg : n_;
@@ -607,7 +610,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     // variant (C4: two-set solve 860 -> 800 us), 128 for one-set solvers (their smaller
     // supernodes lose ~4 % with 256-wide tiles); AA_SOLVE_TILE overrides
     const char* tw = std::getenv("AA_SOLVE_TILE");
-    tile_w_ = tw ? (std::atoi(tw) >= 256 ? 256 : 128) : (max_sets_ >= 2 ? 256 : 128);
+    tile_w_ = tw ? (std::atoi(tw) >= 256 ? 256 : 128) : (KS >= 2 ? 256 : 128);
     const int min_sub = ms ? std::atoi(ms) : 256;
     constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
     static_assert(kSubSegRows == 64, "LDS accounting below assumes 64-row segments");

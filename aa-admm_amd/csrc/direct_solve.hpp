@@ -38,8 +38,10 @@ public:
     // the top are stored and solved here, and the top rows of the forward result are summed
     // over the GPUs between the two sweeps.
     // max_sets = 2 sizes the workspaces and the fused subtrees' LDS budget for solve2().
+    // wide: plan the layout (subtree cut, 256-wide split-K tiles) for two sets even when
+    // max_sets = 1, so both solvers sum in the same order.
     void build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part = nullptr, int my_part = -1,
-               int top_beg = -1, Comm* comm = nullptr, int max_sets = 1);
+               int top_beg = -1, Comm* comm = nullptr, int max_sets = 1, bool wide = false);
     // x (n x 3, stride 3 doubles) = A^-1 b ; b is read only. gate: skip when ctrl->done (or !reject).
     void solve(const double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s);
     // x0 = A^-1 b0 and x1 = A^-1 b1 in one pass (needs build(..., max_sets = 2))

@@ -275,7 +275,9 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     // solve (enqueue_iteration_z); AA_Z_PIPELINE=0 restores the sequential order
     pipe_z_ = st_.variant == AA_VARIANT_Z && st_.acceleration_type == 1;
     if (const char* e = std::getenv("AA_Z_PIPELINE")) pipe_z_ = pipe_z_ && e[0] != '0';
-    solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_, pipe_z_ ? 2 : 1);
+    // Z variant + Anderson: the two-set layout whether pipelined or not (same sums, same bits)
+    solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_, pipe_z_ ? 2 : 1,
+                  st_.variant == AA_VARIANT_Z && st_.acceleration_type == 1);
 
     // ---- element ownership (partitioned): an element touching a node of part r belongs to
     // rank r (it cannot touch another part: the separators split the mesh); elements whose free
@@ -406,8 +408,16 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     ctrl_.alloc(1);
     lzq_.alloc(1);
     if (const char* q = std::getenv("AA_LOCAL_QUEUE")) use_queue_ = q[0] != '0';
+    lq_ = make_local_queue(ctx_->device, lzq_.p);
     hist_cap_ = std::max(1, st_.admm_iters);
     hist_prim_.alloc(hist_cap_); hist_comb_.alloc(hist_cap_); hist_rej_.alloc(hist_cap_);
+    hist_clock_.alloc(hist_cap_ + 1);
+    {
+        int khz = 0;
+        AA_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx_->device));
+        if (khz > 0) clock_khz_ = khz;
+    }
+    if (!(st_.eps_rel >= 0.0)) throw Error(ERR_ARG, "initialize: eps_rel must be >= 0");
     if (accel) {
         const int m = st_.anderson_m;
         const long long dim = st_.variant == AA_VARIANT_UX ? Z_ + 3LL * nf_ : Z_;
@@ -522,7 +532,7 @@ void ElasticSolver::local_z_all(const double* xfull, const double* u, double* z,
     if (timed) ev_begin("local_z");
     for (auto& g : groups_) {
         launch_local_z(g.d, xfull, u, z, y, nf_, st_.variant, mode, ctrl_.p, red ? pa_ : nullptr, off, s(),
-                       use_queue_ ? lzq_.p : nullptr);
+                       use_queue_ ? &lq_ : nullptr);
         off += blocks_for(g.d.count);
     }
     if (timed) ev_end("local_z");
@@ -537,7 +547,10 @@ void ElasticSolver::prologue() {
     c.cap = hist_cap_;
     c.aa_m = accel ? st_.anderson_m : 0;
     c.aa_active = accel ? 1 : 0;
+    c.hist_clock = hist_clock_.p;
+    c.eps_rel = st_.eps_rel;
     AA_HIP(hipMemcpyAsync(ctrl_.p, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s()));
+    launch_stamp(ctrl_.p, s());
     launch_predict(n_, nf_, xs_.p, vs_.p, mass_.p, st_.timestep_s, st_.gravity, xbar_.p, Mxbar_.p, xfull_.p, s());
     // partitioned: the mass term of a shared separator row enters the right-hand side once
     // (rank 0); the other ranks contribute only their elements' D^T rows to it
@@ -770,6 +783,12 @@ void ElasticSolver::fetch_results() {
         AA_HIP(hipMemcpy(h_prim_.data(), hist_prim_.p, nrec_ * 8, hipMemcpyDeviceToHost));
         AA_HIP(hipMemcpy(h_comb_.data(), hist_comb_.p, nrec_ * 8, hipMemcpyDeviceToHost));
         AA_HIP(hipMemcpy(h_rej_.data(), hist_rej_.p, nrec_ * 4, hipMemcpyDeviceToHost));
+        std::vector<long long> clk(nrec_);
+        AA_HIP(hipMemcpy(clk.data(), hist_clock_.p, nrec_ * sizeof(long long), hipMemcpyDeviceToHost));
+        h_time_.resize(nrec_);
+        for (int i = 0; i < nrec_; ++i) h_time_[i] = (double)(clk[i] - c.clock0) / clock_khz_;
+    } else {
+        h_time_.clear();
     }
     rt_.iterations = c.iters_run;
     rt_.rejects = c.nrej;
@@ -830,6 +849,27 @@ int ElasticSolver::history(double* prim, double* comb, int* rej, int cap) const 
         if (rej) rej[i] = h_rej_[i];
     }
     return nrec_;
+}
+
+// run limits of later steps (bench: a run-to-epsilon leg after the fixed-iteration steps,
+// without re-factoring): drops the captured graph, grows the history if needed
+void ElasticSolver::set_iterations(int admm_iters, double eps_rel) {
+    if (!initialized_) throw Error(ERR_STATE, "set_iterations before initialize()");
+    if (admm_iters < 0 || !(eps_rel >= 0.0)) throw Error(ERR_ARG, "set_iterations: admm_iters >= 0 and eps_rel >= 0");
+    drop_graph();
+    st_.admm_iters = admm_iters;
+    st_.eps_rel = eps_rel;
+    if (std::max(1, admm_iters) > hist_cap_) {
+        hist_cap_ = admm_iters;
+        hist_prim_.alloc(hist_cap_); hist_comb_.alloc(hist_cap_); hist_rej_.alloc(hist_cap_);
+        hist_clock_.alloc(hist_cap_ + 1);
+    }
+}
+
+int ElasticSolver::times(double* time_ms, int cap) const {
+    const int n = std::min(cap, (int)h_time_.size());
+    for (int i = 0; i < n && time_ms; ++i) time_ms[i] = h_time_[i];
+    return (int)h_time_.size();
 }
 
 double ElasticSolver::bench_iterations(int iters) {

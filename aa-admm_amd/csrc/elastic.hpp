@@ -40,6 +40,8 @@ public:
     void get_v(double* out);
     void set_v(const double* v3);
     int history(double* prim, double* comb, int* rej, int cap) const;
+    int times(double* time_ms, int cap) const;
+    void set_iterations(int admm_iters, double eps_rel);
     aa_runtime runtime() const { return rt_; }
 
     // benchmarking: run `iters` iterations of the ADMM loop body of a fresh time step;
@@ -91,9 +93,13 @@ private:
     int nbg_ = 0;
     DevBuf<Ctrl> ctrl_;
     DevBuf<int> lzq_;          // work-queue counter of the hyperelastic local step
+    LocalQueue lq_;
     bool use_queue_ = true;
     DevBuf<double> hist_prim_, hist_comb_;
     DevBuf<int> hist_rej_;
+    DevBuf<long long> hist_clock_;
+    double clock_khz_ = 100000.0;
+    std::vector<double> h_time_;
     int red_blocks_ = 0, aa_blocks_ = 0, hist_cap_ = 0;
     // partition: own free nodes [own_beg_, own_end_), shared top [top_beg_, nf_)
     Comm* comm_ = nullptr;

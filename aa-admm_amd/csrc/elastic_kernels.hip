@@ -48,6 +48,19 @@ __device__ __forceinline__ double block_sum_all(const double* red, int nb, doubl
     return a;
 }
 
+// history row k = nrec (prim, comb, reject, device clock); true when the run-to-epsilon stop
+// (comb <= eps_rel * comb of the first row) is reached. Single thread.
+__device__ __forceinline__ bool record_iter(Ctrl* c, double* hp, double* hc, int* hr, double comb) {
+    const int k = c->nrec;
+    if (k < c->cap) {
+        hp[k] = c->prim; hc[k] = comb; hr[k] = c->reject;
+        if (c->hist_clock) c->hist_clock[k] = (long long)wall_clock64();
+    }
+    c->nrec = k + 1;
+    if (k == 0) c->eps_abs = c->eps_rel * comb;
+    return c->eps_rel > 0 && comb <= c->eps_abs;
+}
+
 __device__ __forceinline__ bool gated(const Ctrl* c, int gate_reject) {
     if (!c) return false;
     if (c->done) return true;
@@ -421,9 +434,7 @@ __global__ __launch_bounds__(kCtlBlock) void k_control(int op, Ctrl* ctrl, const
             ctrl->iters_run += 1;
             ctrl->comb = comb;
             if (comb < kCombEps) { ctrl->done = 1; break; }
-            const int k = ctrl->nrec;
-            if (k < ctrl->cap) { hist_prim[k] = ctrl->prim; hist_comb[k] = comb; hist_rej[k] = ctrl->reject; }
-            ctrl->nrec = k + 1;
+            if (record_iter(ctrl, hist_prim, hist_comb, hist_rej, comb)) ctrl->done = 1;
             break;
         }
         case CTL_COMB_Z:
@@ -431,12 +442,10 @@ __global__ __launch_bounds__(kCtlBlock) void k_control(int op, Ctrl* ctrl, const
             const double comb = a + b;
             ctrl->iters_run += 1;
             ctrl->comb = comb;
-            const int k = ctrl->nrec;
-            if (k < ctrl->cap) { hist_prim[k] = ctrl->prim; hist_comb[k] = comb; hist_rej[k] = ctrl->reject; }
-            ctrl->nrec = k + 1;
+            const bool eps = record_iter(ctrl, hist_prim, hist_comb, hist_rej, comb);
             // ZP: decided one iteration late (pipelined): done = 2 asks for the speculative
             // next iteration's x to be rolled back (launch_copy gate 2)
-            if (comb < kCombEps) ctrl->done = op == CTL_COMB_ZP ? 2 : 1;
+            if (comb < kCombEps || eps) ctrl->done = op == CTL_COMB_ZP ? 2 : 1;
             break;
         }
     }
@@ -544,11 +553,9 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
             ctrl->comb = comb;
             ctrl->iters_run += 1;
             if (brk) ctrl->done = 1;
-            else {
-                const int kk = ctrl->nrec;
-                if (kk < ctrl->cap) { hist_prim[kk] = ctrl->prim; hist_comb[kk] = comb; hist_rej[kk] = ctrl->reject; }
-                ctrl->nrec = kk + 1;
-            }
+            // run-to-epsilon stop: this iteration completes as a last one would (the default
+            // copies below still happen); k_aa_solve turns eps_hit into done, gating the mix
+            else if (record_iter(ctrl, hist_prim, hist_comb, hist_rej, comb)) ctrl->eps_hit = 1;
         }
         if (brk) return;
     }
@@ -756,6 +763,11 @@ constexpr int kSolveBlock = 1024;
 template <int MM>
 __global__ __launch_bounds__(kSolveBlock) void k_aa_solve(Ctrl* ctrl, const double* red, int nb) {
     if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
+    if (ctrl->eps_hit) {   // run-to-epsilon stop recorded by k_aa_reduce (one block: no race)
+        __syncthreads();
+        if (threadIdx.x == 0) ctrl->done = 1;
+        return;
+    }
     constexpr int NVAL = 2 + 2 * MM;
     constexpr int NCH = kSolveBlock / NVAL;     // block partials are split into NCH chunks per value
     __shared__ double tot[NVAL];
@@ -897,27 +909,70 @@ __global__ __launch_bounds__(kBlock) void k_aa_mix(Seg2 G, double* cur, long lon
 
 inline int grid_for(long long n) { long long b = (n + kBlock - 1) / kBlock; return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048); }
 
+// ---- element-level test hooks: the device prox / COD functions on given inputs (tests only)
+// op 0 linear tet (9), 1 NeoHookean, 2 StVK (prm: E, nu, h -> vol = h^3/6), 3 tri H prox, 4 tri X
+// prox (prm: -, -, limit_min, limit_max)
+__global__ void k_test_prox(int op, double E, double nu, double p2, double p3, const double* __restrict__ in, int n,
+                            double* __restrict__ out, int* __restrict__ iters) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const int D = op >= 3 ? 6 : 9;
+    double v[9], z[9];
+    for (int i = 0; i < D; ++i) v[i] = in[(size_t)e * D + i];
+    int it = 0;
+    if (op == 0) {
+        dev::tet_linear_prox(v, z);
+    } else if (op <= 2) {
+        const double mu = E / (2.0 * (1.0 + nu)), lam = E * nu / ((1.0 + nu) * (1.0 - 2.0 * nu));
+        for (int i = 0; i < 9; ++i) z[i] = v[i];
+        int fail = 0;
+        it = dev::hyper_prox(op, mu, lam, lam + 2.0 * mu / 3.0, p2 * p2 * p2 / 6.0, v, z, &fail);
+        if (fail) it = -1;
+    } else {
+        dev::tri_prox(v, z, op == 3 ? 1 : 0, p2, p3);
+    }
+    for (int i = 0; i < D; ++i) out[(size_t)e * D + i] = z[i];
+    if (iters) iters[e] = it;
+}
+
+__global__ __launch_bounds__(kSolveBlock) void k_test_cod(int n, const double* __restrict__ M, const double* __restrict__ b,
+                                                          double* __restrict__ x) {
+    __shared__ CodLds S;
+    __shared__ double sb[kMaxM], sx[kMaxM];
+    for (int q = threadIdx.x; q < n * n; q += blockDim.x) S.A[q] = M[q];
+    if ((int)threadIdx.x < n) sb[threadIdx.x] = b[threadIdx.x];
+    __syncthreads();
+    cod_solve_block(n, S, sb, sx);
+    __syncthreads();
+    if ((int)threadIdx.x < n) x[threadIdx.x] = sx[threadIdx.x];
+}
+
 }  // namespace
 
 // ============================================================================ launchers
+// per solver (initialize): the resident grid of the work-queue kernel on `device` and the refill
+// threshold (AA_LQ_REFILL, default 60 idle lanes)
+LocalQueue make_local_queue(int device, int* counter) {
+    LocalQueue q;
+    q.counter = counter;
+    int cus = 0, per = 0;
+    AA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_local_z_hq<4>, kBlock, 0));
+    q.resident = std::max(1, cus * std::max(1, per));
+    const char* r = std::getenv("AA_LQ_REFILL");
+    q.refill = r ? std::atoi(r) : 60;
+    return q;
+}
+
 void launch_local_z(const GroupDev& g, const double* xfull, const double* u, double* z, double* y, int nf,
-                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s, int* queue) {
+                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s, const LocalQueue* queue) {
     if (g.count == 0) return;
     const int nb = blocks_for(g.count);
-    if (g.kind == 0 && g.mat != 0 && !red && queue) {   // hyperelastic, no partials: work queue
-        static int resident = 0;
-        if (!resident) {
-            int dev = 0, cus = 0, per = 0;
-            AA_HIP(hipGetDevice(&dev));
-            AA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_local_z_hq<4>, kBlock, 0));
-            resident = std::max(1, cus * std::max(1, per));
-        }
-        AA_HIP(hipMemsetAsync(queue, 0, sizeof(int), s));
-        static int refill = -1;
-        if (refill < 0) { const char* r = std::getenv("AA_LQ_REFILL"); refill = r ? std::atoi(r) : 60; }
+    if (g.kind == 0 && g.mat != 0 && !red && queue && queue->counter) {   // hyperelastic, no partials: work queue
+        AA_HIP(hipMemsetAsync(queue->counter, 0, sizeof(int), s));
+        const int resident = std::max(1, queue->resident), refill = queue->refill;
         hipLaunchKernelGGL(k_local_z_hq<4>, dim3(std::min(nb, resident)), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
-                           ctrl, queue, refill);
+                           ctrl, queue->counter, refill);
         AA_CHECK_LAUNCH();
         return;
     }
@@ -975,6 +1030,13 @@ void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const
 void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b, int nblocks, int accel,
                     double* hist_prim, double* hist_comb, int* hist_rej, hipStream_t s) {
     hipLaunchKernelGGL(k_control, dim3(1), dim3(kCtlBlock), 0, s, op, ctrl, red_a, red_b, nblocks, accel, hist_prim, hist_comb, hist_rej);
+    AA_CHECK_LAUNCH();
+}
+
+__global__ void k_stamp(Ctrl* ctrl) { ctrl->clock0 = (long long)wall_clock64(); }
+
+void launch_stamp(Ctrl* ctrl, hipStream_t s) {
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, s, ctrl);
     AA_CHECK_LAUNCH();
 }
 
@@ -1049,6 +1111,18 @@ void launch_aa_mix(Seg2 G, double* cur, long long eff, double* dF, double* dG, C
         case 16: hipLaunchKernelGGL(k_aa_mix<16>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
         default: hipLaunchKernelGGL(k_aa_mix<32>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
     }
+    AA_CHECK_LAUNCH();
+}
+
+void launch_test_prox(int op, const double* prm4, const double* in, int n, double* out, int* iters, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_test_prox, dim3((n + 63) / 64), dim3(64), 0, s, op, prm4[0], prm4[1], prm4[2], prm4[3], in, n, out,
+                       iters);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_test_cod(int n, const double* M, const double* b, double* x, hipStream_t s) {
+    hipLaunchKernelGGL(k_test_cod, dim3(1), dim3(kSolveBlock), 0, s, n, M, b, x);
     AA_CHECK_LAUNCH();
 }
 

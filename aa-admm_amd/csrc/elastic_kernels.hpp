@@ -36,7 +36,16 @@ struct Ctrl {
     double M[kMaxM * kMaxM];      // normal-equation matrix, column-major m x m
     // Geometry ALM loop (ALMGeometrySolver.h:186-263): `reset` flag and accepted-iteration cap
     int alm_reset, max_iter;
+    // time-to-epsilon: device clock (wall_clock64) of every recorded iteration and
+    // of the step's start; optional stop once comb <= eps_rel * comb of the first recorded
+    // iteration (eps_rel = 0: the reference's loop, only the comb < 1e-20 break).
+    long long* hist_clock;
+    long long clock0;
+    double eps_rel, eps_abs;
+    int eps_hit, pad_;
 };
+// device stamp of the step's start (ctrl->clock0)
+void launch_stamp(Ctrl* ctrl, hipStream_t s);
 
 // A vector seen as two concatenated segments (e.g. (u, x) of the UX variant).
 struct Seg2 {
@@ -56,10 +65,18 @@ struct ElasticLaunch;  // fwd
 // ---- launchers (elastic_kernels.hip) ---------------------------------------------------
 enum LocalMode { LZ_NORMAL = 0, LZ_REDO = 1, LZ_INIT = 2 };
 
+// Work queue of the hyperelastic local step: a device counter, the resident grid on the solver's
+// device and the refill threshold (computed once per solver, make_local_queue)
+struct LocalQueue {
+    int* counter = nullptr;
+    int resident = 0, refill = 60;
+};
+LocalQueue make_local_queue(int device, int* counter);
 // z = prox(P x + u/w); prim partials; optional y = w(w z + c - u). gate: !done (and reject for REDO)
-// queue: one device int; hyperelastic groups without partials then run as a persistent work queue
+// queue given: hyperelastic groups without partials run as a persistent work queue
 void launch_local_z(const GroupDev& g, const double* xfull, const double* u, double* z, double* y, int nf,
-                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s, int* queue = nullptr);
+                    int variant, int mode, Ctrl* ctrl, double* red, int red_off, hipStream_t s,
+                    const LocalQueue* queue = nullptr);
 // r = w(P x - z); prim2/dual2 partials; u += r (UX variant update_u fused with the residual)
 void launch_resid_update_u(const GroupDev& g, const double* xfull, const double* xlast, const double* z, double* u,
                            int nf, Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s);
@@ -111,5 +128,9 @@ void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, doub
 void launch_aa_solve(Ctrl* ctrl, const double* red, int nblocks, int m, hipStream_t s);
 void launch_aa_mix(Seg2 G, double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, Seg2 out, int m,
                    hipStream_t s);
+
+// ---- element-level test hooks (aa_test_* in the C ABI; tests only)
+void launch_test_prox(int op, const double* prm4, const double* in, int n, double* out, int* iters, hipStream_t s);
+void launch_test_cod(int n, const double* M, const double* b, double* x, hipStream_t s);
 
 }  // namespace aa

@@ -182,8 +182,7 @@ void GeomSolver::add_constraints(int hard, int type, const int* idx, int k, int 
     if (type < GEO_PLANE || type > GEO_REF_SURFACE) throw Error(ERR_ARG, "add_constraints: unknown constraint type");
     const int want = type == GEO_ANGLE ? 3 : type == GEO_EDGE ? 2 : type == GEO_PLANE ? k : 1;
     if (k != want) throw Error(ERR_ARG, "add_constraints: wrong number of indices for this constraint type");
-    if (type == GEO_PLANE && (k < 3 || k > kGeoMaxK))
-        throw Error(ERR_ARG, "add_constraints: plane constraints need 3..8 points on this device path");
+    if (type == GEO_PLANE && k < 3) throw Error(ERR_ARG, "add_constraints: plane constraints need at least 3 points");
     if (!(weight >= 0.0)) throw Error(ERR_ARG, "add_constraints: weight must be >= 0");
     const int P = n_params(type);
     if (P && !params) throw Error(ERR_ARG, "add_constraints: this constraint type needs parameters");
@@ -268,7 +267,10 @@ void GeomSolver::setup(int n_points, double penalty, int spd_solver_type) {
     arows_.assign(n_, {});
     for (auto& g : hgroups_) {
         for (int v : g.idx) if (v >= n_) throw Error(ERR_ARG, "constraint references a point index >= n_points");
-        const double w = g.hard ? 1.0 : std::sqrt(g.weight);
+        // ALM: soft rows weighted, hard rows x rho; GeometrySolver: every row unweighted, x rho
+        // (GeometrySolver.h:100-119)
+        const double w = (g.hard || plain_) ? 1.0 : std::sqrt(g.weight);
+        const double scale = (g.hard || plain_) ? rho_ : 1.0;
         const std::vector<double> D = reduction_block(g.type, g.K, w);
         const int C = cols_of(g.type, g.K), K = g.K;
         std::vector<double> DtD((size_t)K * K, 0.0);
@@ -276,7 +278,7 @@ void GeomSolver::setup(int n_points, double penalty, int spd_solver_type) {
             for (int b = 0; b < K; ++b) {
                 double sacc = 0;
                 for (int r = 0; r < C; ++r) sacc += D[(size_t)r * K + a] * D[(size_t)r * K + b];
-                DtD[(size_t)a * K + b] = (g.hard ? rho_ : 1.0) * sacc;
+                DtD[(size_t)a * K + b] = scale * sacc;
             }
         const int cnt = g.count();
         for (int c = 0; c < cnt; ++c) {
@@ -422,7 +424,7 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
                 lg.idx.insert(lg.idx.end(), hg.idx.begin() + (size_t)e * K, hg.idx.begin() + (size_t)(e + 1) * K);
                 lg.prm.insert(lg.prm.end(), hg.prm.begin() + (size_t)e * Pn, hg.prm.begin() + (size_t)(e + 1) * Pn);
             }
-            if (hg.hard)
+            if (has_u(hg))
                 for (int r = 0; r < P; ++r) { br[r] += geo_u_blocks(c[r]); zr[r] += 3LL * C * c[r]; }
             owned.push_back(std::move(lg));
         }
@@ -453,10 +455,12 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
         dg.idx.upload(idx, s());
         dg.prm.upload(prm, s());
         GeoGroupDev& d = dg.d;
-        d.type = hg.type; d.K = K; d.cols = C; d.hard = hg.hard; d.count = cnt;
+        d.type = hg.type; d.K = K; d.cols = C; d.hard = has_u(hg) ? 1 : 0; d.count = cnt;
         d.sw = std::sqrt(hg.weight);
-        d.yscale = hg.hard ? rho_ : hg.weight;
-        d.uoff = hg.hard ? Zh_ : 0;
+        d.yscale = d.hard ? rho_ : hg.weight;
+        // project_and_combine's a = rho / (w + rho), w = weight_^2 (Constraint.h:125-128)
+        d.comb_a = (plain_ && !hg.hard) ? rho_ / (d.sw * d.sw + rho_) : 0.0;
+        d.uoff = d.hard ? Zh_ : 0;
         d.slot0 = slots_;
         d.idx = dg.idx.p;
         d.prm = dg.prm.p;
@@ -467,8 +471,8 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
             d.warm = dg.warm.p;
             d.surf = surfs_[hg.surf].dev();
         }
-        if (hg.hard) { Zh_ += 3LL * C * cnt; red_blocks_ += geo_u_blocks(cnt); }
-        else soft_cols += (long long)C * cnt;
+        if (d.hard) { Zh_ += 3LL * C * cnt; red_blocks_ += geo_u_blocks(cnt); }
+        if (!hg.hard) soft_cols += (long long)C * cnt;
         slots_ += (long long)K * cnt;
         ncons += cnt;
     }
@@ -513,7 +517,7 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     AA_HIP(hipStreamSynchronize(s()));
     factored_ = true;
     cur_m_ = -1;
-    rt_.hard_cols = (long long)(Zh_ / 3);
+    rt_.hard_cols = (long long)(Zh_ / 3) - (plain_ ? soft_cols : 0);
     rt_.soft_cols = soft_cols;
     rt_.n_constraints = ncons;
     rt_.factor_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -540,7 +544,7 @@ void GeomSolver::prepare_m(int m) {
     const long long dim = Zh_ + 3LL * n_;
     if (m > 0) {
         aa_cur_.alloc(dim);
-        aa_dF_.alloc((size_t)m * dim); aa_dF_.zero(s());
+        aa_dF_.alloc((size_t)m * (plain_ ? std::max<long long>(1, Zh_) : dim)); aa_dF_.zero(s());
         aa_dG_.alloc((size_t)m * dim); aa_dG_.zero(s());
         aa_blocks_ = aa_reduce_blocks(zh_max_ + 3LL * n_);   // the same grid on every rank
         const int mm = m <= 8 ? 8 : (m <= 16 ? 16 : 32);
@@ -584,7 +588,88 @@ void GeomSolver::prologue(const double* init_x3, int max_iter, int m, int cap) {
     c.aa_m = m;
     c.aa_active = m > 0 ? 1 : 0;
     AA_HIP(hipMemcpyAsync(ctrl_.p, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s()));
+    if (plain_) {
+        // GeometrySolver::ADMM_init_variables (GeometrySolver.h:356-382): one z / x / u update
+        // from (init_x, 0), then current = default; the accelerator starts from it
+        const long long nx = 3LL * n_;
+        int off = 0;
+        for (auto& g : groups_) {
+            launch_geo_z_plain(g.d, cur_x_.p, cur_u_.p, z_.p, y_.p, ctrl_.p, nullptr, 0, 0, s());
+            off += geo_u_blocks(g.d.count);
+        }
+        launch_geo_rhs(n_, slot_ptr_.p, slot_idx_.p, y_.p, rhs_fixed_.p, b_.p, ctrl_.p, s());
+        solver_.solve(b_.p, new_x_.p, ctrl_.p, 0, s());
+        enqueue_u_update(red_.p, s());
+        if (Zh_) launch_copy(cur_u_.p, new_u_.p, Zh_, ctrl_.p, 0, s());
+        launch_copy(cur_x_.p, new_x_.p, nx, ctrl_.p, 0, s());
+        if (m > 0) {
+            if (Zh_) launch_copy(aa_cur_.p, new_u_.p, Zh_, ctrl_.p, 0, s());
+            launch_copy(aa_cur_.p + Zh_, new_x_.p, nx, ctrl_.p, 0, s());
+        }
+    }
     launch_geo_start(ctrl_.p, clock0_.p, s());
+}
+
+// ADMM_u_update (+ the ALM residual partials): u_new = u + T(x_new) - z on every group with u
+void GeomSolver::enqueue_u_update(double* red, hipStream_t st) {
+    int off = 0;
+    for (auto& g : groups_) {
+        if (!g.d.hard) continue;
+        launch_geo_u(g.d, new_x_.p, cur_x_.p, z_.p, cur_u_.p, new_u_.p, ctrl_.p, red, off, st);
+        off += geo_u_blocks(g.d.count);
+    }
+}
+
+// one pass of the while-loop body of GeometrySolver::solve_ADMM (Geometry/GeometrySolver.h:180-251)
+void GeomSolver::enqueue_iteration_plain(int m) {
+    Ctrl* c = ctrl_.p;
+    const long long nx = 3LL * n_;
+    auto z_update = [&](int gate) {
+        int off = 0;
+        for (auto& g : groups_) {
+            launch_geo_z_plain(g.d, cur_x_.p, cur_u_.p, z_.p, y_.p, c, red_.p, off, gate, s());
+            off += geo_u_blocks(g.d.count);
+        }
+        if (comm_) comm_->allreduce_sum(red_.p, red_g_.p, (size_t)nbg_, s());
+    };
+    ev_mark("z");
+    z_update(0);                                                                         // ADMM_z_update
+    ev_mark("z");
+    launch_plain_control(c, redg_, nbg_, m > 0, 0, hist_comb_.p, hist_clock_.p, s());  // residual, reset test
+    if (m > 0) {   // residual increased: swap to the un-accelerated (u, x), accelerator->replace, redo
+        launch_geo_restore(cur_u_.p, cur_x_.p, aa_cur_.p, new_u_.p, new_x_.p, Zh_, nx, c, s());
+        z_update(1);
+        launch_plain_control(c, redg_, nbg_, 1, 1, hist_comb_.p, hist_clock_.p, s());
+    }
+    ev_mark("rhs");
+    launch_geo_rhs(n_, slot_ptr_.p, slot_idx_.p, y_.p, rhs_fixed_.p, b_.p, c, s());     // ADMM_x_update
+    ev_mark("rhs");
+    ev_mark("solve");
+    solver_.solve(b_.p, new_x_.p, c, 0, s());
+    ev_mark("solve");
+    ev_mark("u");
+    enqueue_u_update(red_.p, s());                                                       // ADMM_u_update
+    ev_mark("u");
+    ev_mark("aa");
+    if (m > 0) {   // aa->compute(default_u, default_x, current_u, current_x): u is the effective part
+        Seg2 G{new_u_.p, Zh_, new_x_.p, nx};
+        Seg2 none{nullptr, 0, nullptr, 0};
+        Seg2 out{cur_u_.p, Zh_, cur_x_.p, nx};
+        launch_aa_reduce(G, aa_cur_.p, Zh_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, none, m, s(), nullptr,
+                         nullptr, 0, nullptr, nullptr, nullptr, aamask_);
+        if (comm_) comm_->allreduce_sum(aa_red_.p, aa_red_g_.p, aa_red_.n, s());
+        launch_aa_solve(c, aag_, aa_blocks_, m, s());
+        launch_aa_mix(G, aa_cur_.p, Zh_, aa_dF_.p, aa_dG_.p, c, out, m, s());
+        if (instrument_ && n_mk_log_ < (int)(mk_log_.n / 2)) {
+            AA_HIP(hipMemcpyAsync(mk_log_.p + 2 * n_mk_log_, &c->aa_mk, sizeof(int), hipMemcpyDeviceToDevice, s()));
+            AA_HIP(hipMemcpyAsync(mk_log_.p + 2 * n_mk_log_ + 1, &c->aa_skip, sizeof(int), hipMemcpyDeviceToDevice, s()));
+            ++n_mk_log_;
+        }
+    } else {   // swap(default, current)
+        if (Zh_) launch_copy(cur_u_.p, new_u_.p, Zh_, c, 0, s());
+        launch_copy(cur_x_.p, new_x_.p, nx, c, 0, s());
+    }
+    ev_mark("aa");
 }
 
 void GeomSolver::ev_mark(const char* name) {
@@ -597,6 +682,7 @@ void GeomSolver::ev_mark(const char* name) {
 
 // one pass of the while-loop body of solve_ADMM (ALMGeometrySolver.h:197-267)
 void GeomSolver::enqueue_iteration(int m) {
+    if (plain_) return enqueue_iteration_plain(m);
     Ctrl* c = ctrl_.p;
     const long long nx = 3LL * n_;
     ev_mark("z");
@@ -609,12 +695,7 @@ void GeomSolver::enqueue_iteration(int m) {
     solver_.solve(b_.p, new_x_.p, c, 0, s());                                           // SPD_solver_->solve
     ev_mark("solve");
     ev_mark("u");
-    int off = 0;
-    for (auto& g : groups_) {                                                            // ADMM_u_update + residual
-        if (!g.d.hard) continue;
-        launch_geo_u(g.d, new_x_.p, cur_x_.p, z_.p, cur_u_.p, new_u_.p, c, red_.p, off, s());
-        off += geo_u_blocks(g.d.count);
-    }
+    enqueue_u_update(red_.p, s());                                                       // ADMM_u_update + residual
     ev_mark("u");
     ev_mark("aa");
     if (comm_) comm_->allreduce_sum(red_.p, red_g_.p, (size_t)nbg_, s());
@@ -629,6 +710,11 @@ void GeomSolver::enqueue_iteration(int m) {
         if (comm_) comm_->allreduce_sum(aa_red_.p, aa_red_g_.p, aa_red_.n, s());
         launch_aa_solve(c, aag_, aa_blocks_, m, s());
         launch_aa_mix(G, aa_cur_.p, Zh_ + nx, aa_dF_.p, aa_dG_.p, c, out, m, s());
+        if (instrument_ && n_mk_log_ < (int)(mk_log_.n / 2)) {   // this launch's window / skip flag
+            AA_HIP(hipMemcpyAsync(mk_log_.p + 2 * n_mk_log_, &c->aa_mk, sizeof(int), hipMemcpyDeviceToDevice, s()));
+            AA_HIP(hipMemcpyAsync(mk_log_.p + 2 * n_mk_log_ + 1, &c->aa_skip, sizeof(int), hipMemcpyDeviceToDevice, s()));
+            ++n_mk_log_;
+        }
     } else {
         if (Zh_) launch_copy(cur_u_.p, new_u_.p, Zh_, c, 0, s());
         launch_copy(cur_x_.p, new_x_.p, nx, c, 0, s());
@@ -705,25 +791,27 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
     }
     fetch_results();
     if (comm_) {   // every rank ends with the full solution: zero what it does not own, sum
+        double* sol = solution_buf();
         auto zero = [&](int q0, int q1) {
-            if (q1 > q0) AA_HIP(hipMemsetAsync(new_x_.p + 3 * (size_t)q0, 0, 24 * (size_t)(q1 - q0), s()));
+            if (q1 > q0) AA_HIP(hipMemsetAsync(sol + 3 * (size_t)q0, 0, 24 * (size_t)(q1 - q0), s()));
         };
         zero(0, own_beg_);
         zero(own_end_, top_beg_);
         if (rank_ != 0) zero(top_beg_, n_);
-        comm_->allreduce_sum(new_x_.p, new_x_.p, 3 * (size_t)n_, s());
+        comm_->allreduce_sum(sol, sol, 3 * (size_t)n_, s());
         AA_HIP(hipStreamSynchronize(s()));
     }
     have_solution_ = true;
     rt_.solve_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// get_solution (ALMGeometrySolver.h:280-282) = default_x_: the x of the last accepted iteration,
-// which is the last x-update since the loop always ends on an acceptance
+// get_solution: ALM (ALMGeometrySolver.h:280-282) = default_x_, the x of the last accepted
+// iteration, which is the last x-update since the loop always ends on an acceptance;
+// GeometrySolver (GeometrySolver.h:254-256) = *current_x_
 void GeomSolver::get_solution(double* x3) const {
     if (!have_solution_) throw Error(ERR_STATE, "get_solution before solve_ADMM");
     std::vector<double> x(3 * (size_t)n_);
-    AA_HIP(hipMemcpy(x.data(), new_x_.p, x.size() * 8, hipMemcpyDeviceToHost));
+    AA_HIP(hipMemcpy(x.data(), plain_ ? cur_x_.p : new_x_.p, x.size() * 8, hipMemcpyDeviceToHost));
     for (int q = 0; q < n_; ++q)
         for (int d = 0; d < 3; ++d) x3[3 * (size_t)int2user_[q] + d] = x[3 * (size_t)q + d];
 }
@@ -751,6 +839,8 @@ double GeomSolver::bench_iterations(int iters) {
     if (!setup_done_ || !factored_ || cur_m_ < 0) throw Error(ERR_STATE, "bench before solve_ADMM");
     for (auto& kv : kstats_) { for (auto e : kv.second.ev) (void)hipEventDestroy(e); kv.second.ev.clear(); }
     prologue(last_init_.data(), 1 << 30, cur_m_, iters + 1);
+    mk_log_.alloc(2 * (size_t)std::max(1, iters));
+    n_mk_log_ = 0;
     AA_HIP(hipStreamSynchronize(s()));
     instrument_ = true;
     hipEvent_t e0, e1;
@@ -771,6 +861,17 @@ double GeomSolver::bench_iterations(int iters) {
             AA_HIP(hipEventElapsedTime(&t, k.ev[i], k.ev[i + 1]));
             k.total_ms += t; k.launches += 1;
         }
+    }
+    if (cur_m_ > 0 && n_mk_log_ > 0) {
+        // Anderson bytes of each launch from the window it actually used (mk < m while a window
+        // fills or after a reset; an ALM reject skips the step and only restores u, x)
+        std::vector<int> lg(2 * (size_t)n_mk_log_);
+        AA_HIP(hipMemcpy(lg.data(), mk_log_.p, lg.size() * sizeof(int), hipMemcpyDeviceToHost));
+        const double dim = (double)Zh_ + 3.0 * n_;
+        double tot = 0;
+        for (int k = 0; k < n_mk_log_; ++k)
+            tot += lg[2 * k + 1] ? 16.0 * dim : 8.0 * dim * (2.0 * lg[2 * k] + 8.0);
+        kstats_["aa"].bytes = tot / n_mk_log_;
     }
     fetch_results();
     return ms;

@@ -18,7 +18,8 @@ namespace aa {
 
 class GeomSolver {
 public:
-    explicit GeomSolver(Context* ctx) : ctx_(ctx) {}
+    // plain = false: ALMGeometrySolver<3>; true: GeometrySolver<3> (Geometry/GeometrySolver.h)
+    explicit GeomSolver(Context* ctx, bool plain = false) : ctx_(ctx), plain_(plain) {}
     ~GeomSolver();
 
     int add_ref_surface(const double* V3, int nv, const int* F3, int nf);
@@ -61,6 +62,8 @@ private:
     struct Reg { std::vector<int> idx; std::vector<double> coef; double tgt[3]; };
 
     Context* ctx_;
+    bool plain_ = false;
+    bool has_u(const HostGroup& g) const { return plain_ || g.hard; }   // z / u columns on device
     hipStream_t s() const { return ctx_->stream; }
 
     // host model
@@ -111,6 +114,8 @@ private:
     int graph_chunk_ = 0, graph_m_ = -1;
     void drop_graph();
 
+    DevBuf<int> mk_log_;   // (aa_mk, aa_skip) per instrumented Anderson launch
+    int n_mk_log_ = 0;
     bool instrument_ = false;
     struct KStat { std::vector<hipEvent_t> ev; double bytes = 0; double total_ms = 0; int launches = 0; };
     std::map<std::string, KStat> kstats_;
@@ -120,7 +125,10 @@ private:
     void prepare_m(int m);
     void prologue(const double* init_x3, int max_iter, int m, int cap);
     void enqueue_iteration(int m);
+    void enqueue_iteration_plain(int m);
+    void enqueue_u_update(double* red, hipStream_t st);
     void fetch_results();
+    double* solution_buf() { return plain_ ? cur_x_.p : new_x_.p; }
 };
 
 }  // namespace aa

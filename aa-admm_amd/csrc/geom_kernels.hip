@@ -296,16 +296,22 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
 }
 
 // ------------------------------------------------------------------ z step
-template <int T, int K>
-__global__ __launch_bounds__(kBlock) void k_geo_z(GeoGroupDev g, const double* __restrict__ x,
-                                                  const double* __restrict__ u, double* __restrict__ z,
-                                                  double* __restrict__ y, const Ctrl* ctrl) {
-    if (gated(ctrl)) return;
+// One constraint: v = T(x) (+u), z = P(v); PLAIN (GeometrySolver<3>): soft groups combine
+// z = a v + (1 - a) P(v) (Constraint::project_and_combine, Constraint.h:118-130) and the
+// return value is this constraint's |T(x) - z|^2 (GeometrySolver::get_ADMM_residual,
+// GeometrySolver.h:459-461); ALM: returns 0.
+template <int T, int K, bool PLAIN>
+__device__ __forceinline__ double geo_z_one(const GeoGroupDev& g, int e, const double* __restrict__ x,
+                                            const double* __restrict__ u, double* __restrict__ z,
+                                            double* __restrict__ y) {
     constexpr int C = (T == GEO_ANGLE || T == GEO_EDGE) ? K - 1 : K;
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= g.count) return;
     double v[3 * C], uu[3 * C];
+    double t[PLAIN ? 3 * C : 1];
     transform<T, K>(g, e, x, v);
+    if constexpr (PLAIN) {
+#pragma unroll
+        for (int i = 0; i < 3 * C; ++i) t[i] = v[i];
+    }
     if (g.hard) {
 #pragma unroll
         for (int i = 0; i < 3 * C; ++i) { uu[i] = u[g.uoff + (size_t)i * g.count + e]; v[i] += uu[i]; }
@@ -324,17 +330,156 @@ __global__ __launch_bounds__(kBlock) void k_geo_z(GeoGroupDev g, const double* _
         for (int c = 0; c < C; ++c) {
             double qx, qy, qz;
             const int w0 = g.warm ? g.warm[e] : -1;
-            const int t = bvh_closest(g.surf, v[3 * c], v[3 * c + 1], v[3 * c + 2], w0, qx, qy, qz);
-            if (g.warm) g.warm[e] = t;
+            const int tr = bvh_closest(g.surf, v[3 * c], v[3 * c + 1], v[3 * c + 2], w0, qx, qy, qz);
+            if (g.warm) g.warm[e] = tr;
             v[3 * c] = qx; v[3 * c + 1] = qy; v[3 * c + 2] = qz;
         }
     }   // CLOSENESS: identity
+    double part = 0;
+    if constexpr (PLAIN) {   // every plain group carries u (g.hard == 1)
+        if (g.comb_a > 0) {
+            const double a = g.comb_a, b = 1.0 - g.comb_a;
+#pragma unroll
+            for (int i = 0; i < 3 * C; ++i) v[i] = (t[i] + uu[i]) * a + v[i] * b;
+        }
+#pragma unroll
+        for (int i = 0; i < 3 * C; ++i) { const double r = t[i] - v[i]; part += r * r; }
+    }
     if (g.hard) {
 #pragma unroll
         for (int i = 0; i < 3 * C; ++i) { z[g.uoff + (size_t)i * g.count + e] = v[i]; uu[i] = v[i] - uu[i]; }
         write_slots<T, K>(g, e, uu, g.yscale, y);
     } else {
         write_slots<T, K>(g, e, v, g.yscale, y);
+    }
+    return part;
+}
+
+template <int T, int K>
+__global__ __launch_bounds__(kBlock) void k_geo_z(GeoGroupDev g, const double* __restrict__ x,
+                                                  const double* __restrict__ u, double* __restrict__ z,
+                                                  double* __restrict__ y, const Ctrl* ctrl) {
+    if (gated(ctrl)) return;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= g.count) return;
+    (void)geo_z_one<T, K, false>(g, e, x, u, z, y);
+}
+
+// GeometrySolver z-update with the residual's block partials; gate 1 = only after a residual
+// increase (the recomputation that follows the swap to the un-accelerated iterate)
+template <int T, int K>
+__global__ __launch_bounds__(kBlock) void k_geo_zp(GeoGroupDev g, const double* __restrict__ x,
+                                                   const double* __restrict__ u, double* __restrict__ z,
+                                                   double* __restrict__ y, const Ctrl* ctrl, double* red, int red_off,
+                                                   int gate) {
+    if (gated(ctrl) || (gate && !ctrl->reject)) return;
+    __shared__ double sm[kBlock / 64];
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double part = 0;
+    if (e < g.count) part = geo_z_one<T, K, true>(g, e, x, u, z, y);
+    if (red) {
+        const double sum = block_sum(part, sm);
+        if (threadIdx.x == 0) red[red_off + blockIdx.x] = sum;
+    }
+}
+
+// PlaneConstraint with any number of points (faces of valence > kGeoMaxK; PlanarityOpt.cpp:235-246
+// adds one per polygon face). The same arithmetic as plane_project<K> / write_slots<PLANE, K> in
+// the same order, with the 3 x K working rows kept in this constraint's own rhs slot rows
+// (scratch, overwritten by the final slot values) instead of registers.
+template <bool PLAIN>
+__global__ __launch_bounds__(kBlock) void k_geo_z_plane_dyn(GeoGroupDev g, const double* __restrict__ x,
+                                                            const double* __restrict__ u, double* __restrict__ z,
+                                                            double* __restrict__ y, const Ctrl* ctrl, double* red,
+                                                            int red_off, int gate) {
+    if (gated(ctrl) || (gate && !ctrl->reject)) return;
+    __shared__ double sm[kBlock / 64];
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double part = 0;
+    if (e < g.count) {
+        const int K = g.K;
+        double* yr = y + 3 * (size_t)(g.slot0 + (long long)e * K);
+        auto pt = [&](int a, int d) { return x[3 * (size_t)g.idx[(size_t)a * g.count + e] + d]; };
+        auto uat = [&](int a, int d) { return u[g.uoff + (size_t)(3 * a + d) * g.count + e]; };
+        double m[3] = {0, 0, 0};
+        for (int a = 0; a < K; ++a)
+            for (int d = 0; d < 3; ++d) m[d] += pt(a, d);
+        for (int d = 0; d < 3; ++d) m[d] /= K;
+        for (int a = 0; a < K; ++a)
+            for (int d = 0; d < 3; ++d) {
+                double v = pt(a, d) - m[d];
+                if (g.hard) v += uat(a, d);
+                yr[3 * a + d] = v;
+            }
+        double W[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+        for (int sweep = 0; sweep < 30; ++sweep) {
+            bool rotated = false;
+            for (int pr = 0; pr < 3; ++pr) {
+                const int p = pr == 2 ? 1 : 0, q = pr == 0 ? 1 : 2;
+                double aa = 0, bb = 0, gg = 0;
+                for (int k = 0; k < K; ++k) {
+                    const double rp = yr[3 * k + p], rq = yr[3 * k + q];
+                    aa += rp * rp; bb += rq * rq; gg += rp * rq;
+                }
+                if (fabs(gg) > 1e-15 * sqrt(aa * bb) && gg != 0.0) {
+                    rotated = true;
+                    const double zeta = (bb - aa) / (2.0 * gg);
+                    const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                    const double c = 1.0 / sqrt(1.0 + tt * tt), sn = c * tt;
+                    for (int k = 0; k < K; ++k) {
+                        const double rp = yr[3 * k + p], rq = yr[3 * k + q];
+                        yr[3 * k + p] = c * rp - sn * rq;
+                        yr[3 * k + q] = sn * rp + c * rq;
+                    }
+                    for (int k = 0; k < 3; ++k) {
+                        const double wp = W[p][k], wq = W[q][k];
+                        W[p][k] = c * wp - sn * wq;
+                        W[q][k] = sn * wp + c * wq;
+                    }
+                }
+            }
+            if (!rotated) break;
+        }
+        double nr[3];
+        for (int d = 0; d < 3; ++d) {
+            double sq = 0;
+            for (int k = 0; k < K; ++k) sq += yr[3 * k + d] * yr[3 * k + d];
+            nr[d] = sq;
+        }
+        int i = 0;
+        if (nr[1] < nr[i]) i = 1;
+        if (nr[2] < nr[i]) i = 2;
+        double n0 = W[i][0], n1 = W[i][1], n2 = W[i][2];
+        const double l = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+        if (l > 0) { n0 /= l; n1 /= l; n2 /= l; }
+        double qm[3] = {0, 0, 0};
+        for (int a = 0; a < K; ++a) {
+            double t[3], uu[3] = {0, 0, 0}, v[3];
+            for (int d = 0; d < 3; ++d) {
+                t[d] = pt(a, d) - m[d];
+                if (g.hard) uu[d] = uat(a, d);
+                v[d] = g.hard ? t[d] + uu[d] : t[d];
+            }
+            const double dp = n0 * v[0] + n1 * v[1] + n2 * v[2];
+            double q[3] = {v[0] - n0 * dp, v[1] - n1 * dp, v[2] - n2 * dp};
+            if constexpr (PLAIN) {
+                if (g.comb_a > 0)
+                    for (int d = 0; d < 3; ++d) q[d] = v[d] * g.comb_a + q[d] * (1.0 - g.comb_a);
+                for (int d = 0; d < 3; ++d) { const double r = t[d] - q[d]; part += r * r; }
+            }
+            for (int d = 0; d < 3; ++d) {
+                if (g.hard) { z[g.uoff + (size_t)(3 * a + d) * g.count + e] = q[d]; q[d] -= uu[d]; }
+                yr[3 * a + d] = q[d];
+                qm[d] += q[d];
+            }
+        }
+        for (int d = 0; d < 3; ++d) qm[d] /= K;
+        for (int a = 0; a < K; ++a)
+            for (int d = 0; d < 3; ++d) yr[3 * a + d] = g.yscale * (yr[3 * a + d] - qm[d]);
+    }
+    if (red) {
+        const double sum = block_sum(part, sm);
+        if (threadIdx.x == 0) red[red_off + blockIdx.x] = sum;
     }
 }
 
@@ -364,6 +509,38 @@ __global__ __launch_bounds__(kBlock) void k_geo_u(GeoGroupDev g, const double* _
     }
     const double s = block_sum(part, sm);
     if (threadIdx.x == 0) red[red_off + blockIdx.x] = s;
+}
+
+// k_geo_u of a plane group with any number of points (same arithmetic and order as transform<PLANE, K>)
+__global__ __launch_bounds__(kBlock) void k_geo_u_plane_dyn(GeoGroupDev g, const double* __restrict__ xnew,
+                                                            const double* __restrict__ xcur, const double* __restrict__ z,
+                                                            const double* __restrict__ u, double* __restrict__ unew,
+                                                            const Ctrl* ctrl, double* red, int red_off) {
+    if (gated(ctrl)) return;
+    __shared__ double sm[kBlock / 64];
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double part = 0;
+    if (e < g.count) {
+        const int K = g.K;
+        double mn[3] = {0, 0, 0}, mp[3] = {0, 0, 0};
+        for (int a = 0; a < K; ++a) {
+            const size_t v = 3 * (size_t)g.idx[(size_t)a * g.count + e];
+            for (int d = 0; d < 3; ++d) { mn[d] += xnew[v + d]; mp[d] += xcur[v + d]; }
+        }
+        for (int d = 0; d < 3; ++d) { mn[d] /= K; mp[d] /= K; }
+        for (int a = 0; a < K; ++a) {
+            const size_t v = 3 * (size_t)g.idx[(size_t)a * g.count + e];
+            for (int d = 0; d < 3; ++d) {
+                const size_t o = g.uoff + (size_t)(3 * a + d) * g.count + e;
+                const double dn = xnew[v + d] - mn[d], dpv = xcur[v + d] - mp[d];
+                const double r = dn - z[o], dd = dn - dpv;
+                part += r * r + dd * dd;
+                unew[o] = u[o] + r;
+            }
+        }
+    }
+    const double sum = block_sum(part, sm);
+    if (threadIdx.x == 0) red[red_off + blockIdx.x] = sum;
 }
 
 // ------------------------------------------------------------------ rhs gather
@@ -413,6 +590,33 @@ __global__ __launch_bounds__(kBlock) void k_geo_control(Ctrl* ctrl, const double
     }
 }
 
+// GeometrySolver::solve_ADMM decisions (GeometrySolver.h:180-231): op 0 after the z-update --
+// residual = |Dx - z| from the partials; with Anderson, a residual above the previous one
+// flags the swap to the un-accelerated iterate (reject; the history is NOT reset: replace);
+// otherwise the iteration is recorded. op 1 (only when flagged) records the recomputed
+// residual. Recording ends the loop after max_iter iterations, else prev = residual.
+__global__ __launch_bounds__(kBlock) void k_plain_control(Ctrl* ctrl, const double* red, int nb, int accel, int op,
+                                                          double* hist_comb, unsigned long long* hist_clock) {
+    if (ctrl->done || (op == 1 && !ctrl->reject)) return;
+    __shared__ double sm[kBlock / 64];
+    double a = 0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) a += red[i];
+    a = block_sum(a, sm);
+    if (threadIdx.x != 0) return;
+    const double res = sqrt(a);
+    if (op == 0) {
+        ctrl->reject = (accel && res > ctrl->prev_prim) ? 1 : 0;
+        if (ctrl->reject) { ctrl->nrej += 1; return; }
+    }
+    ctrl->comb = res;
+    const int k = ctrl->nrec;
+    if (k < ctrl->cap) { hist_comb[k] = res; hist_clock[k] = wall_clock64(); }
+    ctrl->nrec = k + 1;
+    ctrl->iters_run += 1;
+    if (ctrl->nrec >= ctrl->max_iter) ctrl->done = 1;
+    else ctrl->prev_prim = res;
+}
+
 __global__ void k_geo_start(Ctrl* ctrl, unsigned long long* clock0) {
     (void)ctrl;
     *clock0 = wall_clock64();
@@ -437,6 +641,36 @@ __global__ __launch_bounds__(kBlock) void k_closest(SurfDev S, const double* __r
     c[3 * (size_t)i] = qx; c[3 * (size_t)i + 1] = qy; c[3 * (size_t)i + 2] = qz;
 }
 
+// test hook: Constraint::project_impl of plane (any k) / angle / edge on transformed points
+template <int K>
+__device__ void test_plane(double* v) { plane_project<K>(v); }
+
+__global__ void k_test_geo_project(int type, int k, double p0, double p1, const double* __restrict__ in, int n,
+                                   double* __restrict__ out) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const int C = (type == GEO_ANGLE || type == GEO_EDGE) ? k - 1 : k;
+    double v[3 * kGeoMaxK];
+    for (int i = 0; i < 3 * C; ++i) v[i] = in[(size_t)e * 3 * C + i];
+    if (type == GEO_PLANE) {
+        switch (k) {
+            case 3: test_plane<3>(v); break;
+            case 4: test_plane<4>(v); break;
+            case 5: test_plane<5>(v); break;
+            case 6: test_plane<6>(v); break;
+            case 7: test_plane<7>(v); break;
+            default: test_plane<8>(v); break;
+        }
+    } else if (type == GEO_ANGLE) {
+        angle_project(v, p0, p1);
+    } else if (type == GEO_EDGE) {
+        const double s2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+        const double r = s2 > 0 ? p0 / sqrt(s2) : p0;
+        v[0] *= r; v[1] *= r; v[2] *= r;
+    }
+    for (int i = 0; i < 3 * C; ++i) out[(size_t)e * 3 * C + i] = v[i];
+}
+
 inline int grid_for(long long n) { long long b = (n + kBlock - 1) / kBlock; return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048); }
 
 }  // namespace
@@ -452,7 +686,7 @@ inline int grid_for(long long n) { long long b = (n + kBlock - 1) / kBlock; retu
                 case 6: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 6>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
                 case 7: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 7>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
                 case 8: hipLaunchKernelGGL((KERNEL<GEO_PLANE, 8>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
-                default: throw Error(ERR_ARG, "plane constraint with unsupported vertex count");         \
+                default: throw Error(ERR_ARG, "plane constraint with < 3 points");                       \
             }                                                                                              \
             break;                                                                                         \
         case GEO_ANGLE: hipLaunchKernelGGL((KERNEL<GEO_ANGLE, 3>), grid, dim3(kBlock), 0, s, __VA_ARGS__); break; \
@@ -467,7 +701,29 @@ void launch_geo_z(const GeoGroupDev& g, const double* x, const double* u, double
                   hipStream_t s) {
     if (g.count == 0) return;
     const dim3 grid(blocks_for(g.count));
-    GEO_DISPATCH(k_geo_z, g, x, u, z, y, ctrl)
+    if (g.type == GEO_PLANE && g.K > kGeoMaxK) {
+        hipLaunchKernelGGL(k_geo_z_plane_dyn<false>, grid, dim3(kBlock), 0, s, g, x, u, z, y, ctrl, nullptr, 0, 0);
+    } else {
+        GEO_DISPATCH(k_geo_z, g, x, u, z, y, ctrl)
+    }
+    AA_CHECK_LAUNCH();
+}
+
+void launch_geo_z_plain(const GeoGroupDev& g, const double* x, const double* u, double* z, double* y, const Ctrl* ctrl,
+                        double* red, int red_off, int gate, hipStream_t s) {
+    if (g.count == 0) return;
+    const dim3 grid(blocks_for(g.count));
+    if (g.type == GEO_PLANE && g.K > kGeoMaxK) {
+        hipLaunchKernelGGL(k_geo_z_plane_dyn<true>, grid, dim3(kBlock), 0, s, g, x, u, z, y, ctrl, red, red_off, gate);
+    } else {
+        GEO_DISPATCH(k_geo_zp, g, x, u, z, y, ctrl, red, red_off, gate)
+    }
+    AA_CHECK_LAUNCH();
+}
+
+void launch_plain_control(Ctrl* ctrl, const double* red, int nb, int accel, int op, double* hist_comb,
+                          unsigned long long* hist_clock, hipStream_t s) {
+    hipLaunchKernelGGL(k_plain_control, dim3(1), dim3(kBlock), 0, s, ctrl, red, nb, accel, op, hist_comb, hist_clock);
     AA_CHECK_LAUNCH();
 }
 
@@ -477,7 +733,10 @@ void launch_geo_u(const GeoGroupDev& g, const double* xnew, const double* xcur, 
                   double* unew, const Ctrl* ctrl, double* red, int red_off, hipStream_t s) {
     if (g.count == 0 || !g.hard) return;
     const dim3 grid(blocks_for(g.count));
-    GEO_DISPATCH(k_geo_u, g, xnew, xcur, z, u, unew, ctrl, red, red_off)
+    if (g.type == GEO_PLANE && g.K > kGeoMaxK)
+        hipLaunchKernelGGL(k_geo_u_plane_dyn, grid, dim3(kBlock), 0, s, g, xnew, xcur, z, u, unew, ctrl, red, red_off);
+    else
+        GEO_DISPATCH(k_geo_u, g, xnew, xcur, z, u, unew, ctrl, red, red_off)
     AA_CHECK_LAUNCH();
 }
 
@@ -508,6 +767,16 @@ void launch_geo_restore(double* cu, double* cx, double* aacur, const double* du,
 void launch_closest(const SurfDev& sd, const double* p, double* c, int n, hipStream_t s) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_closest, dim3(blocks_for(n)), dim3(kBlock), 0, s, sd, p, c, n);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_test_geo_project(int type, int k, const double* prm2, const double* in, int n, double* out, hipStream_t s) {
+    if (n <= 0) return;
+    if (type == GEO_PLANE && (k < 3 || k > kGeoMaxK)) throw Error(ERR_ARG, "test hook: plane k must be 3..8 (register path)");
+    if (type == GEO_ANGLE && k != 3) throw Error(ERR_ARG, "test hook: angle k = 3");
+    if (type == GEO_EDGE && k != 2) throw Error(ERR_ARG, "test hook: edge k = 2");
+    if (type != GEO_PLANE && type != GEO_ANGLE && type != GEO_EDGE) throw Error(ERR_ARG, "test hook: plane, angle or edge");
+    hipLaunchKernelGGL(k_test_geo_project, dim3((n + 63) / 64), dim3(64), 0, s, type, k, prm2[0], prm2[1], in, n, out);
     AA_CHECK_LAUNCH();
 }
 

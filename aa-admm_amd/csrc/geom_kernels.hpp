@@ -9,7 +9,7 @@ namespace aa {
 
 // constraint types (Geometry/Constraint.h) -- must match include/aa_admm.h AA_CON_*
 enum GeoType { GEO_PLANE = 0, GEO_ANGLE = 1, GEO_EDGE = 2, GEO_CLOSENESS = 3, GEO_POINT_TO_REF = 4, GEO_REF_SURFACE = 5 };
-constexpr int kGeoMaxK = 8;   // largest plane supported on device (face valence)
+constexpr int kGeoMaxK = 8;   // planes up to this valence run in registers; larger ones in slot-row scratch
 
 // Bounding-volume hierarchy over one reference triangle surface (closest-point queries of
 // PointToRefSurfaceConstraint / ReferenceSurfceConstraint). Nodes in depth-first order:
@@ -43,6 +43,7 @@ struct GeoGroupDev {
     int count;
     double sw;            // weight_ = sqrt(weight) (Constraint.h:64-69)
     double yscale;        // scale of the rhs contribution: rho (hard) / weight (soft)
+    double comb_a;        // GeometrySolver soft groups: rho / (weight + rho) (project_and_combine); else 0
     long long uoff;       // hard: u / z offset, SoA [(c*3 + d)][count]
     long long slot0;      // first rhs slot of this group: slot(e, a) = slot0 + e*K + a
     const int* idx;       // [K][count] internal point ids
@@ -55,6 +56,15 @@ struct GeoGroupDev {
 // (hard) and the rhs slot rows y[slot] = yscale * T^T (z - u)  (hard)  /  w T^T P(Dx)  (soft)
 void launch_geo_z(const GeoGroupDev& g, const double* x, const double* u, double* z, double* y, const Ctrl* ctrl,
                   hipStream_t s);
+// GeometrySolver<3> z-update (Geometry/GeometrySolver.h:423-439): every group carries u (hard = 1),
+// soft groups combine z = a v + (1 - a) P(v) (comb_a = a); block partials of |T(x) - z|^2 into
+// red[red_off + block]; gate 1 = run only when ctrl->reject (the recomputation after a swap)
+void launch_geo_z_plain(const GeoGroupDev& g, const double* x, const double* u, double* z, double* y, const Ctrl* ctrl,
+                        double* red, int red_off, int gate, hipStream_t s);
+// GeometrySolver decisions: op 0 = residual check (reject flag / record), op 1 = record the
+// recomputed residual after a swap (see k_plain_control)
+void launch_plain_control(Ctrl* ctrl, const double* red, int nb, int accel, int op, double* hist_comb,
+                          unsigned long long* hist_clock, hipStream_t s);
 // b = rhs_fixed + sum of the slot rows of each point (fixed order)
 void launch_geo_rhs(int n, const int* ptr, const int* slots, const double* y, const double* rhs_fixed, double* b,
                     const Ctrl* ctrl, hipStream_t s);
@@ -75,5 +85,8 @@ void launch_geo_restore(double* cu, double* cx, double* aacur, const double* du,
                         long long nx, const Ctrl* ctrl, hipStream_t s);
 // closest points of `n` points (test hook / soft-energy evaluation)
 void launch_closest(const SurfDev& sd, const double* p, double* c, int n, hipStream_t s);
+
+// test hook (aa_test_geom_project): project_impl of n constraints of one type on transformed points
+void launch_test_geo_project(int type, int k, const double* prm2, const double* in, int n, double* out, hipStream_t s);
 
 }  // namespace aa

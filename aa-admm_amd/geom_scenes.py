@@ -24,7 +24,6 @@ from __future__ import annotations
 
 import dataclasses
 import math
-import struct
 from typing import List, Optional
 
 import numpy as np
@@ -73,6 +72,7 @@ class GeomScene:
     iters: int = 100
     aa_m: int = 10
     name: str = "geom"
+    solver: str = "alm"                             # "alm": ALMGeometrySolver<3>; "plain": GeometrySolver<3>
 
     @property
     def n_points(self) -> int:
@@ -324,51 +324,3 @@ def wire_grid(nx=707, ny=707, *, iters=100, aa_m=20, shear=1.2, ref_factor=2, **
 # ----------------------------------------------------------------------------------------
 # reference-driver I/O (test infrastructure; oracle/ref_drivers/ref_geom_driver.cpp)
 # ----------------------------------------------------------------------------------------
-
-def write_geom_scene(sc: GeomScene, path: str) -> None:
-    with open(path, "wb") as f:
-        f.write(b"AAGEOM01")
-        f.write(struct.pack("<i", sc.n_points))
-        f.write(np.ascontiguousarray(sc.x0, "<f8").tobytes())
-        f.write(np.ascontiguousarray(sc.ref_points, "<f8").tobytes())
-        f.write(struct.pack("<i", len(sc.surfaces)))
-        for V, F in sc.surfaces:
-            f.write(struct.pack("<ii", len(V), len(F)))
-            f.write(np.ascontiguousarray(V, "<f8").tobytes())
-            f.write(np.ascontiguousarray(F, "<i4").tobytes())
-        f.write(struct.pack("<i", len(sc.groups)))
-        for g in sc.groups:
-            npar = N_PARAMS[g.type]
-            f.write(struct.pack("<iiiidi", int(g.hard), g.type, g.k, g.count, g.weight, npar))
-            f.write(np.ascontiguousarray(g.idx, "<i4").tobytes())
-            if npar:
-                f.write(np.ascontiguousarray(g.params, "<f8").reshape(g.count, npar).tobytes())
-        r = len(sc.reg_kind)
-        f.write(struct.pack("<i", r))
-        for i in range(r):
-            a, b = sc.reg_ptr[i], sc.reg_ptr[i + 1]
-            f.write(struct.pack("<iid", int(sc.reg_kind[i]), int(b - a), float(sc.reg_weight[i])))
-            f.write(np.ascontiguousarray(sc.reg_idx[a:b], "<i4").tobytes())
-            f.write(np.ascontiguousarray(sc.reg_coef[a:b], "<f8").tobytes())
-            f.write(np.ascontiguousarray(sc.reg_target[i], "<f8").tobytes())
-        f.write(struct.pack("<dii", sc.penalty, sc.iters, sc.aa_m))
-
-
-def read_geom_result(path: str, n_points: int):
-    data = open(path, "rb").read()
-    assert data[:8] == b"AAGEOMR1", "bad result file"
-    off = 8
-
-    def take(dtype, count):
-        nonlocal off
-        a = np.frombuffer(data, dtype=dtype, count=count, offset=off)
-        off += a.nbytes
-        return a.copy()
-
-    nrec = int(take("<i4", 1)[0])
-    comb = take("<f8", nrec)
-    t = take("<f8", nrec)
-    x = take("<f8", 3 * n_points).reshape(-1, 3)
-    setup_s, loop_s = take("<f8", 2)
-    n_faces_added = int(take("<i4", 1)[0])
-    return dict(comb=comb, time_s=t, x=x, setup_s=float(setup_s), loop_s=float(loop_s), faces_added=n_faces_added)

@@ -19,13 +19,12 @@ These replace the reference's GUI sample glue that *feeds* `admm::Solver`
 
 A `Scene` is a plain container of fp64/int32 arrays -- exactly what the C ABI
 (`include/aa_admm.h`) takes -- plus the solver settings of the reference's
-`Solver::Settings` (Solver.hpp:45-67). `write_scene` serialises it for the reference
+`Solver::Settings` (Solver.hpp:45-67). `oracle/refio.write_scene` serialises it for the reference
 driver under oracle/ (test infrastructure only).
 """
 from __future__ import annotations
 
 import dataclasses
-import struct
 from typing import List, Optional
 
 import numpy as np
@@ -232,50 +231,3 @@ def beams(dim=3, *, variant=VARIANT_X, aa_m=6, iters=100, n_steps=1, accel=1, ma
     return Scene(x=x, masses=m, groups=groups, pin_idx=np.array(pins, np.int32), pin_pts=np.array(pts),
                  pin_vel=np.array(vel), variant=variant, iters=iters, aa_m=aa_m, n_steps=n_steps, accel=accel,
                  name=f"beams{dim}")
-
-
-# ----------------------------------------------------------------------------------------
-# reference-driver I/O (test infrastructure; see oracle/ref_drivers/ref_elastic_driver.cpp)
-# ----------------------------------------------------------------------------------------
-
-def write_scene(scene: Scene, path: str) -> None:
-    with open(path, "wb") as f:
-        f.write(b"AASCENE1" if scene.rest is None else b"AASCENE2")
-        f.write(struct.pack("<ii", scene.variant, scene.n_nodes))
-        f.write(np.ascontiguousarray(scene.x, dtype="<f8").tobytes())
-        if scene.rest is not None:
-            f.write(np.ascontiguousarray(scene.rest, dtype="<f8").tobytes())
-        f.write(np.repeat(np.asarray(scene.masses, dtype="<f8"), 3).tobytes())
-        f.write(struct.pack("<i", len(scene.groups)))
-        for g in scene.groups:
-            f.write(struct.pack("<iiddddi", g.kind, g.material, g.E, g.nu, g.limit_min, g.limit_max, len(g.idx)))
-            f.write(np.ascontiguousarray(g.idx, dtype="<i4").tobytes())
-        f.write(struct.pack("<i", len(scene.pin_idx)))
-        f.write(np.ascontiguousarray(scene.pin_idx, dtype="<i4").tobytes())
-        f.write(np.ascontiguousarray(scene.pin_pts, dtype="<f8").tobytes())
-        f.write(np.ascontiguousarray(scene.pin_vel, dtype="<f8").tobytes())
-        f.write(struct.pack("<dddiiii", scene.dt, scene.gravity, scene.penalty, scene.iters, scene.accel,
-                            scene.aa_m, scene.n_steps))
-
-
-def read_ref_result(path: str, n_nodes: int):
-    """Per time step: dict(prim, comb, reject, x, v) as written by the reference driver."""
-    data = open(path, "rb").read()
-    off = 0
-
-    def take(dtype, count):
-        nonlocal off
-        arr = np.frombuffer(data, dtype=dtype, count=count, offset=off)
-        off += arr.nbytes
-        return arr.copy()
-
-    n_steps = int(take("<i4", 1)[0])
-    steps = []
-    for _ in range(n_steps):
-        nrec = int(take("<i4", 1)[0])
-        steps.append(dict(prim=take("<f8", nrec), comb=take("<f8", nrec), reject=take("<i4", nrec),
-                          x=take("<f8", 3 * n_nodes).reshape(-1, 3), v=take("<f8", 3 * n_nodes).reshape(-1, 3)))
-    if off + 8 * n_steps <= len(data):
-        for s, t in zip(steps, take("<f8", n_steps)):
-            s["step_ms"] = float(t)
-    return steps

@@ -52,6 +52,9 @@ typedef struct {
     double penalty;         /* -ap   (UX variant; the Z variant uses 1)            */
     int acceleration_type;  /* 0 = NOACC, 1 = ANDERSON  (-a)                       */
     int variant;            /* AA_VARIANT_Z / AA_VARIANT_UX                        */
+    double eps_rel;         /* run-to-epsilon (new, not in the reference): > 0 ends a
+                               step once comb <= eps_rel * comb of its first iteration;
+                               0 = the reference's loop (admm_iters, comb < 1e-20 break) */
 } aa_settings;
 
 /* RuntimeData (Solver.hpp:69-80) plus device-side counters. */
@@ -100,6 +103,11 @@ int aa_elastic_set_v(aa_elastic h, const double* v3);
 /* Per-iteration (prim, comb, reject) of the last step -- the rows Solver::save() writes
  * (Solver.hpp:130-155). Returns the count in *n (<= cap copied). */
 int aa_elastic_get_history(aa_elastic h, double* prim, double* comb, int* reject, int cap, int* n);
+/* Change Settings::admm_iters / eps_rel of later steps without re-initialising (no refactor). */
+int aa_elastic_set_iterations(aa_elastic h, int admm_iters, double eps_rel);
+/* Device-clock time (ms) from the start of the last step() to the end of each recorded
+ * iteration (the reference's per-iteration elapsed times; time-to-epsilon). */
+int aa_elastic_get_times(aa_elastic h, double* time_ms, int cap, int* n);
 int aa_elastic_runtime(aa_elastic h, aa_runtime* out);                   /* runtime_data()    */
 
 /* ---- multi-GPU: mesh partitioned over the GPUs of one node -----------
@@ -140,7 +148,7 @@ typedef struct aa_geom_s* aa_geom;        /* one ALMGeometrySolver<3> instance  
 
 /* Constraint types (Geometry/Constraint.h). Index count k per constraint and the per-constraint
  * parameters each type takes (params is [count][P], row-major):
- *   AA_CON_PLANE        PlaneConstraint(idI, w)                     k = 3..8  P = 0  (:396-414)
+ *   AA_CON_PLANE        PlaneConstraint(idI, w)                     k >= 3    P = 0  (:396-414)
  *   AA_CON_ANGLE        AngleConstraint<3>(tip, s1, s2, w, min, max) k = 3     P = 2  (:220-296)
  *   AA_CON_EDGE         EdgeLengthConstraint<3>(i1, i2, w, length)   k = 2     P = 1  (:194-218)
  *   AA_CON_CLOSENESS    ClosenessConstraint<3>(i, w, target)         k = 1     P = 3  (:299-326;
@@ -172,6 +180,15 @@ typedef struct {
 } aa_geom_runtime;
 
 int aa_geom_create(aa_ctx ctx, aa_geom* out);                                  /* ALMGeometrySolver() */
+/* Solver kinds: AA_GEOM_ALM = ALMGeometrySolver<3> (Geometry/ALMGeometrySolver.h);
+ * AA_GEOM_PLAIN = GeometrySolver<3> (Geometry/GeometrySolver.h:85-263): every constraint row
+ * unweighted and scaled by the penalty, u on every column, soft constraints projected with
+ * Constraint::project_and_combine (Constraint.h:118-130), residual |Dx - z|, Anderson on (u, x)
+ * with u the effective part and `replace` (no history reset) when the residual increases;
+ * get_solution() = current_x_. Same calls otherwise.                                         */
+#define AA_GEOM_ALM 0
+#define AA_GEOM_PLAIN 1
+int aa_geom_create_kind(aa_ctx ctx, int kind, aa_geom* out);
 int aa_geom_destroy(aa_geom h);                                                /* ~ALMGeometrySolver  */
 /* Reference surface (TriMeshAABB / igl::AABB over V (nv x 3), F (nf x 3)); returns its id. */
 int aa_geom_add_ref_surface(aa_geom h, const double* V3, int nv, const int* F3, int nf, int* id);
@@ -201,6 +218,22 @@ int aa_geom_kernel_stats(aa_geom h, const char* name, double* avg_ms, double* by
  * constraints; the first solve partitions the points (nested dissection of the global matrix on
  * the initial positions) and each rank projects the constraints of its part. */
 int aa_geom_set_comm(aa_geom h, aa_comm c);
+
+/* ---- element-level test hooks (parity tests only; not part of the reference API) ----------
+ * The device functions of the local step / Anderson solve / projections applied to host arrays
+ * (uploaded, one device thread per element), so tests can pin them to the reference's element
+ * tables (tests/golden/elements.npz, geom_elements.npz) directly:
+ *   aa_test_prox: op 0 TetEnergyTerm::prox (in/out 9 per tet, TetEnergyTerm.cpp:74-96),
+ *     1 NeoHookeanTet / 2 StVKTet prox (L-BFGS, TetEnergyTerm.cpp:151-162; prm4 = E, nu, h with
+ *     vol = h^3/6; iters = L-BFGS iterations, -1 on a line-search failure), 3 / 4 TriEnergyTerm
+ *     prox of the H / X solver copy (6 per tri; prm4[2..3] = limit_min, limit_max)
+ *   aa_test_cod_solve: the Anderson normal-equation solve (Eigen CompleteOrthogonalDecomposition,
+ *     AndersonAcceleration.h:186-188) of a k x k column-major M
+ *   aa_test_geom_project: Constraint::project_impl of plane (k 3..8) / angle (k 3) / edge (k 2)
+ *     on n transformed point sets (3 x cols each, column-major); prm2 = angle min, max / edge length */
+int aa_test_prox(aa_ctx ctx, int op, const double* prm4, const double* in, int n, double* out, int* iters);
+int aa_test_cod_solve(aa_ctx ctx, int k, const double* M, const double* b, double* theta);
+int aa_test_geom_project(aa_ctx ctx, int type, int k, const double* prm2, const double* in, int n, double* out);
 
 #ifdef __cplusplus
 }

@@ -149,29 +149,40 @@ public:
         if (initialized_) push_pins();
     }
 
+    // Nodes and energy terms are handed to the device solver on the FIRST initialize(); a later
+    // initialize() re-runs only the device setup with the new settings (the reference rebuilds
+    // its matrices from the same members).
     bool initialize(const Settings& s) {
         settings_ = s;
-        int total = 0;
-        if (aa_elastic_add_nodes(h_, m_x.data(), m_masses.data(), (int)m_x.size() / 3, &total) != AA_OK) return false;
-        for (auto& e : energyterms) {
-            aa_lame l = e->lame.c();
-            const int rc = e->kind == 0
-                ? aa_elastic_add_tets(h_, e->verts.data(), e->inds.data(), e->count, e->material, &l, e->vertex_offset)
-                : aa_elastic_add_tris(h_, e->verts.data(), e->inds.data(), e->count, &l, e->vertex_offset);
-            check(rc);
+        if (!bound_) {
+            int total = 0;
+            if (aa_elastic_add_nodes(h_, m_x.data(), m_masses.data(), (int)m_x.size() / 3, &total) != AA_OK) return false;
+            for (auto& e : energyterms) {
+                aa_lame l = e->lame.c();
+                const int rc = e->kind == 0
+                    ? aa_elastic_add_tets(h_, e->verts.data(), e->inds.data(), e->count, e->material, &l, e->vertex_offset)
+                    : aa_elastic_add_tris(h_, e->verts.data(), e->inds.data(), e->count, &l, e->vertex_offset);
+                if (rc != AA_OK) return false;
+            }
+            bound_ = true;
         }
         push_pins();
         aa_settings cs{s.timestep_s, s.verbose, s.admm_iters, s.gravity, s.constraint_w, s.Anderson_m, s.penalty,
-                       (int)s.acceleration_type, s.variant};
+                       (int)s.acceleration_type, s.variant, 0.0};
         if (aa_elastic_initialize(h_, &cs) != AA_OK) return false;
         initialized_ = true;
+        v_seen_.clear();
         return true;
     }
 
+    // m_v edited by the caller between steps (the reference reads m_v directly) is pushed to the
+    // device first; m_x is a mirror of the device state (positions change only through step()).
     void step() {
+        if (!v_seen_.empty() && v_seen_ != m_v) check(aa_elastic_set_v(h_, m_v.data()));
         check(aa_elastic_step(h_));
         check(aa_elastic_get_x(h_, m_x.data()));
         check(aa_elastic_get_v(h_, m_v.data()));
+        v_seen_ = m_v;
     }
 
     const Settings& settings() const { return settings_; }
@@ -196,7 +207,8 @@ private:
     aa_ctx ctx_ = nullptr;
     aa_elastic h_ = nullptr;
     Settings settings_;
-    bool initialized_ = false;
+    bool initialized_ = false, bound_ = false;
+    VecX v_seen_;
     std::vector<int> pins_;
     std::vector<double> pin_pts_;
 };

@@ -23,8 +23,12 @@
 #define AA_GEOMETRY_HPP
 
 #include <cmath>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
 #include <memory>
 #include <stdexcept>
+#include <string>
 #include <vector>
 
 #include "aa_admm.h"
@@ -145,22 +149,25 @@ public:
     PlaneConstraint(const std::vector<int>& idI, Scalar weight) : Constraint<3>(AA_CON_PLANE, idI, weight) {}
 };
 
-template <unsigned int N>
-class ALMGeometrySolver {   // ALMGeometrySolver.h:59-320
+namespace detail {
+// The two reference solvers share their public surface; KIND selects the device loop
+// (AA_GEOM_ALM: ALMGeometrySolver.h:59-320, AA_GEOM_PLAIN: GeometrySolver.h:57-464).
+template <unsigned int N, int KIND>
+class GeometrySolverFacade {
 public:
-    static_assert(N == 3, "the MI355X path implements ALMGeometrySolver<3>");
-    explicit ALMGeometrySolver(int device = 0) {
+    static_assert(N == 3, "the MI355X path implements the N = 3 geometry solvers");
+    explicit GeometrySolverFacade(int device = 0) {
         check(aa_ctx_create(device, &ctx_));
-        check(aa_geom_create(ctx_, &h_));
+        check(aa_geom_create_kind(ctx_, KIND, &h_));
     }
-    ~ALMGeometrySolver() {
+    ~GeometrySolverFacade() {
         for (auto* c : hard_) delete c;
         for (auto* c : soft_) delete c;
         if (h_) aa_geom_destroy(h_);
         if (ctx_) aa_ctx_destroy(ctx_);
     }
-    ALMGeometrySolver(const ALMGeometrySolver&) = delete;
-    ALMGeometrySolver& operator=(const ALMGeometrySolver&) = delete;
+    GeometrySolverFacade(const GeometrySolverFacade&) = delete;
+    GeometrySolverFacade& operator=(const GeometrySolverFacade&) = delete;
 
     void add_hard_constraint(Constraint<N>* c) { hard_.push_back(c); }
     void add_soft_constraint(Constraint<N>* c) { soft_.push_back(c); }
@@ -213,7 +220,18 @@ public:
     }
     const Matrix3X& get_solution() const { return x_; }
 
-    std::vector<Scalar> function_values_;   // combined residual per accepted iteration
+    // save(Anderson_m) (ALMGeometrySolver.h:343-365, GeometrySolver.h:322-346): "elapsed\tvalue"
+    // rows, 16 digits, to ./result/residual-<m>.txt or ./result/residual-no.txt
+    void save(int Anderson_m) const {
+        const std::string file = Anderson_m > 0 ? "./result/residual-" + std::to_string(Anderson_m) + ".txt"
+                                                : std::string("./result/residual-no.txt");
+        std::ofstream ofs(file, std::ios::out | std::ios::ate);
+        if (!ofs.is_open()) { std::cout << "Cannot open: " << file << std::endl; return; }
+        ofs << std::setprecision(16);
+        for (size_t i = 0; i < elapsed_time_.size(); i++) ofs << elapsed_time_[i] << '\t' << function_values_[i] << std::endl;
+    }
+
+    std::vector<Scalar> function_values_;   // residual per (accepted) iteration
     std::vector<Scalar> elapsed_time_;      // seconds since the loop started
 
 private:
@@ -266,6 +284,23 @@ private:
             i = j;
         }
     }
+};
+}  // namespace detail
+
+// ALMGeometrySolver<3> (Geometry/ALMGeometrySolver.h): hard constraints through the augmented
+// Lagrangian, weighted soft rows, combined residual, accept/reject with Anderson reset
+template <unsigned int N>
+class ALMGeometrySolver : public detail::GeometrySolverFacade<N, AA_GEOM_ALM> {
+public:
+    explicit ALMGeometrySolver(int device = 0) : detail::GeometrySolverFacade<N, AA_GEOM_ALM>(device) {}
+};
+
+// GeometrySolver<3> (Geometry/GeometrySolver.h): all rows unweighted x penalty, soft constraints
+// through Constraint::project_and_combine, residual |Dx - z|, Anderson on (u, x) with `replace`
+template <unsigned int N>
+class GeometrySolver : public detail::GeometrySolverFacade<N, AA_GEOM_PLAIN> {
+public:
+    explicit GeometrySolver(int device = 0) : detail::GeometrySolverFacade<N, AA_GEOM_PLAIN>(device) {}
 };
 
 #endif  // AA_GEOMETRY_HPP

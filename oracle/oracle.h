@@ -44,6 +44,8 @@ void oracle_cod_solve(int n, const double* M_colmajor, const double* b, double* 
 /* Geometry ALM path (ALMGeometrySolver<3>::setup_ADMM + solve_ADMM): reads an AAGEOM01 scene
  * file, writes an AAGEOMR1 result file (formats: aa-admm_amd/geom_scenes.py). 0 on success. */
 int  oracle_geom_run_file(const char* scene_path, const char* out_path, char* err, int err_cap);
+/* mode 1: GeometrySolver<3> (Geometry/GeometrySolver.h) instead of ALMGeometrySolver<3> */
+int  oracle_geom_run_file_mode(const char* scene_path, const char* out_path, int mode, char* err, int err_cap);
 /* closest points on a triangle mesh (igl AABB::squared_distance semantics) */
 void oracle_closest_point(const double* V, int nv, const int* F, int nf, const double* P, int np, double* out);
 /* Constraint<3>::project_impl of one constraint on transformed points (3 x cols, column-major) */

@@ -314,7 +314,106 @@ struct Reader {
     }
 };
 
-int run(const char* scene_path, const char* out_path) {
+// GeometrySolver<3>::solve_ADMM (Geometry/GeometrySolver.h:153-252) + ADMM_init_variables
+// (:356-382) and the private updates (:423-461). D = [D_hard ; D_soft] (unweighted rows).
+int run_plain(std::vector<Con>& hard, std::vector<Con>& soft, const std::vector<TriSurface>& surf,
+              const std::vector<std::vector<std::pair<int, double>>>& Dh,
+              const std::vector<std::vector<std::pair<int, double>>>& Ds, const std::vector<double>& rhs_fixed,
+              const std::vector<int>& perm, Envelope& chol, int n, double rho, int max_iter, int m,
+              const std::vector<double>& x0, const char* out_path, double setup_s) {
+    const int Zh = 3 * (int)Dh.size(), Z = Zh + 3 * (int)Ds.size();
+    std::vector<double> x1(x0), x2(x0), u1(Z, 0.0), u2(Z, 0.0), Dx(Z), Dxu(Z), z(Z), b(3 * (size_t)n);
+    std::vector<double>*cx = &x1, *dx = &x2, *cu = &u1, *du = &u2;
+    auto compute_Dx = [&](const std::vector<double>& x) {
+        for (auto& c : hard) apply_transform(c, x.data(), Dx.data());
+        for (auto& c : soft) { Con cc = c; cc.idO += Zh / 3; apply_transform(cc, x.data(), Dx.data()); }
+    };
+    auto z_update = [&]() {
+        for (int i = 0; i < Z; ++i) Dxu[i] = Dx[i] + (*cu)[i];
+        for (auto& c : hard) project(c, surf, Dxu.data(), z.data(), false);
+        for (auto& c : soft) {   // project_and_combine (Constraint.h:118-130)
+            Con cc = c; cc.idO += Zh / 3;
+            project(cc, surf, Dxu.data(), z.data(), false);
+            const double w = c.sw * c.sw, a = rho / (w + rho);
+            const size_t o = 3 * (size_t)cc.idO;
+            for (int i = 0; i < 3 * c.cols(); ++i) z[o + i] = Dxu[o + i] * a + z[o + i] * (1 - a);
+        }
+    };
+    auto x_update = [&]() {   // default_x = A^-1 (rhs_fixed + rho D^T (z - u))
+        b = rhs_fixed;
+        int row = 0;
+        for (auto* D : {&Dh, &Ds})
+            for (auto& rr : *D) {
+                for (auto& e : rr)
+                    for (int d = 0; d < 3; ++d) b[3 * (size_t)e.first + d] += rho * e.second * (z[3 * (size_t)row + d] - (*cu)[3 * (size_t)row + d]);
+                ++row;
+            }
+        std::vector<double> bp(3 * (size_t)n);
+        for (int i = 0; i < n; ++i) for (int d = 0; d < 3; ++d) bp[3 * (size_t)perm[i] + d] = b[3 * (size_t)i + d];
+        chol.solve3(bp.data());
+        for (int i = 0; i < n; ++i) for (int d = 0; d < 3; ++d) (*dx)[3 * (size_t)i + d] = bp[3 * (size_t)perm[i] + d];
+    };
+    auto u_update = [&]() { for (int i = 0; i < Z; ++i) (*du)[i] = (*cu)[i] + Dx[i] - z[i]; };
+    auto residual = [&]() { double s = 0; for (int i = 0; i < Z; ++i) { const double r = Dx[i] - z[i]; s += r * r; } return std::sqrt(s); };
+    // ADMM_init_variables
+    compute_Dx(*cx); z_update(); x_update(); compute_Dx(*dx); u_update();
+    *cx = *dx; *cu = *du;
+    Anderson aa;
+    std::vector<double> g((size_t)Z + 3 * (size_t)n), o(g.size());
+    auto pack = [&](const std::vector<double>& u, const std::vector<double>& x) {
+        std::copy(u.begin(), u.end(), g.begin());
+        std::copy(x.begin(), x.end(), g.begin() + Z);
+    };
+    if (m > 0) { pack(*cu, *cx); aa.init(m, (int)g.size(), Z, g.data()); }
+    std::vector<double> comb_hist, time_hist;
+    double prev = std::numeric_limits<double>::max();
+    int iter_count = 0, x_updates = 0;
+    auto tl = std::chrono::steady_clock::now();
+    for (;;) {
+        z_update();
+        double cur = residual();
+        if (m > 0 && cur > prev) {   // swap to the un-accelerated iterate, accelerator->replace
+            std::swap(cx, dx); std::swap(cu, du);
+            pack(*cu, *cx); aa.replace(g.data());
+            compute_Dx(*cx); z_update(); cur = residual();
+        }
+        ++iter_count;
+        comb_hist.push_back(cur);
+        time_hist.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - tl).count());
+        if (iter_count >= max_iter) break;
+        prev = cur;
+        x_update(); ++x_updates;
+        compute_Dx(*dx);
+        u_update();
+        if (m > 0) {
+            pack(*du, *dx);
+            aa.compute(g.data(), o.data());
+            std::copy(o.begin(), o.begin() + Z, cu->begin());
+            std::copy(o.begin() + Z, o.end(), cx->begin());
+        } else { std::swap(du, cu); std::swap(dx, cx); }
+        compute_Dx(*cx);
+    }
+    const double loop_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tl).count();
+    FILE* o2 = fopen(out_path, "wb");
+    if (!o2) throw std::runtime_error("cannot open output");
+    fwrite("AAGEOMR1", 1, 8, o2);
+    const int nrec = (int)comb_hist.size();
+    fwrite(&nrec, 4, 1, o2);
+    fwrite(comb_hist.data(), 8, nrec, o2);
+    fwrite(time_hist.data(), 8, nrec, o2);
+    fwrite(cx->data(), 8, 3 * (size_t)n, o2);   // get_solution() = *current_x_ (GeometrySolver.h:254-256)
+    fwrite(&setup_s, 8, 1, o2);
+    fwrite(&loop_s, 8, 1, o2);
+    fwrite(&x_updates, 4, 1, o2);
+    fclose(o2);
+    return 0;
+}
+
+// plain = true: GeometrySolver<3> (Geometry/GeometrySolver.h:85-263) instead of the ALM solver --
+// all constraint rows unweighted and scaled by rho, u on every column, soft constraints
+// projected with project_and_combine (Constraint.h:118-130), residual |Dx - z| after the z-update,
+// Anderson on (u, x) with u the effective part, `replace` (no history reset) on a residual increase
+int run(const char* scene_path, const char* out_path, bool plain) {
     FILE* f = fopen(scene_path, "rb");
     if (!f) throw std::runtime_error("cannot open scene");
     Reader r{f};
@@ -392,14 +491,14 @@ int run(const char* scene_path, const char* out_path) {
     std::vector<std::vector<std::pair<int, double>>> Dh, Ds;
     int zc = 0, sc = 0;
     for (auto& c : hard) add_rows(c, false, zc, Dh);
-    for (auto& c : soft) add_rows(c, true, sc, Ds);
+    for (auto& c : soft) add_rows(c, !plain, sc, Ds);
     // global = rho Dh^T Dh + Ds^T Ds + L^T L (scalar n x n), rhs_fixed = L^T b
     std::vector<std::vector<std::pair<int, double>>> Arows(n);
     auto accum = [&](const std::vector<std::pair<int, double>>& row, double s) {
         for (auto& a : row) for (auto& b : row) Arows[a.first].push_back({b.first, s * a.second * b.second});
     };
     for (auto& row : Dh) accum(row, rho);
-    for (auto& row : Ds) accum(row, 1.0);
+    for (auto& row : Ds) accum(row, plain ? rho : 1.0);
     std::vector<double> rhs_fixed(3 * (size_t)n, 0.0);
     for (auto& g : regs) {
         std::vector<std::pair<int, double>> row;
@@ -433,6 +532,8 @@ int run(const char* scene_path, const char* out_path) {
     const int Zh = 3 * zc, Zs = 3 * sc;
     auto t1 = std::chrono::steady_clock::now();
 
+    if (plain) return run_plain(hard, soft, surf, Dh, Ds, rhs_fixed, perm, chol, n, rho, max_iter, m, x0, out_path,
+                                std::chrono::duration<double>(t1 - t0).count());
     // ---- solve_ADMM
     const bool accel = m > 0;
     std::vector<double> cur_x(x0), def_x(x0), new_x(3 * (size_t)n), cur_u(Zh, 0.0), def_u(Zh, 0.0), new_u(Zh);
@@ -525,8 +626,13 @@ int run(const char* scene_path, const char* out_path) {
 }  // namespace oracle
 
 extern "C" int oracle_geom_run_file(const char* scene_path, const char* out_path, char* err, int err_cap) {
+    return oracle_geom_run_file_mode(scene_path, out_path, 0, err, err_cap);
+}
+
+extern "C" int oracle_geom_run_file_mode(const char* scene_path, const char* out_path, int plain, char* err,
+                                         int err_cap) {
     try {
-        return oracle::run(scene_path, out_path);
+        return oracle::run(scene_path, out_path, plain != 0);
     } catch (const std::exception& e) {
         if (err && err_cap > 0) { std::strncpy(err, e.what(), err_cap - 1); err[err_cap - 1] = 0; }
         return -1;

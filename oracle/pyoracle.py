@@ -11,6 +11,11 @@ import subprocess
 
 import numpy as np
 
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import refio  # noqa: E402  (same directory; test infrastructure)
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
@@ -139,7 +144,7 @@ def cod_solve(M, b):
 
 
 def run_geom(scene):
-    """Runs the oracle's ALM restatement on a geom_scenes.GeomScene; dict like read_geom_result
+    """Runs the oracle's ALM (or, scene.solver == "plain", GeometrySolver) restatement on a geom_scenes.GeomScene; dict like read_geom_result
     (`faces_added` carries the number of x-updates, i.e. accepted + rejected iterations)."""
     import importlib
     import sys
@@ -149,12 +154,13 @@ def run_geom(scene):
     L = lib()
     with tempfile.TemporaryDirectory() as tmp:
         sp, op = os.path.join(tmp, "s.bin"), os.path.join(tmp, "o.bin")
-        gs.write_geom_scene(scene, sp)
+        refio.write_geom_scene(scene, sp)
         err = C.create_string_buffer(512)
-        rc = L.oracle_geom_run_file(sp.encode(), op.encode(), err, C.c_int(512))
+        rc = L.oracle_geom_run_file_mode(sp.encode(), op.encode(), C.c_int(1 if scene.solver == "plain" else 0), err,
+                                         C.c_int(512))
         if rc != 0:
             raise RuntimeError("oracle: " + err.value.decode())
-        res = gs.read_geom_result(op, scene.n_points)
+        res = refio.read_geom_result(op, scene.n_points)
     res["x_updates"] = res.pop("faces_added")
     return res
 

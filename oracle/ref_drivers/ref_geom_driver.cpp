@@ -15,7 +15,16 @@
 //     add_laplacian / add_relative_laplacian / add_closeness (ALMGeometrySolver.h:296-318)
 //     setup_ADMM(n, penalty, LDLT) (:81-161), solve_ADMM(x0, eps, iters, m) (:163-283)
 //   -> AAGEOMR1 result: function_values_, elapsed_time_, get_solution(), timings.
+// Built with -DREF_PLAIN (oracle/_ref/ref_geom_plain) the same scene drives the reference's
+// GeometrySolver<3> instead (Geometry/GeometrySolver.h:85-263: project_and_combine for the
+// soft constraints, Anderson on (u, x) with `replace` on a residual increase).
+#ifdef REF_PLAIN
+#include "GeometrySolver.h"
+typedef GeometrySolver<3> RefSolver;
+#else
 #include "ALMGeometrySolver.h"
+typedef ALMGeometrySolver<3> RefSolver;
+#endif
 #include "Constraint.h"
 #include "MeshTypes.h"
 #include "TriMeshAABB.h"
@@ -81,7 +90,7 @@ int main(int argc, char** argv) {
     }
     Eigen::Map<const Matrix3X> X0(x0.data(), 3, n), REF(refp.data(), 3, n);
 
-    ALMGeometrySolver<3> solver;
+    RefSolver solver;
     const int n_groups = r.get<int>();
     for (int gi = 0; gi < n_groups; ++gi) {
         const int hard = r.get<int>(), type = r.get<int>(), k = r.get<int>(), count = r.get<int>();

@@ -1,0 +1,110 @@
+"""Reference-driver I/O (TEST INFRASTRUCTURE, not product code): serialises scenes.Scene /
+geom_scenes.GeomScene for the headless drivers under oracle/ref_drivers/ (which run the
+reference compiled from its own sources, oracle/Makefile) and the oracle's C++ restatement,
+and reads their results back. Used by tests/, tests/golden/make_golden*.py, smoke() and
+bench.py's cpu_baseline leg only.
+
+File formats: oracle/ref_drivers/ref_elastic_driver.cpp (AASCENE1/2) and
+ref_geom_driver.cpp (the geometry scene / result layout).
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+
+
+def _n_params(ctype):
+    import importlib
+    return importlib.import_module("aa-admm_amd.geom_scenes").N_PARAMS[ctype]
+
+def write_scene(scene: Scene, path: str) -> None:
+    with open(path, "wb") as f:
+        f.write(b"AASCENE1" if scene.rest is None else b"AASCENE2")
+        f.write(struct.pack("<ii", scene.variant, scene.n_nodes))
+        f.write(np.ascontiguousarray(scene.x, dtype="<f8").tobytes())
+        if scene.rest is not None:
+            f.write(np.ascontiguousarray(scene.rest, dtype="<f8").tobytes())
+        f.write(np.repeat(np.asarray(scene.masses, dtype="<f8"), 3).tobytes())
+        f.write(struct.pack("<i", len(scene.groups)))
+        for g in scene.groups:
+            f.write(struct.pack("<iiddddi", g.kind, g.material, g.E, g.nu, g.limit_min, g.limit_max, len(g.idx)))
+            f.write(np.ascontiguousarray(g.idx, dtype="<i4").tobytes())
+        f.write(struct.pack("<i", len(scene.pin_idx)))
+        f.write(np.ascontiguousarray(scene.pin_idx, dtype="<i4").tobytes())
+        f.write(np.ascontiguousarray(scene.pin_pts, dtype="<f8").tobytes())
+        f.write(np.ascontiguousarray(scene.pin_vel, dtype="<f8").tobytes())
+        f.write(struct.pack("<dddiiii", scene.dt, scene.gravity, scene.penalty, scene.iters, scene.accel,
+                            scene.aa_m, scene.n_steps))
+
+
+def read_ref_result(path: str, n_nodes: int):
+    """Per time step: dict(prim, comb, reject, x, v) as written by the reference driver."""
+    data = open(path, "rb").read()
+    off = 0
+
+    def take(dtype, count):
+        nonlocal off
+        arr = np.frombuffer(data, dtype=dtype, count=count, offset=off)
+        off += arr.nbytes
+        return arr.copy()
+
+    n_steps = int(take("<i4", 1)[0])
+    steps = []
+    for _ in range(n_steps):
+        nrec = int(take("<i4", 1)[0])
+        steps.append(dict(prim=take("<f8", nrec), comb=take("<f8", nrec), reject=take("<i4", nrec),
+                          x=take("<f8", 3 * n_nodes).reshape(-1, 3), v=take("<f8", 3 * n_nodes).reshape(-1, 3)))
+    if off + 8 * n_steps <= len(data):
+        for s, t in zip(steps, take("<f8", n_steps)):
+            s["step_ms"] = float(t)
+    return steps
+
+
+def write_geom_scene(sc: GeomScene, path: str) -> None:
+    with open(path, "wb") as f:
+        f.write(b"AAGEOM01")
+        f.write(struct.pack("<i", sc.n_points))
+        f.write(np.ascontiguousarray(sc.x0, "<f8").tobytes())
+        f.write(np.ascontiguousarray(sc.ref_points, "<f8").tobytes())
+        f.write(struct.pack("<i", len(sc.surfaces)))
+        for V, F in sc.surfaces:
+            f.write(struct.pack("<ii", len(V), len(F)))
+            f.write(np.ascontiguousarray(V, "<f8").tobytes())
+            f.write(np.ascontiguousarray(F, "<i4").tobytes())
+        f.write(struct.pack("<i", len(sc.groups)))
+        for g in sc.groups:
+            npar = _n_params(g.type)
+            f.write(struct.pack("<iiiidi", int(g.hard), g.type, g.k, g.count, g.weight, npar))
+            f.write(np.ascontiguousarray(g.idx, "<i4").tobytes())
+            if npar:
+                f.write(np.ascontiguousarray(g.params, "<f8").reshape(g.count, npar).tobytes())
+        r = len(sc.reg_kind)
+        f.write(struct.pack("<i", r))
+        for i in range(r):
+            a, b = sc.reg_ptr[i], sc.reg_ptr[i + 1]
+            f.write(struct.pack("<iid", int(sc.reg_kind[i]), int(b - a), float(sc.reg_weight[i])))
+            f.write(np.ascontiguousarray(sc.reg_idx[a:b], "<i4").tobytes())
+            f.write(np.ascontiguousarray(sc.reg_coef[a:b], "<f8").tobytes())
+            f.write(np.ascontiguousarray(sc.reg_target[i], "<f8").tobytes())
+        f.write(struct.pack("<dii", sc.penalty, sc.iters, sc.aa_m))
+
+
+def read_geom_result(path: str, n_points: int):
+    data = open(path, "rb").read()
+    assert data[:8] == b"AAGEOMR1", "bad result file"
+    off = 8
+
+    def take(dtype, count):
+        nonlocal off
+        a = np.frombuffer(data, dtype=dtype, count=count, offset=off)
+        off += a.nbytes
+        return a.copy()
+
+    nrec = int(take("<i4", 1)[0])
+    comb = take("<f8", nrec)
+    t = take("<f8", nrec)
+    x = take("<f8", 3 * n_points).reshape(-1, 3)
+    setup_s, loop_s = take("<f8", 2)
+    n_faces_added = int(take("<i4", 1)[0])
+    return dict(comb=comb, time_s=t, x=x, setup_s=float(setup_s), loop_s=float(loop_s), faces_added=n_faces_added)

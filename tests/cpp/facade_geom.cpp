@@ -4,7 +4,8 @@
 // constraints as optimize_mesh does (new PointToRefSurfaceConstraint / PlaneConstraint /
 // AngleConstraint / EdgeLengthConstraint ..., add_*laplacian, add_closeness), runs
 // setup_ADMM + solve_ADMM and writes function_values_ and get_solution() to a binary file.
-//   facade_geom scene.bin out.bin
+//   facade_geom scene.bin out.bin [eps] [plain]
+// "plain" drives GeometrySolver<3> (Geometry/GeometrySolver.h) instead of ALMGeometrySolver<3>.
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -26,8 +27,8 @@ struct Reader {
 };
 }  // namespace
 
-int main(int argc, char** argv) {
-    if (argc < 3) { std::fprintf(stderr, "usage: facade_geom scene.bin out.bin\n"); return 2; }
+template <class Solver>
+int run(int argc, char** argv) {
     Reader r(argv[1]);
     char magic[8];
     r.f.read(magic, 8);
@@ -45,7 +46,7 @@ int main(int argc, char** argv) {
         auto F = r.vec<int>(3 * (size_t)nf);
         surf.push_back(std::make_shared<TriMeshAABB>(V, F));
     }
-    ALMGeometrySolver<3> solver;
+    Solver solver;
     const int ng = r.get<int>();
     for (int gi = 0; gi < ng; ++gi) {
         const int hard = r.get<int>(), type = r.get<int>(), k = r.get<int>(), count = r.get<int>();
@@ -99,4 +100,10 @@ int main(int argc, char** argv) {
     o.write(reinterpret_cast<const char*>(solver.get_solution().data()), 24 * (size_t)n);
     std::printf("%d %.17g %.17g\n", nf, nf ? solver.function_values_[0] : 0.0, nf ? solver.function_values_.back() : 0.0);
     return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) { std::fprintf(stderr, "usage: facade_geom scene.bin out.bin [eps] [plain]\n"); return 2; }
+    if (argc > 4 && std::strcmp(argv[4], "plain") == 0) return run<GeometrySolver<3>>(argc, argv);
+    return run<ALMGeometrySolver<3>>(argc, argv);
 }

@@ -22,6 +22,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import refio  # noqa: E402
 scenes = importlib.import_module("aa-admm_amd.scenes")
 from golden_io import save_case  # noqa: E402
 
@@ -57,12 +59,12 @@ def _with(scene, **kw):
 def run_ref(scene, tmp):
     path_in = os.path.join(tmp, "scene.bin")
     path_out = os.path.join(tmp, "out.bin")
-    scenes.write_scene(scene, path_in)
+    refio.write_scene(scene, path_in)
     drv = os.path.join(REF, "ref_elastic_h" if scene.variant == scenes.VARIANT_H else "ref_elastic_x")
     r = subprocess.run([drv, path_in, path_out], cwd=tmp, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(r.stderr)
-    return scenes.read_ref_result(path_out, scene.n_nodes)
+    return refio.read_ref_result(path_out, scene.n_nodes)
 
 
 def element_tables(tmp):
@@ -119,7 +121,40 @@ def _run_elem(buf, tmp, width, count):
     return np.fromfile(pout, dtype="<f8").reshape(count, width)
 
 
+def scene_digest(sc):
+    """sha256 over the scene arrays: full-size fixtures store outputs only (the scene is
+    regenerated by scenes.tet_drop) and this digest proves the regenerated scene is the same."""
+    import hashlib
+    h = hashlib.sha256()
+    for a in [sc.x, sc.masses] + ([sc.rest] if sc.rest is not None else []) + [g.idx for g in sc.groups]:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return np.frombuffer(h.digest(), np.uint8)
+
+
+def full_drop40(tmp):
+    """The C4 recipe at the CPU-baseline sample size (make_tet_blocks(40,16,20) = 64 000
+    NeoHookean tets, z-AA m=6, 3 time steps x 10 iterations -- the scene bench.py times the
+    reference on): the reference's per-iteration residuals, and positions / velocities on 512
+    sampled nodes plus their column sums per step (the 350 kB state itself is not stored)."""
+    sc = scenes.tet_drop(40, 16, 20, iters=10, n_steps=3)
+    steps = run_ref(sc, tmp)
+    rng = np.random.default_rng(4)
+    sample = np.sort(rng.choice(sc.n_nodes, 512, replace=False)).astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "full_drop40_z_nh_aa6.npz"), digest=scene_digest(sc), sample=sample,
+                        nrec=np.array([len(s["prim"]) for s in steps]),
+                        prim=np.concatenate([s["prim"] for s in steps]), comb=np.concatenate([s["comb"] for s in steps]),
+                        reject=np.concatenate([s["reject"] for s in steps]),
+                        x_sample=np.stack([s["x"][sample] for s in steps]),
+                        v_sample=np.stack([s["v"][sample] for s in steps]),
+                        x_sum=np.stack([s["x"].sum(0) for s in steps]), v_sum=np.stack([s["v"].sum(0) for s in steps]))
+    print("full_drop40_z_nh_aa6", [len(s["prim"]) for s in steps])
+
+
 def main(only=None):
+    if only == ["--full"]:
+        with tempfile.TemporaryDirectory() as tmp:
+            full_drop40(tmp)
+        return
     with tempfile.TemporaryDirectory() as tmp:
         for name, sc in cases().items():
             if only and name not in only:

@@ -26,6 +26,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import refio  # noqa: E402
 gs = importlib.import_module("aa-admm_amd.geom_scenes")
 from golden_io import save_geom_case  # noqa: E402
 
@@ -70,6 +72,39 @@ def mixed_scene(n=8, aa_m=6, iters=50):
     return sc
 
 
+def bigplane_scene(n=10, aa_m=6, iters=40, solver="alm"):
+    """Plane constraints of valence 4, 9 and 12 (vertex patches of a noisy quad grid) -- PlaneConstraint
+    takes any number of points (Constraint.h:396-414; PlanarityOpt.cpp:235-246 adds one per face of
+    any valence) -- hard and soft, with closeness + Laplacian regularisation."""
+    V, Q = gs.quad_grid(n, n, shear=0.7)
+    rng = np.random.default_rng(11)
+    V = V + 0.02 * rng.standard_normal(V.shape)
+    npts = len(V)
+    grid = np.arange(npts).reshape(n + 1, n + 1)
+    p12 = np.array([grid[i:i + 3, j:j + 4].ravel() for i in range(0, n - 1, 2) for j in range(0, n - 2, 3)], np.int32)
+    p9 = np.array([grid[i:i + 3, j:j + 3].ravel() for i in range(1, n - 1, 3) for j in range(1, n - 1, 2)], np.int32)
+    G = gs.ConstraintGroup
+    groups = [G(gs.PLANE, Q.astype(np.int32), 1.0, True), G(gs.PLANE, p12, 1.0, True), G(gs.PLANE, p9, 2.0, False)]
+    reg = gs.RegBuilder()
+    faces = [list(q) for q in Q]
+    rings, _ = gs.one_rings(npts, faces)
+    for v in range(npts):
+        reg.closeness(v, 1.0, V[v])
+        if rings[v] is not None and len(rings[v]) == 4:
+            reg.uniform_laplacian([v] + list(rings[v]), 0.1, relative=True)
+    sc = gs.GeomScene(x0=V, groups=groups, ref_points=V.copy(), surfaces=[], penalty=20.0, iters=iters, aa_m=aa_m,
+                      name="bigplane", solver=solver, **reg.arrays())
+    sc._avg_edge = gs.average_edge_length(V, faces)
+    return sc
+
+
+def plain(sc, penalty=10.0):
+    """The same scene driven through GeometrySolver<3> (Geometry/GeometrySolver.h)."""
+    sc.solver = "plain"
+    sc.penalty = penalty
+    return sc
+
+
 def airport(iters=100, aa_m=10):
     V, F = gs.read_obj(os.path.join(DATA, "polymesh", "airport3k_poly.obj"))
     RV, RF = gs.read_obj(os.path.join(DATA, "trimesh", "airport3k_tri.obj"))
@@ -86,16 +121,23 @@ def cases():
         "geom_mixed_noaa": mixed_scene(aa_m=0, iters=30),
         "geom_airport3k_aa10": airport(),
         "geom_airport3k_noaa": airport(iters=40, aa_m=0),
+        "geom_bigplane_aa6": bigplane_scene(),
+        # GeometrySolver<3> (project_and_combine, Anderson on (u, x) with replace)
+        "geom_plain_mixed_aa6": plain(mixed_scene(iters=40)),
+        "geom_plain_mixed_noaa": plain(mixed_scene(aa_m=0, iters=30)),
+        "geom_plain_bigplane_aa6": plain(bigplane_scene(), penalty=20.0),
+        "geom_plain_pq12_aa10": plain(gs.pq_heightfield(12, 12, iters=50, aa_m=10), penalty=1e3),
     }
 
 
 def run_ref(sc, tmp):
     pin, pout = os.path.join(tmp, "g.bin"), os.path.join(tmp, "g.out")
-    gs.write_geom_scene(sc, pin)
-    r = subprocess.run([os.path.join(REF, "ref_geom"), pin, pout], cwd=tmp, capture_output=True, text=True)
+    refio.write_geom_scene(sc, pin)
+    drv = "ref_geom_plain" if sc.solver == "plain" else "ref_geom"
+    r = subprocess.run([os.path.join(REF, drv), pin, pout], cwd=tmp, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(r.stderr)
-    return gs.read_geom_result(pout, sc.n_points)
+    return refio.read_geom_result(pout, sc.n_points)
 
 
 def run_planarity_app(tmp, iters, m):
@@ -187,10 +229,37 @@ def full_size_c3(tmp):
     print("full_c3_pq317", len(res["comb"]), res["loop_s"])
 
 
+def full_size_c5(tmp):
+    """BASELINE configs[4] at full size (707 x 707 wire mesh, 501 264 points, m = 20), 10 accepted
+    iterations of the reference (its iterations cost ~0.5 s each here): the residual curve and
+    sampled solution points."""
+    sc = gs.wire_grid(707, 707, iters=10, aa_m=20)
+    res = run_ref(sc, tmp)
+    rng = np.random.default_rng(5)
+    sample = np.sort(rng.choice(sc.n_points, 512, replace=False)).astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "full_c5_wire707.npz"), comb=res["comb"], sample=sample,
+                        x_sample=res["x"][sample], x_sum=res["x"].sum(0), x_norm=np.linalg.norm(res["x"]),
+                        digest=scene_digest(sc), ref_loop_s=res["loop_s"], ref_setup_s=res["setup_s"])
+    print("full_c5_wire707", len(res["comb"]), res["loop_s"])
+
+
 def main():
+    only = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if only:   # regenerate only these trajectory fixtures
+        with tempfile.TemporaryDirectory() as tmp:
+            for name, sc in cases().items():
+                if name in only:
+                    res = run_ref(sc, tmp)
+                    save_geom_case(os.path.join(HERE, name + ".npz"), sc, dict(comb=res["comb"], x=res["x"]))
+                    print(name, sc.n_points, len(res["comb"]), f"comb {res['comb'][0]:.4e} -> {res['comb'][-1]:.4e}")
+        return
     if "--full" in sys.argv:
         with tempfile.TemporaryDirectory() as tmp:
             full_size_c3(tmp)
+        return
+    if "--full-c5" in sys.argv:
+        with tempfile.TemporaryDirectory() as tmp:
+            full_size_c5(tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         for name, sc in cases().items():

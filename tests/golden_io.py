@@ -63,7 +63,8 @@ def case_names():
 def save_geom_case(path, sc, outputs):
     d = dict(x0=sc.x0, ref_points=sc.ref_points, reg_kind=sc.reg_kind, reg_ptr=sc.reg_ptr, reg_idx=sc.reg_idx,
              reg_coef=sc.reg_coef, reg_weight=sc.reg_weight, reg_target=sc.reg_target,
-             settings=np.array([sc.penalty, sc.iters, sc.aa_m, sc.avg_edge_length()]),
+             settings=np.array([sc.penalty, sc.iters, sc.aa_m, sc.avg_edge_length(),
+                                1.0 if getattr(sc, "solver", "alm") == "plain" else 0.0]),
              g_meta=np.array([[g.type, int(g.hard), g.k] for g in sc.groups], np.int32).reshape(-1, 3),
              g_weight=np.array([g.weight for g in sc.groups], np.float64))
     for i, g in enumerate(sc.groups):
@@ -93,7 +94,7 @@ def load_geom_case(name):
                       reg_ptr=d["reg_ptr"].astype(np.int32), reg_idx=d["reg_idx"].astype(np.int32),
                       reg_coef=d["reg_coef"], reg_weight=d["reg_weight"], reg_target=d["reg_target"],
                       ref_points=d["ref_points"], surfaces=surfaces, penalty=float(st[0]), iters=int(st[1]),
-                      aa_m=int(st[2]), name=name)
+                      aa_m=int(st[2]), name=name, solver="plain" if len(st) > 4 and st[4] == 1.0 else "alm")
     sc._avg_edge = float(st[3])
     out = {k[4:]: d[k] for k in d.files if k.startswith("out_")}
     return sc, out

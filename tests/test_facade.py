@@ -11,6 +11,7 @@ import pytest
 
 from conftest import REPO
 from golden_io import scenes
+import refio  # noqa: E402  (oracle/ on sys.path via conftest)
 
 SRC = os.path.join(REPO, "tests", "cpp", "facade_cloth.cpp")
 
@@ -32,18 +33,24 @@ def test_geometry_facade_builds(tmp_path):
     build(str(tmp_path / "facade_geom"), GEOM_SRC)
 
 
+def _plain(sc, penalty):
+    sc.solver, sc.penalty = "plain", penalty
+    return sc
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("builder", [
     lambda gs: gs.pq_heightfield(12, 10, iters=40, aa_m=10, noise=0.3),
     lambda gs: gs.wire_grid(12, 12, iters=40, aa_m=20),
+    lambda gs: _plain(gs.pq_heightfield(12, 10, iters=40, aa_m=10, noise=0.3), 1e3),   # GeometrySolver<3>
 ])
 def test_geometry_facade_matches_binding(builder, tmp_path, pkg, ctx):
     sc = builder(pkg.geom_scenes)
     exe, scene, out = str(tmp_path / "facade_geom"), str(tmp_path / "s.bin"), str(tmp_path / "o.bin")
     build(exe, GEOM_SRC)
-    pkg.geom_scenes.write_geom_scene(sc, scene)
+    refio.write_geom_scene(sc, scene)
     eps = 1e-8 * max(sc.avg_edge_length(), 1e-300)
-    r = subprocess.run([exe, scene, out, repr(eps)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, scene, out, repr(eps), sc.solver], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     raw = open(out, "rb").read()
     nf = int(np.frombuffer(raw[:4], np.int32)[0])

@@ -115,6 +115,8 @@ def test_gpu_full_size_drop_c4(pkg, ctx):
     lambda: dataclasses.replace(scenes.tet_drop(4, 2, 2, squash=1.0, iters=30, n_steps=2), gravity=0.0),
     lambda: dataclasses.replace(scenes.tet_drop(6, 2, 3, squash=0.98, iters=200, n_steps=1), gravity=0.0),
     lambda: scenes.beams(2, iters=40, n_steps=2, variant=scenes.VARIANT_X),      # rejects
+    # 64 000 tets: top supernodes wider than 256 (split-K tiles with several column tiles)
+    lambda: scenes.tet_drop(40, 16, 20, iters=12, n_steps=1),
 ])
 def test_gpu_z_pipelined_comb_bit_identical(builder, pkg, ctx, monkeypatch):
     """Z variant + Anderson: the combined-residual solve batched with the next iteration's solve
@@ -129,3 +131,100 @@ def test_gpu_z_pipelined_comb_bit_identical(builder, pkg, ctx, monkeypatch):
     for a, b in zip(seq, pipe):
         for k in ("prim", "comb", "reject", "x", "v"):
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
+
+
+def test_gpu_element_tables(pkg, ctx):
+    """The device prox functions and the Anderson COD solve on the reference's own element
+    tables (elements.npz, made by oracle/_ref/ref_element from TetEnergyTerm.cpp:74-96,151-162,
+    TriEnergyTerm.cpp:74-105 and Eigen's CompleteOrthogonalDecomposition as used by
+    AndersonAcceleration.h:186-188), at the oracle's tolerances: closed-form 1e-12, L-BFGS and
+    COD 1e-6 of the output scale."""
+    import os
+    from golden_io import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "elements.npz"))
+    capi = pkg.capi
+    got, _ = capi.hook_prox(ctx, 0, [0, 0, 0, 0], d["tet_linear_in"])
+    np.testing.assert_allclose(got, d["tet_linear_out"], rtol=0, atol=1e-12)
+    for name in ("tri_h_limits", "tri_h_free"):
+        prm = d[name + "_prm"]
+        got, _ = capi.hook_prox(ctx, 3, [0, 0, prm[2], prm[3]], d[name + "_in"])
+        np.testing.assert_allclose(got, d[name + "_out"], rtol=0, atol=1e-12)
+    for op, name in ((1, "tet_nh"), (2, "tet_stvk")):
+        E, nu, h = d[name + "_prm"][:3]
+        got, it = capi.hook_prox(ctx, op, [E, nu, h, 0], d[name + "_in"])
+        assert np.all(it > 0), it
+        for g, y in zip(got, d[name + "_out"]):
+            np.testing.assert_allclose(g, y, rtol=0, atol=1e-6 * max(1, np.linalg.norm(y)))
+    i = 0
+    while f"cod{i}_M" in d:
+        th = capi.hook_cod_solve(ctx, d[f"cod{i}_M"], d[f"cod{i}_b"])
+        ref = d[f"cod{i}_theta"]
+        np.testing.assert_allclose(th, ref, rtol=0, atol=1e-6 * max(1.0, np.linalg.norm(ref)))
+        i += 1
+    assert i == 15
+
+
+def test_gpu_full_drop40_matches_reference(pkg, ctx):
+    """The C4 recipe at the size bench.py times the reference on (make_tet_blocks(40,16,20) =
+    64 000 NeoHookean tets, 14 637 nodes, z-AA m=6, 3 time steps x 10 iterations) against the
+    reference's own run (tests/golden/full_drop40_z_nh_aa6.npz, make_golden.py --full): per-step
+    residual curves relative to comb_0 (1e-6, L-BFGS prox path), equal reject flags, positions and
+    velocities on 512 sampled nodes and their column sums (1e-6 relative)."""
+    import os
+    import sys
+    from golden_io import GOLDEN
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import scene_digest
+    ref = np.load(os.path.join(GOLDEN, "full_drop40_z_nh_aa6.npz"))
+    sc = scenes.tet_drop(40, 16, 20, iters=10, n_steps=3)
+    assert np.array_equal(scene_digest(sc), ref["digest"]), "regenerated scene differs from the fixture's"
+    got, _ = pkg.capi.run_scene(ctx, sc)
+    o = 0
+    for k, n in enumerate(ref["nrec"]):
+        h = got[k]
+        rc, rp, rr = ref["comb"][o:o + n], ref["prim"][o:o + n], ref["reject"][o:o + n]
+        o += n
+        assert len(h["comb"]) == n
+        assert np.abs(h["comb"] - rc).max() <= 1e-6 * rc[0], (k, np.abs(h["comb"] - rc).max() / rc[0])
+        assert np.abs(h["prim"] - rp).max() <= 1e-5 * rp[0]
+        assert np.array_equal(h["reject"], rr)
+        for key in ("x", "v"):
+            want = ref[key + "_sample"][k]
+            scale = np.abs(want).max()
+            assert np.abs(h[key][ref["sample"]] - want).max() <= 1e-6 * scale, (k, key)
+            assert np.allclose(h[key].sum(0), ref[key + "_sum"][k], rtol=1e-6, atol=1e-6 * scale * len(h[key]))
+
+
+@pytest.mark.parametrize("builder", [
+    lambda: scenes.tet_drop(12, 4, 6, iters=120, n_steps=2),                       # Z, pipelined comb
+    lambda: scenes.cloth(24, 24, iters=120, n_steps=2),                            # UX, fused comb record
+    lambda: scenes.tet_drop(8, 3, 4, iters=120, n_steps=1, accel=0),               # Z, no Anderson
+])
+def test_gpu_run_to_eps(builder, pkg, ctx):
+    """Run-to-epsilon (aa_settings.eps_rel / aa_elastic_set_iterations): a step ends at the first
+    iteration k with comb_k <= eps * comb_0 and is then bit-identical to a run capped at k
+    iterations (history, positions, velocities); the device-clock times are increasing."""
+    capi = pkg.capi
+    sc = builder()
+    full, s = capi.run_scene(ctx, sc)
+    eps = max(1e-6, 2.0 * max(h["comb"].min() / h["comb"][0] for h in full))   # reached in every step
+    hits = [int(np.nonzero(h["comb"] <= eps * h["comb"][0])[0][0]) + 1 for h in full]
+    s.close()
+    a = capi.solver_from_scene(ctx, sc)
+    a.initialize(capi.settings_from_scene(sc))
+    a.set_iterations(sc.iters, eps)
+    b = capi.solver_from_scene(ctx, sc)
+    b.initialize(capi.settings_from_scene(sc))
+    for k in range(sc.n_steps):
+        a.step()
+        ha, ta = a.history(), a.times()
+        b.set_iterations(hits[k], 0.0)   # the state entering step k is the same for a and b
+        b.step()
+        hb = b.history()
+        assert len(ha["comb"]) == hits[k] == a.runtime().iterations, (len(ha["comb"]), hits[k])
+        for key in ("prim", "comb", "reject"):
+            assert np.array_equal(ha[key], hb[key]), key
+        assert np.array_equal(a.x, b.x) and np.array_equal(a.v, b.v)
+        assert len(ta) == hits[k] and np.all(ta > 0) and np.all(np.diff(ta) > 0)
+    a.close(); b.close()
+
