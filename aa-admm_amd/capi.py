@@ -24,7 +24,7 @@ EXPORTS = [
     "aa_settings_default", "aa_elastic_create", "aa_elastic_destroy", "aa_elastic_add_nodes", "aa_elastic_add_tets",
     "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
-    "aa_elastic_get_times", "aa_elastic_set_iterations",
+    "aa_elastic_get_times", "aa_elastic_set_iterations", "aa_elastic_set_x",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats",
     "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_destroy", "aa_comm_info",
     "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
@@ -260,6 +260,13 @@ class Solver:
         out = np.zeros(3 * self.num_nodes())
         _chk(lib().aa_elastic_get_v(self.h, _dp(out)))
         return out.reshape(-1, 3)
+
+    def set_state(self, x, v):
+        """Solver::m_x / m_v assignment between steps (positions and velocities, n x 3)."""
+        x = np.ascontiguousarray(x, np.float64).reshape(-1)
+        v = np.ascontiguousarray(v, np.float64).reshape(-1)
+        _chk(lib().aa_elastic_set_x(self.h, _dp(x)))
+        _chk(lib().aa_elastic_set_v(self.h, _dp(v)))
 
     def history(self, cap=100000):
         p, c, r = np.zeros(cap), np.zeros(cap), np.zeros(cap, np.int32)

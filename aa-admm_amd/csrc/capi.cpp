@@ -176,6 +176,10 @@ int aa_elastic_set_v(aa_elastic h, const double* v3) {
     return guarded([&] { NEED(h && v3, "null argument"); h->s->set_v(v3); });
 }
 
+int aa_elastic_set_x(aa_elastic h, const double* x3) {
+    return guarded([&] { NEED(h && x3, "null argument"); h->s->set_x(x3); });
+}
+
 int aa_elastic_get_history(aa_elastic h, double* prim, double* comb, int* reject, int cap, int* n) {
     return guarded([&] {
         NEED(h, "null handle");

@@ -13,7 +13,9 @@
 // Jacobi (the projection z = sum_i f(s_i) u_i v_i^T is invariant to the SVD's sign and order
 // freedom, so only rounding differs); the 3x3 SVD is a register-resident two-sided Jacobi with
 // Eigen's 2x2 step, stopping rule and descending sort, so that the det-flip picks the same
-// singular pair.
+// singular pair. The 3x3 path is compiled without FMA contraction (Eigen's x86 build has none):
+// for a (near-)singular F the null-space pair, hence U diag(1,1,-1) V^T, is decided by rounding,
+// and only the same operation-by-operation rounding reproduces the reference's choice there.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -80,6 +82,7 @@ __device__ __forceinline__ void tri_prox(const double* z, double* out, int mode,
 struct Rot2 { double c, s; };
 
 __device__ __forceinline__ Rot2 jacobi_rot(double x, double y, double z) {  // J^T [[x y][y z]] J diagonal
+#pragma clang fp contract(off)
     Rot2 r{1.0, 0.0};
     const double deno = 2.0 * fabs(y);
     if (deno < 2.2250738585072014e-308) return r;
@@ -96,6 +99,7 @@ __device__ __forceinline__ Rot2 jacobi_rot(double x, double y, double z) {  // J
 // W, U, V row-major 3x3 in registers; one Eigen-style 2x2 step on pair (P,Q)
 template <int P, int Q>
 __device__ __forceinline__ bool jacobi_pair(double (&W)[9], double (&U)[9], double (&V)[9], double& maxDiag) {
+#pragma clang fp contract(off)
     const double thr = fmax(2.2250738585072014e-308, 2.0 * 2.220446049250313e-16 * maxDiag);
     if (!(fabs(W[P * 3 + Q]) > thr || fabs(W[Q * 3 + P]) > thr)) return false;
     // real 2x2 Jacobi SVD of [[W_pp W_pq][W_qp W_qq]]
@@ -137,6 +141,7 @@ __device__ __forceinline__ bool jacobi_pair(double (&W)[9], double (&U)[9], doub
 
 // F row-major 3x3 -> U S V^T, S descending (Eigen JacobiSVD semantics, square case)
 __device__ __forceinline__ void svd3(const double (&F)[9], double (&U)[9], double (&S)[3], double (&V)[9]) {
+#pragma clang fp contract(off)
     double scale = 0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) scale = fmax(scale, fabs(F[i]));
@@ -180,11 +185,13 @@ __device__ __forceinline__ void svd3(const double (&F)[9], double (&U)[9], doubl
 }
 
 __device__ __forceinline__ double det3rm(const double (&F)[9]) {
+#pragma clang fp contract(off)
     return F[0] * (F[4] * F[8] - F[5] * F[7]) - F[1] * (F[3] * F[8] - F[5] * F[6]) + F[2] * (F[3] * F[7] - F[4] * F[6]);
 }
 
 // z column-major 9 -> out column-major 9
 __device__ __forceinline__ void tet_linear_prox(const double* z, double* out) {
+#pragma clang fp contract(off)
     double F[9], U[9], S[3], V[9];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
@@ -203,6 +210,7 @@ __device__ __forceinline__ void tet_linear_prox(const double* z, double* out) {
 
 // k*vol*(F - U V^T)   (Z variant get_gradient of the linear tet)
 __device__ __forceinline__ void tet_linear_grad(const double* z, double kvol, double* g) {
+#pragma clang fp contract(off)
     double F[9], U[9], S[3], V[9];
 #pragma unroll
     for (int r = 0; r < 3; ++r)

@@ -805,14 +805,16 @@ void ElasticSolver::step() {
     if (!initialized_) throw Error(ERR_STATE, "step() before initialize()");
     auto t0 = std::chrono::steady_clock::now();
     const bool accel = st_.acceleration_type == 1;
+    const bool graph = use_graph_ && st_.admm_iters > 0;
+    if (graph && !gexec_) {   // pointers and control flow are fixed after initialize: capture once,
+        // before the prologue starts the step's device clock (capture is host work)
+        AA_HIP(hipStreamBeginCapture(s(), hipStreamCaptureModeThreadLocal));
+        enqueue_iterations(st_.admm_iters, accel);
+        AA_HIP(hipStreamEndCapture(s(), &graph_));
+        AA_HIP(hipGraphInstantiate(&gexec_, graph_, nullptr, nullptr, 0));
+    }
     prologue();
-    if (use_graph_ && st_.admm_iters > 0) {
-        if (!gexec_) {   // pointers and control flow are fixed after initialize: capture once
-            AA_HIP(hipStreamBeginCapture(s(), hipStreamCaptureModeThreadLocal));
-            enqueue_iterations(st_.admm_iters, accel);
-            AA_HIP(hipStreamEndCapture(s(), &graph_));
-            AA_HIP(hipGraphInstantiate(&gexec_, graph_, nullptr, nullptr, 0));
-        }
+    if (graph) {
         AA_HIP(hipGraphLaunch(gexec_, s()));
     } else {
         enqueue_iterations(st_.admm_iters, accel);
@@ -832,6 +834,17 @@ void ElasticSolver::step() {
 
 void ElasticSolver::get_x(double* out) { std::copy(x_.begin(), x_.end(), out); }
 void ElasticSolver::get_v(double* out) { std::copy(v_.begin(), v_.end(), out); }
+// Solver::m_x assignment between steps (the reference's public member): the next step starts
+// from these positions
+void ElasticSolver::set_x(const double* x3) {
+    std::copy(x3, x3 + x_.size(), x_.begin());
+    if (initialized_) {
+        std::vector<double> xs(3 * (size_t)n_);
+        for (int q = 0; q < n_; ++q) for (int j = 0; j < 3; ++j) xs[3 * (size_t)q + j] = x_[3 * (size_t)int2node_[q] + j];
+        AA_HIP(hipMemcpy(xs_.p, xs.data(), xs.size() * 8, hipMemcpyHostToDevice));
+    }
+}
+
 void ElasticSolver::set_v(const double* v3) {
     std::copy(v3, v3 + v_.size(), v_.begin());
     if (initialized_) {

@@ -39,6 +39,7 @@ public:
     void get_x(double* out);
     void get_v(double* out);
     void set_v(const double* v3);
+    void set_x(const double* x3);
     int history(double* prim, double* comb, int* rej, int cap) const;
     int times(double* time_ms, int cap) const;
     void set_iterations(int admm_iters, double eps_rel);

@@ -592,11 +592,7 @@ void GeomSolver::prologue(const double* init_x3, int max_iter, int m, int cap) {
         // GeometrySolver::ADMM_init_variables (GeometrySolver.h:356-382): one z / x / u update
         // from (init_x, 0), then current = default; the accelerator starts from it
         const long long nx = 3LL * n_;
-        int off = 0;
-        for (auto& g : groups_) {
-            launch_geo_z_plain(g.d, cur_x_.p, cur_u_.p, z_.p, y_.p, ctrl_.p, nullptr, 0, 0, s());
-            off += geo_u_blocks(g.d.count);
-        }
+        for (auto& g : groups_) launch_geo_z_plain(g.d, cur_x_.p, cur_u_.p, z_.p, y_.p, ctrl_.p, nullptr, 0, 0, s());
         launch_geo_rhs(n_, slot_ptr_.p, slot_idx_.p, y_.p, rhs_fixed_.p, b_.p, ctrl_.p, s());
         solver_.solve(b_.p, new_x_.p, ctrl_.p, 0, s());
         enqueue_u_update(red_.p, s());

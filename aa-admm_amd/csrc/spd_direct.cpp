@@ -269,6 +269,7 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree) {
             const double inv = 1.0 / dk;
             for (int i = k + 1; i < f; ++i) ck[i] *= inv;
             const long long work = (long long)(f - k) * (f - k);
+            (void)work;   // (only read by the OpenMP if-clause on the host pass)
 #pragma omp parallel for schedule(dynamic, 16) if (work > 200000)
             for (int j = k + 1; j < f; ++j) {
                 const double ljk = ck[j];

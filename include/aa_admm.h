@@ -100,6 +100,7 @@ int aa_elastic_num_nodes(aa_elastic h, int* n);
 int aa_elastic_get_x(aa_elastic h, double* x3);                          /* Solver::m_x        */
 int aa_elastic_get_v(aa_elastic h, double* v3);                          /* Solver::m_v        */
 int aa_elastic_set_v(aa_elastic h, const double* v3);
+int aa_elastic_set_x(aa_elastic h, const double* x3);                    /* Solver::m_x = x   */
 /* Per-iteration (prim, comb, reject) of the last step -- the rows Solver::save() writes
  * (Solver.hpp:130-155). Returns the count in *n (<= cap copied). */
 int aa_elastic_get_history(aa_elastic h, double* prim, double* comb, int* reject, int cap, int* n);

@@ -171,17 +171,20 @@ public:
                        (int)s.acceleration_type, s.variant, 0.0};
         if (aa_elastic_initialize(h_, &cs) != AA_OK) return false;
         initialized_ = true;
+        x_seen_.clear();
         v_seen_.clear();
         return true;
     }
 
-    // m_v edited by the caller between steps (the reference reads m_v directly) is pushed to the
-    // device first; m_x is a mirror of the device state (positions change only through step()).
+    // m_x / m_v edited by the caller between steps (the reference reads them directly) are pushed
+    // to the device first.
     void step() {
+        if (!x_seen_.empty() && x_seen_ != m_x) check(aa_elastic_set_x(h_, m_x.data()));
         if (!v_seen_.empty() && v_seen_ != m_v) check(aa_elastic_set_v(h_, m_v.data()));
         check(aa_elastic_step(h_));
         check(aa_elastic_get_x(h_, m_x.data()));
         check(aa_elastic_get_v(h_, m_v.data()));
+        x_seen_ = m_x;
         v_seen_ = m_v;
     }
 
@@ -208,7 +211,7 @@ private:
     aa_elastic h_ = nullptr;
     Settings settings_;
     bool initialized_ = false, bound_ = false;
-    VecX v_seen_;
+    VecX x_seen_, v_seen_;
     std::vector<int> pins_;
     std::vector<double> pin_pts_;
 };

@@ -146,8 +146,8 @@ def test_gpu_geom_error_behaviour(pkg, ctx):
     with pytest.raises(capi.AAError) as e:             # solve before setup ("solver not initialized")
         g.solve(np.zeros((4, 3)), 1e-8, 10, 0)
     assert e.value.code == -2
-    with pytest.raises(capi.AAError):                  # plane with 9 points: beyond the device path
-        g.add_constraints(True, capi.AA_CON_PLANE, np.arange(9)[None], 1.0)
+    with pytest.raises(capi.AAError):                  # a plane needs at least 3 points (any valence above)
+        g.add_constraints(True, capi.AA_CON_PLANE, np.arange(2)[None], 1.0)
     with pytest.raises(capi.AAError):                  # angle constraints take exactly 3 indices
         g.add_constraints(True, capi.AA_CON_ANGLE, np.arange(4)[None], 1.0, np.array([[0.5, 2.0]]))
     with pytest.raises(capi.AAError):                  # unknown reference surface
