@@ -40,11 +40,6 @@ __device__ __forceinline__ bool arrive_last(int* cnt, int nt, int lane) {
     return (int)prev == nt - 1;
 }
 
-__device__ __forceinline__ double ld_sc1(const double* p) {   // L1-bypassing load (in-launch hand-offs)
-    return __longlong_as_double((long long)__hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT));
-}
-
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -58,30 +53,18 @@ __device__ __forceinline__ double wsum(double v) {
 // solver's own vectors (Y, U, split-K partials, LDS) are NR-interleaved, and every offset the
 // host built for 3 columns is scaled by NR / 3 on the device. Each column's sums run in the
 // same order for NR = 3 and 6, so a batched solve is bit-identical to two single ones.
-// SC1: values handed between workgroups of one launch (persistent sweeps) are stored write-
-// through and loaded past L1 (MI355X_MICROARCH.md "Valid forms", row 1)
-template <int NR, bool SC1 = false>
+template <int NR>
 __device__ __forceinline__ void ld_ext(const double* __restrict__ P0, const double* __restrict__ P1, size_t node,
                                        double* a) {
     const size_t o = 3 * node;
-    if constexpr (SC1) {
-        a[0] = ld_sc1(P0 + o); a[1] = ld_sc1(P0 + o + 1); a[2] = ld_sc1(P0 + o + 2);
-        if constexpr (NR == 6) { a[3] = ld_sc1(P1 + o); a[4] = ld_sc1(P1 + o + 1); a[5] = ld_sc1(P1 + o + 2); }
-    } else {
-        a[0] = P0[o]; a[1] = P0[o + 1]; a[2] = P0[o + 2];
-        if constexpr (NR == 6) { a[3] = P1[o]; a[4] = P1[o + 1]; a[5] = P1[o + 2]; }
-    }
+    a[0] = P0[o]; a[1] = P0[o + 1]; a[2] = P0[o + 2];
+    if constexpr (NR == 6) { a[3] = P1[o]; a[4] = P1[o + 1]; a[5] = P1[o + 2]; }
 }
-template <int NR, bool SC1 = false>
+template <int NR>
 __device__ __forceinline__ void st_ext(double* P0, double* P1, size_t node, const double* a) {
     const size_t o = 3 * node;
-    if constexpr (SC1) {
-        st_sc1(P0 + o, a[0]); st_sc1(P0 + o + 1, a[1]); st_sc1(P0 + o + 2, a[2]);
-        if constexpr (NR == 6) { st_sc1(P1 + o, a[3]); st_sc1(P1 + o + 1, a[4]); st_sc1(P1 + o + 2, a[5]); }
-    } else {
-        P0[o] = a[0]; P0[o + 1] = a[1]; P0[o + 2] = a[2];
-        if constexpr (NR == 6) { P1[o] = a[3]; P1[o + 1] = a[4]; P1[o + 2] = a[5]; }
-    }
+    P0[o] = a[0]; P0[o + 1] = a[1]; P0[o + 2] = a[2];
+    if constexpr (NR == 6) { P1[o] = a[3]; P1[o + 1] = a[4]; P1[o + 2] = a[5]; }
 }
 template <int NR>
 __device__ __forceinline__ void zero(double* a) {
@@ -92,7 +75,7 @@ __device__ __forceinline__ void zero(double* a) {
 // front row q of a supernode (any record with beg, p, ell_w, ell_off): [b_P ; 0]_q + the
 // children's update entries landing on it (ELL pull list: ell_w offsets into U per row, -1 =
 // none; fixed order -> deterministic)
-template <int NR, bool SC1 = false, class N>
+template <int NR, class N>
 __device__ __forceinline__ void front_row(const N& t, int q, const long long* __restrict__ ell,
                                           const double* __restrict__ B0, const double* __restrict__ B1,
                                           const double* __restrict__ U, double* a) {
@@ -104,7 +87,7 @@ __device__ __forceinline__ void front_row(const N& t, int q, const long long* __
         if (o >= 0) {
             const double* u = U + (NR / 3) * o;
 #pragma unroll
-            for (int j = 0; j < NR; ++j) a[j] += SC1 ? ld_sc1(u + j) : u[j];
+            for (int j = 0; j < NR; ++j) a[j] += u[j];
         }
     }
 }
@@ -150,7 +133,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
 }
 
 // [y_P ; -x_B]_r of a supernode (backward input vector)
-template <int NR, bool SC1 = false, class N>
+template <int NR, class N>
 __device__ __forceinline__ void bwd_row(const N& t, int r, const int* __restrict__ bnd, const double* __restrict__ Y,
                                         const double* __restrict__ X0, const double* __restrict__ X1, double* v) {
     if (r < t.p) {
@@ -158,7 +141,7 @@ __device__ __forceinline__ void bwd_row(const N& t, int r, const int* __restrict
 #pragma unroll
         for (int k = 0; k < NR; ++k) v[k] = y[k];
     } else {
-        ld_ext<NR, SC1>(X0, X1, (size_t)bnd[t.bnd_off + r - t.p], v);
+        ld_ext<NR>(X0, X1, (size_t)bnd[t.bnd_off + r - t.p], v);
 #pragma unroll
         for (int k = 0; k < NR; ++k) v[k] = -v[k];
     }
@@ -218,15 +201,16 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
     const int lane = tid & 63, w = tid >> 6;
     const int c = t.c0 + 2 * lane;   // columns c, c+1 (c+1 may be the zero pad column)
     constexpr int per = kBwdTileRows / 4;
+    constexpr int kPf = kBwdPrefetch < per ? kBwdPrefetch : per;
     const int i0 = w * per, i1 = min(i0 + per, t.nr);
-    // the first kBwdPrefetch rows of this lane's G slice are loaded before the vector slice is
+    // the first kPf rows of this lane's G slice are loaded before the vector slice is
     // staged, so their latency overlaps the gathers of bwd_row and the barrier
     const double2* G = reinterpret_cast<const double2*>(Gr + t.goff + (size_t)t.r0 * t.ldr + c);
     const int ld2 = t.ldr / 2;
-    double2 gp[kBwdPrefetch > 0 ? kBwdPrefetch : 1];
+    double2 gp[kPf > 0 ? kPf : 1];
     if (c < t.p) {
 #pragma unroll
-        for (int q = 0; q < kBwdPrefetch; ++q)
+        for (int q = 0; q < kPf; ++q)
             if (i0 + q < i1) gp[q] = G[(size_t)(i0 + q) * ld2];
     }
     for (int i = tid; i < t.nr; i += 256) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
@@ -235,7 +219,7 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
     zero<W>(a);
     if (c < t.p) {
 #pragma unroll
-        for (int q = 0; q < kBwdPrefetch; ++q) {
+        for (int q = 0; q < kPf; ++q) {
             if (i0 + q >= i1) break;
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
@@ -245,7 +229,7 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
             }
         }
 #pragma unroll 8
-        for (int i = i0 + kBwdPrefetch; i < i1; ++i) {
+        for (int i = i0 + kPf; i < i1; ++i) {
             const double2 g = G[(size_t)i * ld2];
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
@@ -308,14 +292,15 @@ __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tile
     const int lane = tid & 63, w = tid >> 6;
     const int r = t.r0 + lane;
     constexpr int per = kFwdTileCols / 4;
+    constexpr int kPf = kFwdPrefetch < per ? kFwdPrefetch : per;
     const int i0 = w * per, i1 = min(i0 + per, t.nc);
-    // the first kFwdPrefetch columns of this lane's G slice are loaded before the front slice is
+    // the first kPf columns of this lane's G slice are loaded before the front slice is
     // assembled, so their latency overlaps the extend-add gathers and the barrier
     const double* G = Gc + t.goff + (size_t)t.c0 * t.R + r;
-    double gp[kFwdPrefetch > 0 ? kFwdPrefetch : 1];
+    double gp[kPf > 0 ? kPf : 1];
     if (r < t.R) {
 #pragma unroll
-        for (int q = 0; q < kFwdPrefetch; ++q)
+        for (int q = 0; q < kPf; ++q)
             if (i0 + q < i1) gp[q] = G[(size_t)(i0 + q) * t.R];
     }
     // this tile's slice of the front f_P = b_P + extend-add of the children's update vectors
@@ -325,13 +310,13 @@ __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tile
     zero<NR>(a);
     if (r < t.R) {
 #pragma unroll
-        for (int q = 0; q < kFwdPrefetch; ++q) {
+        for (int q = 0; q < kPf; ++q) {
             if (i0 + q >= i1) break;
 #pragma unroll
             for (int k = 0; k < NR; ++k) a[k] += gp[q] * f[NR * (i0 + q) + k];
         }
 #pragma unroll 8
-        for (int i = i0 + kFwdPrefetch; i < i1; ++i) {
+        for (int i = i0 + kPf; i < i1; ++i) {
             const double g = G[(size_t)i * t.R];
 #pragma unroll
             for (int k = 0; k < NR; ++k) a[k] += g * f[NR * i + k];
@@ -508,326 +493,10 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
     }
 }
 
-
-// ============================================================ persistent sweeps above the cut
-// One launch per sweep instead of one per tree level: every workgroup dequeues tasks (row tasks
-// of small supernodes, split-K tiles of large ones) in dependency order from one head counter and
-// waits (one lane, relaxed sc1 polls, bounded) until the supernode's inputs have arrived; a
-// tile's first G columns are loaded BEFORE that wait, so they stream while it waits. Values that
-// cross workgroups inside the launch (update vectors U forward, solution rows X backward) are
-// stored write-through (sc1), drained by the storing wave, signalled by one lane after a
-// workgroup barrier, and loaded with sc1 loads (MI355X_MICROARCH.md "Valid forms", row 1). A task
-// only waits on tasks dequeued before it, which running workgroups hold: no residency
-// requirement, no deadlock. The arithmetic of every task is the per-level kernels' (same sums
-// in the same order): results are bit-identical to the level-launch path.
-constexpr int kPB = 256;
-// workgroups per CU the register budget is set for (4 -> <= 128 VGPRs, 3 -> <= 168): 3-4 tile
-// workgroups per CU keep >= 96 KB of factor loads in flight per CU (MI355X_MICROARCH.md: ~32 KB
-// streams at full rate); tighter budgets spill
-constexpr int kPWavesF = 4, kPWavesB = 3;
-constexpr unsigned kSpinCap = 1u << 22;   // ~1 s of polling: give up, flag err, keep going
-
-__device__ __forceinline__ void wait_ge(const int* ctr, int target, int* err) {
-    unsigned spins = 0;
-    while ((int)__hip_atomic_load((gu32*)const_cast<int*>(ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(8);
-        if ((++spins & 31u) == 0 &&
-            (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || spins > kSpinCap)) {
-            __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-    }
-}
-// the acquire / release form of the hand-off (plain loads and stores of U / X): one lane
-// releases after its workgroup's drained stores, one lane acquires after its poll
-__device__ __forceinline__ void acquire_agent() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-__device__ __forceinline__ void release_agent() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-__device__ __forceinline__ void signal_add(int* ctr) {
-    __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int dequeue(int* head, int* s_t) {
-    if (threadIdx.x == 0) *s_t = (int)__hip_atomic_fetch_add((gu32*)head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    return __builtin_amdgcn_readfirstlane(*s_t);   // uniform: task records load through the scalar path
-}
-
-using PTask = DirectSolver::PTask;
-
-template <int NR, int TW, bool ACQ>
-__global__ __launch_bounds__(kPB, kPWavesF) void k_fwd_persist(const PTask* __restrict__ pt, int ntask, int* head, int* farr,
-                                                     const int* __restrict__ ftgt, const Task* __restrict__ tasks,
-                                                     const FTile* __restrict__ ftiles, const FRed* __restrict__ freds,
-                                                     int* __restrict__ cnt, const double* __restrict__ Gc,
-                                                     const long long* __restrict__ ell, const double* __restrict__ B0,
-                                                     const double* __restrict__ B1, double* __restrict__ part,
-                                                     double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
-                                                     int gate_reject, int* err) {
-    if (solve_gated(ctrl, gate_reject)) return;
-    constexpr int FW = TW > DirectSolver::kWaveP ? TW : DirectSolver::kWaveP;
-    constexpr int kPf = 16;
-    // the front vector and, after a barrier, the cross-wave partials share one LDS buffer
-    constexpr int kF = NR * FW > 3 * NR * 64 ? NR * FW : 3 * NR * 64;
-    __shared__ double f[kF];
-    double (*red)[NR * 64] = reinterpret_cast<double (*)[NR * 64]>(f);
-    __shared__ int s_t;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (;;) {
-        const int ti = dequeue(head, &s_t);
-        if (ti >= ntask) break;
-        const PTask P = pt[ti];
-        if (P.kind == 0) {   // rows [r0, r0 + nr) of a small supernode: thread per row (k_fwd)
-            const Task t = tasks[P.idx];
-            const int p = t.p, R = p + t.nb;
-            if (tid == 0) { wait_ge(farr + t.node, ftgt[t.node], err); if constexpr (ACQ) acquire_agent(); }
-            __syncthreads();
-            for (int c = tid; c < p; c += kPB) front_row<NR, !ACQ>(t, c, ell, B0, B1, U, f + NR * c);
-            __syncthreads();
-            if (tid < t.nr) {
-                const int r = t.r0 + tid;
-                const double* G = Gc + t.goff + r;
-                const int cmax = r < p ? r + 1 : p;
-                double a[NR];
-                zero<NR>(a);
-#pragma unroll 8
-                for (int c = 0; c < cmax; ++c) {
-                    const double v = G[(size_t)c * R];
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
-                }
-                if (r < p) {
-                    double* y = Y + NR * (size_t)(t.beg + r);
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) y[k] = a[k];
-                } else {
-                    double fr[NR];
-                    front_row<NR, !ACQ>(t, r, ell, B0, B1, U, fr);
-                    double* u = U + (NR / 3) * t.uoff + NR * (size_t)(r - p);
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) { if constexpr (ACQ) u[k] = fr[k] - a[k]; else st_sc1(u + k, fr[k] - a[k]); }
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0 && t.parent >= 0) { if constexpr (ACQ) release_agent(); signal_add(farr + t.parent); }
-        } else {             // split-K tile of a large supernode (k_fwd_tile)
-            const FTile t = ftiles[P.idx];
-            const int r = t.r0 + lane;
-            constexpr int per = TW / 4;
-            const int i0 = w * per, i1 = min(i0 + per, t.nc);
-            const double* G = Gc + t.goff + (size_t)t.c0 * t.R + r;
-            double gp[kPf];
-            if (r < t.R) {
-#pragma unroll
-                for (int q = 0; q < kPf; ++q)
-                    if (i0 + q < i1) gp[q] = G[(size_t)(i0 + q) * t.R];
-            }
-            if (tid == 0) { wait_ge(farr + t.node, ftgt[t.node], err); if constexpr (ACQ) acquire_agent(); }
-            __syncthreads();
-            for (int i = tid; i < t.nc; i += kPB) front_row<NR, !ACQ>(t, t.c0 + i, ell, B0, B1, U, f + NR * i);
-            __syncthreads();
-            double a[NR];
-            zero<NR>(a);
-            if (r < t.R) {
-#pragma unroll
-                for (int q = 0; q < kPf; ++q) {
-                    if (i0 + q >= i1) break;
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) a[k] += gp[q] * f[NR * (i0 + q) + k];
-                }
-#pragma unroll 8
-                for (int i = i0 + kPf; i < i1; ++i) {
-                    const double g = G[(size_t)i * t.R];
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) a[k] += g * f[NR * i + k];
-                }
-            }
-            __syncthreads();   // every wave is done with f: its space takes the partials
-            if (w > 0)
-#pragma unroll
-                for (int k = 0; k < NR; ++k) red[w - 1][NR * lane + k] = a[k];
-            __syncthreads();
-            if (w == 0) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) a[k] += red[q][NR * lane + k];
-                double* o = part + (NR / 3) * t.poff + NR * lane;
-#pragma unroll
-                for (int k = 0; k < NR; ++k) st_sc1(o + k, a[k]);
-                const FRed rd = freds[t.rid];
-                if (arrive_last(cnt + t.rid, rd.nt, lane)) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    if (lane < rd.nr) {
-                        double b[NR];
-                        zero<NR>(b);
-                        const double* q = part + (NR / 3) * rd.poff + NR * lane;
-#pragma unroll 8
-                        for (int k = 0; k < rd.nt; ++k, q += NR * 64)
-#pragma unroll
-                            for (int m = 0; m < NR; ++m) b[m] += q[m];
-                        const int rr = rd.r0 + lane;
-                        if (rr < rd.p) {
-                            double* y = Y + NR * (size_t)(rd.beg + rr);
-#pragma unroll
-                            for (int k = 0; k < NR; ++k) y[k] = b[k];
-                        } else {
-                            double fr[NR];
-                            front_row<NR, !ACQ>(rd, rr, ell, B0, B1, U, fr);
-                            double* u = U + (NR / 3) * rd.uoff + NR * (size_t)(rr - rd.p);
-#pragma unroll
-                            for (int k = 0; k < NR; ++k) { if constexpr (ACQ) u[k] = fr[k] - b[k]; else st_sc1(u + k, fr[k] - b[k]); }
-                        }
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0) {
-                        __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (rd.parent >= 0) { if constexpr (ACQ) release_agent(); signal_add(farr + rd.parent); }
-                    }
-                }
-            }
-        }
-        __syncthreads();   // LDS and s_t are reused by the next task
-    }
-}
-
-template <int NR, int TW, bool ACQ>
-__global__ __launch_bounds__(kPB, kPWavesB) void k_bwd_persist(const PTask* __restrict__ pt, int ntask, int* head, int* bdone,
-                                                     const int* __restrict__ btgt, const Task* __restrict__ tasks,
-                                                     const BTile* __restrict__ btiles, const BRed* __restrict__ breds,
-                                                     int* __restrict__ cnt, const double* __restrict__ Gr,
-                                                     const int* __restrict__ bnd, const double* __restrict__ Y,
-                                                     double* __restrict__ X0, double* __restrict__ X1,
-                                                     double* __restrict__ part, const Ctrl* ctrl, int gate_reject,
-                                                     int* err) {
-    if (solve_gated(ctrl, gate_reject)) return;
-    constexpr int VW = TW > DirectSolver::kWaveR ? TW : DirectSolver::kWaveR;
-    constexpr int W = 2 * NR;
-    constexpr int kPf = 8;
-    constexpr int kV = NR * VW > 3 * W * 64 ? NR * VW : 3 * W * 64;
-    __shared__ double v[kV];
-    double (*red)[W * 64] = reinterpret_cast<double (*)[W * 64]>(v);
-    __shared__ int s_t;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (;;) {
-        const int ti = dequeue(head, &s_t);
-        if (ti >= ntask) break;
-        const PTask P = pt[ti];
-        if (P.kind == 0) {   // columns [r0, r0 + nr) of a small supernode: thread per column (k_bwd)
-            const Task t = tasks[P.idx];
-            const int R = t.p + t.nb;
-            if (tid == 0 && t.parent >= 0) { wait_ge(bdone + t.parent, btgt[t.parent], err); if constexpr (ACQ) acquire_agent(); }
-            __syncthreads();
-            for (int r = tid; r < R; r += kPB) bwd_row<NR, !ACQ>(t, r, bnd, Y, X0, X1, v + NR * r);
-            __syncthreads();
-            if (tid < t.nr) {
-                const int j = t.r0 + tid;
-                const double* G = Gr + t.goff + j;
-                const int ld = t.ldr;
-                double a[NR];
-                zero<NR>(a);
-#pragma unroll 8
-                for (int r = j; r < R; ++r) {
-                    const double g = G[(size_t)r * ld];
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
-                }
-                st_ext<NR, !ACQ>(X0, X1, (size_t)(t.beg + j), a);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) { if constexpr (ACQ) release_agent(); signal_add(bdone + t.node); }
-        } else {             // split-K tile of a large supernode (k_bwd_tile)
-            const BTile t = btiles[P.idx];
-            const int c = t.c0 + 2 * lane;
-            constexpr int per = TW / 4;
-            const int i0 = w * per, i1 = min(i0 + per, t.nr);
-            const double2* G = reinterpret_cast<const double2*>(Gr + t.goff + (size_t)t.r0 * t.ldr + c);
-            const int ld2 = t.ldr / 2;
-            double2 gp[kPf];
-            if (c < t.p) {
-#pragma unroll
-                for (int q = 0; q < kPf; ++q)
-                    if (i0 + q < i1) gp[q] = G[(size_t)(i0 + q) * ld2];
-            }
-            if (tid == 0 && t.parent >= 0) { wait_ge(bdone + t.parent, btgt[t.parent], err); if constexpr (ACQ) acquire_agent(); }
-            __syncthreads();
-            for (int i = tid; i < t.nr; i += kPB) bwd_row<NR, !ACQ>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
-            __syncthreads();
-            double a[W];
-            zero<W>(a);
-            if (c < t.p) {
-#pragma unroll
-                for (int q = 0; q < kPf; ++q) {
-                    if (i0 + q >= i1) break;
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) {
-                        const double vk = v[NR * (i0 + q) + k];
-                        a[k] += gp[q].x * vk;
-                        a[NR + k] += gp[q].y * vk;
-                    }
-                }
-#pragma unroll 8
-                for (int i = i0 + kPf; i < i1; ++i) {
-                    const double2 g = G[(size_t)i * ld2];
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) {
-                        const double vk = v[NR * i + k];
-                        a[k] += g.x * vk;
-                        a[NR + k] += g.y * vk;
-                    }
-                }
-            }
-            __syncthreads();   // every wave is done with v: its space takes the partials
-            if (w > 0)
-#pragma unroll
-                for (int k = 0; k < W; ++k) red[w - 1][W * lane + k] = a[k];
-            __syncthreads();
-            if (w == 0) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-#pragma unroll
-                    for (int k = 0; k < W; ++k) a[k] += red[q][W * lane + k];
-                double* o = part + (NR / 3) * t.poff + W * lane;
-#pragma unroll
-                for (int k = 0; k < W; ++k) st_sc1(o + k, a[k]);
-                const BRed rd = breds[t.rid];
-                if (arrive_last(cnt + t.rid, rd.nt, lane)) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    if (2 * lane < rd.nc) {
-                        double b[W];
-                        zero<W>(b);
-                        const double* q = part + (NR / 3) * rd.poff + W * lane;
-#pragma unroll 4
-                        for (int k = 0; k < rd.nt; ++k, q += W * 64)
-#pragma unroll
-                            for (int m = 0; m < W; ++m) b[m] += q[m];
-                        const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane);
-                        st_ext<NR, !ACQ>(X0, X1, xo, b);
-                        if (2 * lane + 1 < rd.nc) st_ext<NR, !ACQ>(X0, X1, xo + 1, b + NR);
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0) {
-                        __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if constexpr (ACQ) release_agent();
-                        signal_add(bdone + rd.node);
-                    }
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-
 }  // namespace
 
 void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part, int my_part,
-                         int top_beg, Comm* comm, int max_sets, bool wide) {
+                         int top_beg, Comm* comm, int max_sets, bool wide, int wave_p, int wave_r) {
     n_ = F.n;
     max_sets_ = max_sets >= 2 ? 2 : 1;
     // LDS scale the layout (fused-subtree cut, tile width) is planned for: the two-set budget
@@ -937,13 +606,18 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     const bool stats = std::getenv("AA_SOLVE_STATS") != nullptr;
     const char* sb = std::getenv("AA_SUB_BLOCK");
     sub_block_ = sb ? std::atoi(sb) : 1024;
-    const char* pf = std::getenv("AA_TILE_PREFETCH");
-    tile_pf_ = pf ? std::atoi(pf) : 1;
-    // split-K tile width (forward columns / backward rows): 256 for the two-set solves of the Z
-    // variant (C4: two-set solve 860 -> 800 us), 128 for one-set solvers (their smaller
-    // supernodes lose ~4 % with 256-wide tiles); AA_SOLVE_TILE overrides
+    // split-K tile width (forward columns / backward rows) per level: the widest of 256 / 128 /
+    // 64 that still gives the level >= min_tiles workgroups (a level of few big supernodes gets
+    // narrow tiles and enough workgroups to keep loads in flight on every CU; wide tiles keep the
+    // partial traffic low where there is parallelism anyway). Structure only: the same for
+    // one- and two-set solves. AA_SOLVE_TILE forces one width, AA_SOLVE_MIN_TILES the target.
     const char* tw = std::getenv("AA_SOLVE_TILE");
-    tile_w_ = tw ? (std::atoi(tw) >= 256 ? 256 : 128) : (KS >= 2 ? 256 : 128);
+    const char* mt = std::getenv("AA_SOLVE_MIN_TILES");
+    const int min_tiles = mt ? std::atoi(mt) : 0;   // 0: 256 everywhere (narrower measured slower on C4)
+    const char* wp = std::getenv("AA_SOLVE_WAVEP");
+    const char* wr = std::getenv("AA_SOLVE_WAVER");
+    wave_p_ = wp ? std::atoi(wp) : wave_p;
+    wave_r_ = wr ? std::atoi(wr) : wave_r;
     const int min_sub = ms ? std::atoi(ms) : 256;
     constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
     static_assert(kSubSegRows == 64, "LDS accounting below assumes 64-row segments");
@@ -1082,7 +756,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     long long poff = 0;
     auto mk = [&](int sn, int r0, int nr) {
         Task t{};
-        t.node = sn; t.r0 = r0; t.nr = nr; t.parent = F.parent[sn];
+        t.node = sn; t.r0 = r0; t.nr = nr;
         t.p = p[sn]; t.nb = nb[sn]; t.beg = beg[sn]; t.bnd_off = bnd_off[sn];
         t.ell_w = ell_w[sn];
         t.goff = goff[sn]; t.uoff = uoff[sn]; t.ell_off = ell_off[sn]; t.ldr = ldr[sn];
@@ -1090,7 +764,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     };
     levels_.clear();
     kernels_ = 0;
-    std::vector<int> uf(nn_, 0), ub(nn_, 0);   // units per supernode: forward / backward (persistent sweeps)
+
     int max_lds = 0;
     for (auto& l : hl) {
         if (l.empty()) continue;
@@ -1099,8 +773,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         bool fwave = false, bwave = false;
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
-            if (p[sn] <= kWaveP) fr = std::max(fr, R);
-            if (R <= kWaveR) br = std::max(br, p[sn]);
+            if (p[sn] <= wave_p_) fr = std::max(fr, R);
+            if (R <= wave_r_) br = std::max(br, p[sn]);
         }
         (void)fwave;
         L.fblock = fr > 128 ? 256 : (fr > 64 ? 128 : 64);
@@ -1109,38 +783,61 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         L.fwd_first = (int)tasks.size();
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
-            if (p[sn] <= kWaveP) {
-                for (int r0 = 0; r0 < R; r0 += L.fblock) { tasks.push_back(mk(sn, r0, std::min(L.fblock, R - r0))); ++uf[sn]; }
+            if (p[sn] <= wave_p_) {
+                for (int r0 = 0; r0 < R; r0 += L.fblock) tasks.push_back(mk(sn, r0, std::min(L.fblock, R - r0)));
                 L.lds_fwd = std::max(L.lds_fwd, 24 * p[sn]);
             }
         }
         L.fwd_count = (int)tasks.size() - L.fwd_first;
-        // large supernodes: split-K forward tiles (64 rows x tile_w_ columns; tiles entirely
+        // tile widths of this level (see min_tiles above)
+        auto pick = [&](auto count) {
+            if (tw) return std::atoi(tw) >= 256 ? 256 : (std::atoi(tw) >= 128 ? 128 : 64);
+            if (min_tiles <= 0) return 256;
+            for (int w : {256, 128}) if (count(w) >= min_tiles) return w;
+            return 64;
+        };
+        L.ftw = pick([&](int w) {
+            long long n = 0;
+            for (int sn : l) {
+                if (p[sn] <= wave_p_) continue;
+                const int R = p[sn] + nb[sn];
+                for (int r0 = 0; r0 < R; r0 += 64) n += std::min((r0 + 63) / w + 1, (p[sn] + w - 1) / w);
+            }
+            return n;
+        });
+        L.btw = pick([&](int w) {
+            long long n = 0;
+            for (int sn : l) {
+                const int R = p[sn] + nb[sn];
+                if (R <= wave_r_) continue;
+                for (int c0 = 0; c0 < p[sn]; c0 += 128) n += (R - c0 + w - 1) / w;
+            }
+            return n;
+        });
+        const int ftw = L.ftw, btw = L.btw;
+        // large supernodes: split-K forward tiles (64 rows x ftw columns; tiles entirely
         // above the diagonal of L_PP^-1 are zero and skipped), one reduction task per row block
         L.ft_first = (int)ftiles.size();
         L.fr_first = (int)freds.size();
         for (int sn : l) {
-            if (p[sn] <= kWaveP) continue;
+            if (p[sn] <= wave_p_) continue;
             const int R = p[sn] + nb[sn];
             for (int r0 = 0; r0 < R; r0 += 64) {
                 FRed rd{};
                 rd.beg = beg[sn]; rd.p = p[sn]; rd.r0 = r0; rd.nr = std::min(64, R - r0);
                 rd.uoff = uoff[sn]; rd.ell_off = ell_off[sn]; rd.ell_w = ell_w[sn]; rd.poff = poff;
-                rd.parent = F.parent[sn];
-                for (int c0 = 0; c0 < p[sn]; c0 += tile_w_) {
+                for (int c0 = 0; c0 < p[sn]; c0 += ftw) {
                     if (r0 + 63 < c0) break;
                     FTile ft{};
                     ft.beg = beg[sn]; ft.p = p[sn]; ft.R = R; ft.c0 = c0; ft.r0 = r0;
-                    ft.nc = std::min(tile_w_, p[sn] - c0);
+                    ft.nc = std::min(ftw, p[sn] - c0);
                     ft.goff = goff[sn]; ft.ell_off = ell_off[sn]; ft.ell_w = ell_w[sn]; ft.poff = poff;
-                    ft.node = sn;
                     ft.rid = (int)freds.size();
                     poff += 3 * 64;
                     ftiles.push_back(ft);
                     ++rd.nt;
                 }
                 freds.push_back(rd);
-                ++uf[sn];
             }
         }
         L.ft_count = (int)ftiles.size() - L.ft_first;
@@ -1148,41 +845,39 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         L.bwd_first = (int)tasks.size();
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
-            if (R <= kWaveR) {
-                for (int j0 = 0; j0 < p[sn]; j0 += L.bblock) { tasks.push_back(mk(sn, j0, std::min(L.bblock, p[sn] - j0))); ++ub[sn]; }
+            if (R <= wave_r_) {
+                for (int j0 = 0; j0 < p[sn]; j0 += L.bblock) tasks.push_back(mk(sn, j0, std::min(L.bblock, p[sn] - j0)));
                 L.lds_bwd = std::max(L.lds_bwd, 24 * R);
             }
         }
         L.bwd_count = (int)tasks.size() - L.bwd_first;
-        // large supernodes: split-K tiles (128 columns x tile_w_ rows; the tiles above the
+        // large supernodes: split-K tiles (128 columns x btw rows; the tiles above the
         // diagonal of L_PP^-1 are all zero and skipped) and one reduction task per column block
         L.bt_first = (int)btiles.size();
         L.br_first = (int)breds.size();
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
-            if (R <= kWaveR) continue;
+            if (R <= wave_r_) continue;
             for (int c0 = 0; c0 < p[sn]; c0 += 128) {
                 BRed rd{};
-                rd.beg = beg[sn]; rd.c0 = c0; rd.nc = std::min(128, p[sn] - c0); rd.poff = poff; rd.node = sn;
-                for (int r0 = c0; r0 < R; r0 += tile_w_) {
+                rd.beg = beg[sn]; rd.c0 = c0; rd.nc = std::min(128, p[sn] - c0); rd.poff = poff;
+                for (int r0 = c0; r0 < R; r0 += btw) {
                     BTile bt{};
                     bt.beg = beg[sn]; bt.p = p[sn]; bt.nb = nb[sn]; bt.bnd_off = bnd_off[sn];
-                    bt.c0 = c0; bt.r0 = r0; bt.nr = std::min(tile_w_, R - r0);
-                    bt.goff = goff[sn]; bt.poff = poff; bt.ldr = ldr[sn]; bt.parent = F.parent[sn];
+                    bt.c0 = c0; bt.r0 = r0; bt.nr = std::min(btw, R - r0);
+                    bt.goff = goff[sn]; bt.poff = poff; bt.ldr = ldr[sn];
                     bt.rid = (int)breds.size();
                     poff += 6 * 64;
                     btiles.push_back(bt);
                     ++rd.nt;
                 }
                 breds.push_back(rd);
-                ++ub[sn];
             }
         }
         L.bt_count = (int)btiles.size() - L.bt_first;
         L.br_count = (int)breds.size() - L.br_first;
         max_lds = std::max(max_lds, std::max(L.lds_fwd, L.lds_bwd));
-        kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.bt_count ? 1 : 0) +
-                    (L.ft_count ? 1 : 0);
+        kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.bt_count ? 1 : 0) + (L.ft_count ? 1 : 0);
         levels_.push_back(L);
         if (stats) {
             double by = 0;
@@ -1190,64 +885,15 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             for (int sn : l) {
                 by += 8.0 * (0.5 * p[sn] * (p[sn] + 1.0) + (double)p[sn] * nb[sn]);
                 maxp = std::max(maxp, p[sn]); maxnb = std::max(maxnb, nb[sn]);
-                nw += p[sn] > kWaveP;
+                nw += p[sn] > wave_p_;
             }
-            std::fprintf(stderr, "[solve] level %zu: %zu supernodes (%d wave), max p %d, max nb %d, %.2f MB/sweep, "
-                         "fwd tasks %d (blk %d) bwd tasks %d (blk %d) bwd tiles %d\n", levels_.size() - 1, l.size(), nw, maxp,
-                         maxnb, by / 1e6, L.fwd_count, L.fblock, L.bwd_count, L.bblock, L.bt_count);
+            std::fprintf(stderr, "[solve] level %zu: %zu supernodes (%d tiled), max p %d, max nb %d, %.2f MB/sweep, "
+                         "fwd tasks %d (blk %d) fwd tiles %d (w %d) bwd tasks %d (blk %d) bwd tiles %d (w %d)\n",
+                         levels_.size() - 1, l.size(), nw, maxp, maxnb, by / 1e6, L.fwd_count, L.fblock, L.ft_count, L.ftw,
+                         L.bwd_count, L.bblock, L.bt_count, L.btw);
         }
     }
     if (n_sub_) kernels_ += 2;
-    // ---- persistent sweeps: units per supernode (row tasks or row/column-block reductions),
-    // forward targets (the children's units) and backward targets (the node's own units)
-    {
-        std::vector<int> ftgt(nn_, 0), btgt(nn_, 0);
-        for (int sn = 0; sn < nn_; ++sn) {
-            btgt[sn] = ub[sn];
-            if (F.parent[sn] >= 0) ftgt[F.parent[sn]] += uf[sn];   // fused children have uf = 0
-        }
-        std::vector<PTask> fp, bp;
-        for (const auto& L : levels_) {
-            for (int i = 0; i < L.ft_count; ++i) fp.push_back({1, L.ft_first + i});
-            for (int i = 0; i < L.fwd_count; ++i) fp.push_back({0, L.fwd_first + i});
-        }
-        for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
-            for (int i = 0; i < it->bt_count; ++i) bp.push_back({1, it->bt_first + i});
-            for (int i = 0; i < it->bwd_count; ++i) bp.push_back({0, it->bwd_first + i});
-        }
-        n_fp_ = (int)fp.size();
-        n_bp_ = (int)bp.size();
-        fptasks_.upload(fp, s);
-        bptasks_.upload(bp, s);
-        ftgt_.upload(ftgt, s);
-        btgt_.upload(btgt, s);
-        sync_.alloc(((size_t)4 + 2 * nn_ + 3) / 4 * 4);   // heads + farr + bdone, whole 16-B multiple
-        sync_.zero(s);
-        err_.alloc(1);
-        err_.zero(s);
-        // measured slower than the level launches on every config so far:
-        // opt-in with AA_SOLVE_PERSIST=1
-        const char* pp = std::getenv("AA_SOLVE_PERSIST");
-        persist_ = pp && pp[0] == '1';
-        int dev = 0, cus = 0, a = 0, b = 0;
-        AA_HIP(hipGetDevice(&dev));
-        AA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        auto occ = [&](const void* k) { int o = 0; AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, kPB, 0)); return std::max(1, o); };
-        if (tile_w_ == 256) {
-            a = std::min(occ((const void*)k_fwd_persist<3, 256, false>), occ((const void*)k_bwd_persist<3, 256, false>));
-            b = std::min(occ((const void*)k_fwd_persist<6, 256, false>), occ((const void*)k_bwd_persist<6, 256, false>));
-        } else {
-            a = std::min(occ((const void*)k_fwd_persist<3, 128, false>), occ((const void*)k_bwd_persist<3, 128, false>));
-            b = std::min(occ((const void*)k_fwd_persist<6, 128, false>), occ((const void*)k_bwd_persist<6, 128, false>));
-        }
-        const char* pa = std::getenv("AA_SOLVE_PERSIST_ACQ");
-        persist_acq_ = pa && pa[0] == '1';
-        grid_p3_ = cus * a;
-        grid_p6_ = cus * b;
-        if (stats)
-            std::fprintf(stderr, "[solve] persistent sweeps: %d forward / %d backward tasks, grid %d (3 RHS) / %d (6 RHS)\n",
-                         n_fp_, n_bp_, grid_p3_, grid_p6_);
-    }
     bnd_.upload(bnd, s);
     ell_.upload(ell, s);
     Gr_.upload(Gr, s); Gc_.upload(Gc, s);
@@ -1297,32 +943,19 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
                             int gate_reject, hipStream_t s) {
     constexpr int K = NR / 3;
     const Task* T = tasks_.p;
-    if (persist_) AA_HIP(hipMemsetAsync(sync_.p, 0, sync_.n * sizeof(int), s));   // heads + arrival counters
 #define SUBF(BL) hipLaunchKernelGGL((k_fwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_f_, s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
     if (n_sub_) switch (sub_block_) { case 1024: SUBF(1024); break; case 512: SUBF(512); break; default: SUBF(256); break; }
 #undef SUBF
-    const int pgrid = NR == 6 ? grid_p6_ : grid_p3_;
-    if (persist_) {
-        if (n_fp_) {
-            auto kf = tile_w_ == 256 ? (persist_acq_ ? k_fwd_persist<NR, 256, true> : k_fwd_persist<NR, 256, false>)
-                                     : (persist_acq_ ? k_fwd_persist<NR, 128, true> : k_fwd_persist<NR, 128, false>);
-            hipLaunchKernelGGL(kf, dim3(std::min(pgrid, n_fp_)), dim3(kPB), 0, s, fptasks_.p, n_fp_, fhead(), farr(),
-                               ftgt_.p, T, ftiles_.p, freds_.p, fcnt_.p, Gc_.p, ell_.p, b0, b1, bpart_.p, Y_.p, U_.p,
-                               ctrl, gate_reject, err_.p);
-        }
-    } else {
-        for (auto& L : levels_) {
+    for (auto& L : levels_) {
 #define FWD(BL) hipLaunchKernelGGL((k_fwd<BL, NR>), dim3(L.fwd_count), dim3(BL), K * L.lds_fwd, s, T, L.fwd_first, Gc_.p, \
                                    ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
-            if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
+        if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
-            if (L.ft_count) {
-                auto kf = tile_w_ == 256 ? (tile_pf_ ? k_fwd_tile<NR, 16, 256> : k_fwd_tile<NR, 0, 256>)
-                                         : (tile_pf_ ? k_fwd_tile<NR, 16, 128> : k_fwd_tile<NR, 0, 128>);
-                hipLaunchKernelGGL(kf, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b0, b1,
-                                   bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
-            }
+        if (L.ft_count) {
+            auto kf = L.ftw == 256 ? k_fwd_tile<NR, 16, 256> : (L.ftw == 128 ? k_fwd_tile<NR, 16, 128> : k_fwd_tile<NR, 16, 64>);
+            hipLaunchKernelGGL(kf, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b0, b1,
+                               bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
         }
     }
     // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
@@ -1331,27 +964,16 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     // them and the backward sweep is gated alike on every GPU.
     if (comm_ && top_beg_ < n_)
         comm_->allreduce_sum(Y_.p + NR * (size_t)top_beg_, Y_.p + NR * (size_t)top_beg_, NR * (size_t)(n_ - top_beg_), s);
-    if (persist_) {
-        if (n_bp_) {
-            auto kb = tile_w_ == 256 ? (persist_acq_ ? k_bwd_persist<NR, 256, true> : k_bwd_persist<NR, 256, false>)
-                                     : (persist_acq_ ? k_bwd_persist<NR, 128, true> : k_bwd_persist<NR, 128, false>);
-            hipLaunchKernelGGL(kb, dim3(std::min(pgrid, n_bp_)), dim3(kPB), 0, s, bptasks_.p, n_bp_, bhead(), bdone(),
-                               btgt_.p, T, btiles_.p, breds_.p, bcnt_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, bpart_.p, ctrl,
-                               gate_reject, err_.p);
-        }
-    } else {
-        for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
-            const Level& L = *it;
+    for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
+        const Level& L = *it;
 #define BWD(BL) hipLaunchKernelGGL((k_bwd<BL, NR>), dim3(L.bwd_count), dim3(BL), K * L.lds_bwd, s, T, L.bwd_first, Gr_.p, \
                                    bnd_.p, Y_.p, x0, x1, ctrl, gate_reject)
-            if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
+        if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
-            if (L.bt_count) {
-                auto kb = tile_w_ == 256 ? (tile_pf_ ? k_bwd_tile<NR, 8, 256> : k_bwd_tile<NR, 0, 256>)
-                                         : (tile_pf_ ? k_bwd_tile<NR, 8, 128> : k_bwd_tile<NR, 0, 128>);
-                hipLaunchKernelGGL(kb, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p,
-                                   x0, x1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
-            }
+        if (L.bt_count) {
+            auto kb = L.btw == 256 ? k_bwd_tile<NR, 8, 256> : (L.btw == 128 ? k_bwd_tile<NR, 8, 128> : k_bwd_tile<NR, 8, 64>);
+            hipLaunchKernelGGL(kb, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p,
+                               x0, x1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
         }
     }
 #define SUBB(BL) hipLaunchKernelGGL((k_bwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_b_, s, sub_trees_.p, \
@@ -1360,15 +982,6 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }
 #undef SUBB
     AA_CHECK_LAUNCH();
-}
-
-int DirectSolver::take_error(hipStream_t s) {
-    if (!err_.p) return 0;
-    int e = 0;
-    AA_HIP(hipMemcpyAsync(&e, err_.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    AA_HIP(hipStreamSynchronize(s));
-    if (e) AA_HIP(hipMemsetAsync(err_.p, 0, sizeof(int), s));
-    return e;
 }
 
 }  // namespace aa

@@ -40,8 +40,11 @@ public:
     // max_sets = 2 sizes the workspaces and the fused subtrees' LDS budget for solve2().
     // wide: plan the layout (subtree cut, 256-wide split-K tiles) for two sets even when
     // max_sets = 1, so both solvers sum in the same order.
+    // wave_p / wave_r: supernodes with p above wave_p (forward) / R above wave_r (backward) are
+    // split-K tiled, the rest run as row tasks (defaults kWaveP / kWaveR; AA_SOLVE_WAVEP / _WAVER)
     void build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part = nullptr, int my_part = -1,
-               int top_beg = -1, Comm* comm = nullptr, int max_sets = 1, bool wide = false);
+               int top_beg = -1, Comm* comm = nullptr, int max_sets = 1, bool wide = false, int wave_p = kWaveP,
+               int wave_r = kWaveR);
     // x (n x 3, stride 3 doubles) = A^-1 b ; b is read only. gate: skip when ctrl->done (or !reject).
     void solve(const double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s);
     // x0 = A^-1 b0 and x1 = A^-1 b1 in one pass (needs build(..., max_sets = 2))
@@ -52,14 +55,12 @@ public:
     double bytes_per_solve() const { return bytes_; }
     double bytes_per_solve2() const { return bytes2_; }
     int kernels_per_solve() const { return kernels_; }
-    // 0, or nonzero after a persistent sweep gave up waiting on a dependency (never expected)
-    int take_error(hipStream_t s);
 
     // One workgroup's share of a level: rows [r0, r0 + nr) of supernode `node` (forward) or
     // its columns (backward), a thread per row. The supernode's metadata rides along so a
     // workgroup needs one (scalar) load before its first product.
     struct Task {
-        int node, r0, nr, parent;     // parent: the supernode's parent in the persistent set, or -1
+        int node, r0, nr, pad0;
         int p, nb, beg, bnd_off;
         int ell_w, ldr, pad1, pad2;   // ldr: row stride of the row-major G (p padded to even)
         long long goff, uoff, ell_off, pad3;
@@ -75,15 +76,12 @@ public:
     struct SubTree { int lvl0, nlvl; };
     // split-K backward of large supernodes: a tile (64 columns from c0, nr rows from r0) and the
     // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
-    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid, ldr, parent; long long goff, poff; };
-    struct BRed { int beg, c0, nc, nt, node, pad; long long poff; };
+    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid, ldr, pad; long long goff, poff; };
+    struct BRed { int beg, c0, nc, nt; long long poff; };
     // split-K forward of large supernodes: tile (64 rows from r0, nc columns from c0) and the
     // per-row-block reduction of its nt partials
-    struct FTile { int beg, p, R, c0, r0, nc, rid, ell_w, node, pad; long long goff, ell_off, poff; };
-    struct FRed { int beg, p, r0, nr, nt, ell_w, parent, pad; long long uoff, ell_off, poff; };
-    // persistent above-cut sweeps: one task = (kind, index) -- kind 0 a row task (tasks_), 1 a
-    // split-K tile (ftiles_ / btiles_) -- in dependency order (forward: leaves first)
-    struct PTask { int kind, idx; };
+    struct FTile { int beg, p, R, c0, r0, nc, rid, ell_w; long long goff, ell_off, poff; };
+    struct FRed { int beg, p, r0, nr, nt, ell_w; long long uoff, ell_off, poff; };
 
 private:
     struct Level {
@@ -91,6 +89,7 @@ private:
         int bt_first = 0, bt_count = 0, br_first = 0, br_count = 0;   // split-K backward tiles
         int ft_first = 0, ft_count = 0, fr_first = 0, frd_count = 0;  // split-K forward tiles
         int fblock = 256, bblock = 256, lds_fwd = 0, lds_bwd = 0;
+        int ftw = 256, btw = 256;   // split-K tile widths (forward columns / backward rows)
     };
     int n_ = 0, nn_ = 0, kernels_ = 0, top_beg_ = 0;
     Comm* comm_ = nullptr;
@@ -111,23 +110,9 @@ private:
     DevBuf<int> fcnt_, bcnt_;   // tiles finished per reduction task (reset by the last tile)
     DevBuf<double> bpart_;
     std::vector<Level> levels_;
-    // persistent sweeps above the subtree cut (AA_SOLVE_PERSIST=1; default: one launch per level).
-    // Forward: a task of supernode s waits until its children's units (row tasks / row-block
-    // reductions) have all arrived on farr[s] (target ftgt[s]); backward: until every unit of
-    // its parent has arrived on bdone[parent] (target btgt[parent]). Counters + dequeue heads
-    // live in sync_ (zeroed by a memset node before every solve); err_ flags a spin give-up.
-    bool persist_ = false, persist_acq_ = false;
-    int n_fp_ = 0, n_bp_ = 0, grid_p3_ = 0, grid_p6_ = 0;
-    DevBuf<PTask> fptasks_, bptasks_;
-    DevBuf<int> ftgt_, btgt_, sync_, err_;
-    int* fhead() const { return sync_.p; }
-    int* bhead() const { return sync_.p + 1; }
-    int* farr() const { return sync_.p + 4; }
-    int* bdone() const { return sync_.p + 4 + nn_; }
     // fused bottom subtrees
     int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1, sub_block_ = 256;
-    int tile_pf_ = 1;   // split-K tiles prefetch their first G rows/columns before staging (AA_TILE_PREFETCH)
-    int tile_w_ = 128;  // split-K tile width: forward columns / backward rows (128 or 256)
+    int wave_p_ = kWaveP, wave_r_ = kWaveR;   // row-task / split-K thresholds (AA_SOLVE_WAVEP / _WAVER)
     DevBuf<SubNode> sub_nodes_;
     DevBuf<SubLevel> sub_levels_;
     DevBuf<SubTree> sub_trees_;

@@ -774,8 +774,6 @@ void ElasticSolver::epilogue_enqueue(bool accel) {
 }
 
 void ElasticSolver::fetch_results() {
-    if (solver_.take_error(s()))
-        throw Error(ERR_DEVICE, "global solve: a persistent sweep gave up waiting on a dependency (spin bound)");
     Ctrl c;
     AA_HIP(hipMemcpyAsync(&c, ctrl_.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s()));
     AA_HIP(hipStreamSynchronize(s()));

@@ -236,21 +236,3 @@ def test_gpu_run_to_eps(builder, pkg, ctx):
         assert len(ta) == n and np.all(ta > 0) and np.all(np.diff(ta) > 0)
     a.close(); b.close()
 
-
-@pytest.mark.parametrize("builder", [
-    lambda: scenes.tet_drop(40, 16, 20, iters=8, n_steps=2),                       # Z + AA: 6-RHS and 3-RHS solves
-    lambda: scenes.cloth(48, 48, iters=20, n_steps=2),                             # UX
-    lambda: scenes.cantilever(24, 6, 6, scenes.NEOHOOKEAN, iters=10, n_steps=1),  # Z, narrow tiles
-])
-def test_gpu_persistent_solve_bit_identical(builder, pkg, ctx, monkeypatch):
-    """The persistent above-cut sweeps (one launch per sweep, dependency counters) compute every
-    column with the per-level kernels' sums in the same order: bit-identical to the per-level launches (the default)."""
-    sc = builder()
-    monkeypatch.setenv("AA_SOLVE_PERSIST", "0")
-    lv, _ = pkg.capi.run_scene(ctx, sc)
-    monkeypatch.setenv("AA_SOLVE_PERSIST", "1")
-    ps, _ = pkg.capi.run_scene(ctx, sc)
-    for a, b in zip(lv, ps):
-        for k in ("prim", "comb", "reject", "x", "v"):
-            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
-

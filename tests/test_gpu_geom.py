@@ -158,18 +158,3 @@ def test_gpu_geom_error_behaviour(pkg, ctx):
     assert e.value.code == -4
     g.close()
 
-
-@pytest.mark.parametrize("builder", [
-    lambda gs: gs.pq_heightfield(60, 60, iters=20, aa_m=10, noise=0.3),
-    lambda gs: gs.wire_grid(60, 60, iters=15, aa_m=20),
-])
-def test_gpu_geom_persistent_solve_bit_identical(builder, pkg, ctx, monkeypatch):
-    """Persistent above-cut sweeps (AA_SOLVE_PERSIST=1) vs one launch per tree level: bit-identical."""
-    sc = builder(pkg.geom_scenes)
-    monkeypatch.setenv("AA_SOLVE_PERSIST", "0")
-    a, ga = pkg.capi.run_geom(ctx, sc)
-    monkeypatch.setenv("AA_SOLVE_PERSIST", "1")
-    b, gb = pkg.capi.run_geom(ctx, sc)
-    assert np.array_equal(a["comb"], b["comb"]) and np.array_equal(a["x"], b["x"])
-    ga.close(); gb.close()
-
