@@ -194,7 +194,11 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     double v[D], x[D];
     double vol = 0;
     int e = -1, fail = 0;
-    bool active = false, exhausted = false;
+    // pending: the lane's element is solved but its outputs are not written yet -- they are
+    // written at the next refill, together with the loads of the lane's next element, so a
+    // wave pays the gathers' latency once per refill instead of on every trip in which some
+    // lane finishes
+    bool active = false, pending = false, exhausted = false;
     auto finalize = [&]() {
 #pragma unroll
         for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * g.count + e] = x[i];
@@ -207,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
         }
     };
     for (;;) {
-        const bool need = !active && !exhausted;
+        const bool need = !active && !exhausted;   // idle lanes, pending ones included
         const unsigned long long mask = __ballot(need);
         if (!__any(active || need)) break;
         // refill only once enough lanes are idle (the init path then runs for many lanes at once)
@@ -215,6 +219,10 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
             const int leader = __ffsll((long long)mask) - 1;
             int b = 0;
             if (lane == leader) b = atomicAdd(queue, __popcll(mask));
+            if (pending) {
+                finalize();
+                pending = false;
+            }
             b = __shfl(b, leader, 64);
             if (need) {
                 const int my = b + __popcll(mask & ((1ull << lane) - 1ull));
@@ -237,8 +245,8 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
             }
         }
         if (active && L.iterate(g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail)) {
-            finalize();
             active = false;
+            pending = true;
         }
     }
     if (fail && ctrl) ctrl->fail = 1;
