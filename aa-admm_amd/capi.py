@@ -25,7 +25,7 @@ EXPORTS = [
     "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
     "aa_elastic_get_times", "aa_elastic_set_iterations", "aa_elastic_set_x",
-    "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats",
+    "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats", "aa_elastic_local_stats",
     "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_destroy", "aa_comm_info",
     "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
     "aa_geom_create", "aa_geom_create_kind", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
@@ -300,6 +300,15 @@ class Solver:
         a, b, n = C.c_double(), C.c_double(), C.c_int()
         _chk(lib().aa_elastic_kernel_stats(self.h, name.encode(), C.byref(a), C.byref(b), C.byref(n)))
         return dict(avg_ms=a.value, bytes=b.value, launches=n.value)
+
+    def local_stats(self, reset=True):
+        """Work-queue diagnostics of the hyperelastic local step (AA_LQ_STATS=1 at initialize):
+        the per-element L-BFGS iteration histogram and the trip / refill / wave counts."""
+        out = np.zeros(104, np.int64)
+        n = C.c_int()
+        _chk(lib().aa_elastic_local_stats(self.h, out.ctypes.data_as(C.POINTER(C.c_longlong)), C.c_int(104),
+                                          C.c_int(1 if reset else 0), C.byref(n)))
+        return dict(hist=out[:101].copy(), trips=int(out[101]), refills=int(out[102]), waves=int(out[103]))
 
 
 def solver_from_scene(ctx: Context, scene, comm=None) -> Solver:

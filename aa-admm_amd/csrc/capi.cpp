@@ -272,6 +272,15 @@ int aa_elastic_kernel_stats(aa_elastic h, const char* name, double* avg_ms, doub
     });
 }
 
+int aa_elastic_local_stats(aa_elastic h, long long* out, int cap, int reset, int* count) {
+    return guarded([&] {
+        NEED(h && out && cap >= 0, "bad argument");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        const int n = h->s->local_stats(out, cap, reset != 0);
+        if (count) *count = n;
+    });
+}
+
 // ---- Geometry (ALMGeometrySolver<3>) -------------------------------------------------------
 int aa_geom_create(aa_ctx ctx, aa_geom* out) { return aa_geom_create_kind(ctx, AA_GEOM_ALM, out); }
 

@@ -4,6 +4,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -81,7 +82,12 @@ public:
         (void)hipFree(d);
         AA_HIP(e);
     }
-    bool capturable() const override { return false; }   // eager launches
+    // ncclAllReduce on the solver's stream is recorded into the step's hipGraph (a failed
+    // capture falls back to eager launches on every rank); AA_RCCL_NO_GRAPH=1 forces eager
+    bool capturable() const override {
+        const char* e = std::getenv("AA_RCCL_NO_GRAPH");
+        return !(e && e[0] == '1');
+    }
 
 private:
     ncclComm_t comm_ = nullptr;

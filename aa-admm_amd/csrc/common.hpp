@@ -60,6 +60,38 @@ struct DevBuf {
     size_t bytes() const { return n * sizeof(T); }
 };
 
+// Records what `enqueue` puts on stream s into an instantiated graph. Returns false -- with the
+// stream out of capture mode and nothing recorded kept -- when any part fails (e.g. a collective
+// the communication library cannot capture); the caller then launches eagerly.
+template <class F>
+bool capture_graph(hipStream_t s, F&& enqueue, hipGraph_t* graph, hipGraphExec_t* exec) {
+    *graph = nullptr;
+    *exec = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    bool ok = true;
+    try {
+        enqueue();
+    } catch (const Error&) {
+        ok = false;
+    }
+    hipGraph_t g = nullptr;
+    if (hipStreamEndCapture(s, &g) != hipSuccess) ok = false;
+    if (ok && hipGraphInstantiate(exec, g, nullptr, nullptr, 0) != hipSuccess) {
+        ok = false;
+        *exec = nullptr;
+    }
+    if (!ok) {
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        return false;
+    }
+    *graph = g;
+    return true;
+}
+
 constexpr int kBlock = 256;
 inline int blocks_for(long long n, int block = kBlock) { return (int)((n + block - 1) / block); }
 

@@ -409,6 +409,11 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     lzq_.alloc(1);
     if (const char* q = std::getenv("AA_LOCAL_QUEUE")) use_queue_ = q[0] != '0';
     lq_ = make_local_queue(ctx_->device, lzq_.p);
+    if (const char* q = std::getenv("AA_LQ_STATS"); q && q[0] == '1') {
+        lq_stats_.alloc(kLqStats);
+        lq_stats_.zero(s());
+        lq_.stats = lq_stats_.p;
+    }
     hist_cap_ = std::max(1, st_.admm_iters);
     hist_prim_.alloc(hist_cap_); hist_comb_.alloc(hist_cap_); hist_rej_.alloc(hist_cap_);
     hist_clock_.alloc(hist_cap_ + 1);
@@ -805,13 +810,16 @@ void ElasticSolver::step() {
     if (!initialized_) throw Error(ERR_STATE, "step() before initialize()");
     auto t0 = std::chrono::steady_clock::now();
     const bool accel = st_.acceleration_type == 1;
-    const bool graph = use_graph_ && st_.admm_iters > 0;
+    bool graph = use_graph_ && st_.admm_iters > 0;
     if (graph && !gexec_) {   // pointers and control flow are fixed after initialize: capture once,
         // before the prologue starts the step's device clock (capture is host work)
-        AA_HIP(hipStreamBeginCapture(s(), hipStreamCaptureModeThreadLocal));
-        enqueue_iterations(st_.admm_iters, accel);
-        AA_HIP(hipStreamEndCapture(s(), &graph_));
-        AA_HIP(hipGraphInstantiate(&gexec_, graph_, nullptr, nullptr, 0));
+        bool ok = capture_graph(s(), [&] { enqueue_iterations(st_.admm_iters, accel); }, &graph_, &gexec_);
+        if (comm_) {   // the ranks replay or launch eagerly together
+            double f = ok ? 0.0 : 1.0;
+            comm_->allreduce_sum_host(&f, 1);
+            if (f > 0 && ok) { drop_graph(); ok = false; }
+        }
+        if (!ok) use_graph_ = graph = false;
     }
     prologue();
     if (graph) {
@@ -926,6 +934,20 @@ bool ElasticSolver::kernel_stats(const std::string& name, double* avg_ms, double
     if (bytes) *bytes = k.bytes;
     if (launches) *launches = k.launches;
     return true;
+}
+
+int ElasticSolver::local_stats(long long* out, int cap, bool reset) {
+    const int n = std::min(cap, kLqStats);
+    if (!lq_stats_.p) {
+        for (int i = 0; i < n; ++i) out[i] = 0;
+        return n;
+    }
+    std::vector<unsigned long long> h(kLqStats);
+    AA_HIP(hipMemcpyAsync(h.data(), lq_stats_.p, kLqStats * sizeof(unsigned long long), hipMemcpyDeviceToHost, s()));
+    AA_HIP(hipStreamSynchronize(s()));
+    for (int i = 0; i < n; ++i) out[i] = (long long)h[i];
+    if (reset) lq_stats_.zero(s());
+    return n;
 }
 
 }  // namespace aa

@@ -49,6 +49,8 @@ public:
     // returns device-synchronised wall ms. Per-kernel-class event timings are collected.
     double bench_iterations(int iters);
     bool kernel_stats(const std::string& name, double* avg_ms, double* bytes, int* launches) const;
+    // the local-step work queue's diagnostics (kLqStats counters; 0 when not enabled); reset after
+    int local_stats(long long* out, int cap, bool reset);
 
 private:
     struct HostGroup {
@@ -94,6 +96,7 @@ private:
     int nbg_ = 0;
     DevBuf<Ctrl> ctrl_;
     DevBuf<int> lzq_;          // work-queue counter of the hyperelastic local step
+    DevBuf<unsigned long long> lq_stats_;   // its diagnostics (AA_LQ_STATS=1)
     LocalQueue lq_;
     bool use_queue_ = true;
     DevBuf<double> hist_prim_, hist_comb_;

@@ -186,8 +186,15 @@ template <int NV>
 __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double* __restrict__ xfull,
                                                        const double* __restrict__ u, double* __restrict__ z,
                                                        double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
-                                                       int* __restrict__ queue, int refill) {
+                                                       int* __restrict__ queue, int refill,
+                                                       unsigned long long* __restrict__ stats) {
     if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
+    unsigned trips = 0, refills = 0;
+    __shared__ unsigned hist[101];   // diagnostics only: per-block histogram, flushed at the end
+    if (stats) {
+        for (int i = threadIdx.x; i < 101; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+    }
     constexpr int D = 3 * (NV - 1);
     const int lane = threadIdx.x & 63;
     dev::HyperLbfgs L;
@@ -214,8 +221,10 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
         const bool need = !active && !exhausted;   // idle lanes, pending ones included
         const unsigned long long mask = __ballot(need);
         if (!__any(active || need)) break;
+        ++trips;
         // refill only once enough lanes are idle (the init path then runs for many lanes at once)
         if (mask && (__popcll(mask) >= refill || !__any(active))) {
+            ++refills;
             const int leader = __ffsll((long long)mask) - 1;
             int b = 0;
             if (lane == leader) b = atomicAdd(queue, __popcll(mask));
@@ -239,15 +248,30 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
                         x[i] = v[i];
                     }
                     vol = g.vol[e];
-                    if (L.start(g.mat, g.mu, g.lambda, g.k, vol, v, x)) finalize();
-                    else active = true;
+                    if (L.start(g.mat, g.mu, g.lambda, g.k, vol, v, x)) {
+                        finalize();
+                        if (stats) atomicAdd(&hist[0], 1u);
+                    } else {
+                        active = true;
+                    }
                 }
             }
         }
         if (active && L.iterate(g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail)) {
             active = false;
             pending = true;
+            if (stats) atomicAdd(&hist[min(L.k_it, 100)], 1u);
         }
+    }
+    if (stats) {
+        if (lane == 0) {
+            atomicAdd(stats + 101, (unsigned long long)trips);
+            atomicAdd(stats + 102, (unsigned long long)refills);
+            atomicAdd(stats + 103, 1ull);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 101; i += blockDim.x)
+            if (hist[i]) atomicAdd(stats + i, (unsigned long long)hist[i]);
     }
     if (fail && ctrl) ctrl->fail = 1;
 }
@@ -980,7 +1004,7 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
         AA_HIP(hipMemsetAsync(queue->counter, 0, sizeof(int), s));
         const int resident = std::max(1, queue->resident), refill = queue->refill;
         hipLaunchKernelGGL(k_local_z_hq<4>, dim3(std::min(nb, resident)), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
-                           ctrl, queue->counter, refill);
+                           ctrl, queue->counter, refill, queue->stats);
         AA_CHECK_LAUNCH();
         return;
     }

@@ -756,19 +756,22 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
     prologue(init_x3, max_iter, m, max_iter);
     const int target = std::max(1, max_iter);
     const int chunk = std::min(target, 64);
-    const bool use_graph = !(std::getenv("AA_ADMM_NO_GRAPH") && std::getenv("AA_ADMM_NO_GRAPH")[0] == '1') &&
-                           !(comm_ && !comm_->capturable());
+    bool use_graph = !(std::getenv("AA_ADMM_NO_GRAPH") && std::getenv("AA_ADMM_NO_GRAPH")[0] == '1') &&
+                     !(comm_ && !comm_->capturable());
     auto run_chunk = [&]() {
-        if (use_graph) {
-            if (!gexec_ || graph_chunk_ != chunk || graph_m_ != m) {
-                drop_graph();
-                AA_HIP(hipStreamBeginCapture(s(), hipStreamCaptureModeThreadLocal));
-                for (int i = 0; i < chunk; ++i) enqueue_iteration(m);
-                AA_HIP(hipStreamEndCapture(s(), &graph_));
-                AA_HIP(hipGraphInstantiate(&gexec_, graph_, nullptr, nullptr, 0));
-                graph_chunk_ = chunk;
-                graph_m_ = m;
+        if (use_graph && (!gexec_ || graph_chunk_ != chunk || graph_m_ != m)) {
+            drop_graph();
+            bool ok = capture_graph(s(), [&] { for (int i = 0; i < chunk; ++i) enqueue_iteration(m); }, &graph_, &gexec_);
+            if (comm_) {   // the ranks replay or launch eagerly together
+                double f = ok ? 0.0 : 1.0;
+                comm_->allreduce_sum_host(&f, 1);
+                if (f > 0 && ok) { drop_graph(); ok = false; }
             }
+            use_graph = ok;
+            graph_chunk_ = chunk;
+            graph_m_ = m;
+        }
+        if (use_graph) {
             AA_HIP(hipGraphLaunch(gexec_, s()));
         } else {
             for (int i = 0; i < chunk; ++i) enqueue_iteration(m);

@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--eps-cap", type=int, default=500)
     p.add_argument("--no-secondary", action="store_true",
                    help="c4 only: skip the secondary C3 (planar-quad, configs[2]) object in the same JSON line")
+    p.add_argument("--lq-stats", action="store_true",
+                   help="c4: count the local step's L-BFGS iterations per element and its work-queue trips over "
+                        "the timed steps (AA_LQ_STATS=1; atomics in the kernel, so not for the timed number)")
     return p.parse_args()
 
 
@@ -440,6 +443,8 @@ def main():
     sc, desc = elastic_scene(args)
     comm, part = make_comm(pkg, ctx, args, world, rank)
     solver = capi.solver_from_scene(ctx, sc, comm)
+    if args.lq_stats:
+        os.environ["AA_LQ_STATS"] = "1"
     t0 = time.time()
     solver.initialize(capi.settings_from_scene(sc))
     setup_ms = (time.time() - t0) * 1e3
@@ -449,6 +454,8 @@ def main():
     # the timed steps (and the run-to-epsilon leg) replay the drop from its initial state
     x0, v0 = np.asarray(sc.x, np.float64).reshape(-1, 3), np.zeros((sc.n_nodes, 3))
     solver.set_state(x0, v0)
+    if args.lq_stats:
+        solver.local_stats(reset=True)
 
     barrier(dist, ctx)
     t0 = time.perf_counter()
@@ -466,6 +473,15 @@ def main():
     iters_all = float(iters_run) if comm is not None else allreduce(dist, float(iters_run), _sum_op(dist))
     value = iters_all / elapsed_max
 
+    lq = None
+    if args.lq_stats:
+        st = solver.local_stats(reset=True)
+        h = st["hist"]
+        its = float((h * np.arange(len(h))).sum())
+        lq = {"elements": int(h.sum()), "mean_lbfgs_iters": round(its / max(1, h.sum()), 3),
+              "hist": {str(i): int(c) for i, c in enumerate(h) if c},
+              "trips": st["trips"], "refills": st["refills"], "waves": st["waves"],
+              "lane_busy_frac": round(its / max(1, 64 * st["trips"]), 4)}
     # roofline of the dominant kernel class, timed live with HIP events on the solver's stream
     # (separate instrumented pass of the same iteration loop, after the timed region; every
     # rank of a partitioned run takes part -- the loop has collectives)
@@ -557,6 +573,8 @@ def main():
         }
         if comm is not None:
             line["config"]["partition"] = {"elements_rank0": rt.n_elements, "z_dim_rank0": rt.z_dim}
+        if lq is not None:
+            line["local_step_queue"] = lq
         if secondary is not None:
             line["secondary"] = secondary
         print(json.dumps(line))

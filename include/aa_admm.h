@@ -143,6 +143,13 @@ int aa_elastic_bench_iterations(aa_elastic h, int iters, double* ms);
 /* Average device time (ms) per launch of the named kernel class over the last bench call,
  * measured with HIP events on the solver's stream; and its algorithmic bytes per launch. */
 int aa_elastic_kernel_stats(aa_elastic h, const char* name, double* avg_ms, double* bytes, int* launches);
+/* Diagnostics of the hyperelastic local step's work queue, summed over its launches since the
+ * last reset (enabled by AA_LQ_STATS=1 in the environment at aa_elastic_initialize; zeros
+ * otherwise): out[0..100] elements by L-BFGS iteration count (mcloptlib LBFGS.hpp:205-305 outer
+ * iterations; 0 = the start point passed the gradient test), out[101] trips (one L-BFGS
+ * iteration for every busy lane of a wave), out[102] queue refills, out[103] waves. Writes
+ * min(cap, 104) counters into *count. */
+int aa_elastic_local_stats(aa_elastic h, long long* out, int cap, int reset, int* count);
 
 /* ==== Geometry: ALMGeometrySolver<3> + Constraint<3> (bldeng/AA-ADMM Geometry/) ============= */
 typedef struct aa_geom_s* aa_geom;        /* one ALMGeometrySolver<3> instance             */
