@@ -4,10 +4,11 @@
 
 Counters are summed over every dispatch of a kernel (the short name k_...<...>), together with
 the dispatches' wall time (End - Start). Derived per kernel:
-  fp64_tflops    = SQ_INSTS_VALU_FLOPS_FP64 (+ _TRANS) / wall       (FMA counts 2)
-  valu_issue     = 4 * SQ_ACTIVE_INST_VALU / (4 * SQ_WAVE_CYCLES)    share of wave time issuing VALU
-  lane_util      = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU * 4)   active lanes per VALU cycle
-  busy_frac      = SQ_ACTIVE_INST_VALU * 4 / (SQ_BUSY_CYCLES * SIMDs per SE) VALU pipes busy while the SE is
+  fp64_tflops    = 64 * SQ_INSTS_VALU_FLOPS_FP64 (+ _TRANS) / wall   (the counter counts the FLOPs of one
+                   lane per wave instruction, FMA = 2: x 64 lanes = an upper bound, all lanes busy)
+  valu_issue     = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES              share of wave time issuing VALU
+  lane_util      = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)  active lanes per VALU cycle
+                   (1.000 on a kernel without divergence, k_u_and_y)
 The fp64 vector peak of MI355X: 256 CUs x 4 SIMDs x 16 fp64 FMA lanes/clk x 2 FLOP x 2.4 GHz
 = 78.6 TFLOP/s (half the f32 vector rate, 157.3 TF in MI355X_MICROARCH.md).
 """
@@ -52,7 +53,7 @@ def main():
     for k, c in acc.items():
         w = wall[k].get(paths[0], 0.0)
         n = int(wall[k].get("n:" + paths[0], 0))
-        flops = c.get("SQ_INSTS_VALU_FLOPS_FP64", 0) + c.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0)
+        flops = 64 * (c.get("SQ_INSTS_VALU_FLOPS_FP64", 0) + c.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0))
         wc = c.get("SQ_WAVE_CYCLES", 0)
         av = c.get("SQ_ACTIVE_INST_VALU", 0)
         row = {
@@ -63,7 +64,7 @@ def main():
             "frac_fp64_peak": flops / w / 1e12 / PEAK_FP64_TF if w else 0,
             "valu_insts_per_dispatch": c.get("SQ_INSTS_VALU", 0) / n if n else 0,
             "valu_issue_frac_of_wave_cycles": av / wc if wc else 0,
-            "lane_util": c.get("SQ_THREAD_CYCLES_VALU", 0) / (64 * 4 * av) if av else 0,
+            "lane_util": c.get("SQ_THREAD_CYCLES_VALU", 0) / (64 * av) if av else 0,
         }
         for extra in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
                       "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD"):
