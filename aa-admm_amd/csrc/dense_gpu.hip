@@ -1,0 +1,215 @@
+// Dense front assembly + partial factorization on the GPU (see spd_direct.hpp DenseFrontBackend):
+// the large fronts near the root of the nested-dissection tree, which hold most of the factor's
+// flops (C4: ~240 of 247 GFLOP in fronts of order >= 1024), are assembled and factored with
+// rocSOLVER / rocBLAS on the solver's stream instead of the host's right-looking loop.
+//   assembly   scatter-add of A's pivot columns, then of each child's update matrix (child order,
+//              one launch each: every front entry receives its terms in the host loop's order)
+//   factor     dpotrf (L11), dtrsm (L21 = F21 L11^-T), dsyrk (F22 -= L21 L21^T)
+//   outputs    dtrtri (Linv = L11^-1), dtrmm (M = L21 Linv), transposed to the host's row-major
+//              layouts on the device; F22 stays on the device when the parent is factored here
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+#include "common.hpp"
+#include "dense_gpu.hpp"
+
+namespace aa {
+
+namespace {
+
+void rb_check(rocblas_status st, const char* what) {
+    if (st != rocblas_status_success) throw Error(ERR_DEVICE, std::string(what) + ": " + rocblas_status_to_string(st));
+}
+
+// F(i, j) += v for the COO entries (distinct entries: no conflicts)
+__global__ void k_scatter_coo(double* __restrict__ F, int f, const int* __restrict__ ri, const int* __restrict__ cj,
+                              const double* __restrict__ v, int n) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) F[(size_t)cj[k] * f + ri[k]] += v[k];
+}
+
+// extend-add of one child's update matrix (lower triangle, m x m; row-major a*m+b or column-major
+// b*m+a) into the front: entry (a, b), b <= a, lands on F(max(ra, rb), min(ra, rb)). Distinct
+// (a, b) land on distinct entries (map is injective), so one launch per child has no conflicts.
+__global__ void k_extend_add(double* __restrict__ F, int f, const double* __restrict__ U, int m, int rowmajor,
+                             const int* __restrict__ map) {
+    const int a = blockIdx.y * blockDim.y + threadIdx.y;
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= m || b > a) return;
+    int ra = map[a], rb = map[b];
+    if (ra < rb) { const int t = ra; ra = rb; rb = t; }
+    F[(size_t)rb * f + ra] += rowmajor ? U[(size_t)a * m + b] : U[(size_t)b * m + a];
+}
+
+// dst (rows x cols, row-major) = src (column-major, leading dimension ld); lower = true keeps
+// only entries with column <= row (zero elsewhere). 32 x 32 tiles through LDS.
+__global__ void k_to_rowmajor(double* __restrict__ dst, const double* __restrict__ src, int ld, int rows, int cols,
+                              int lower) {
+    __shared__ double t[32][33];
+    const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+    for (int q = threadIdx.y; q < 32; q += blockDim.y) {   // read: consecutive threads, consecutive rows
+        const int c = c0 + q, r = r0 + threadIdx.x;
+        if (r < rows && c < cols) t[q][threadIdx.x] = src[(size_t)c * ld + r];
+    }
+    __syncthreads();
+    for (int q = threadIdx.y; q < 32; q += blockDim.y) {   // write: consecutive threads, consecutive columns
+        const int r = r0 + q, c = c0 + threadIdx.x;
+        if (r < rows && c < cols) dst[(size_t)r * cols + c] = (lower && c > r) ? 0.0 : t[threadIdx.x][q];
+    }
+}
+
+template <class T>
+struct Grow {   // device buffer that only grows
+    DevBuf<T> b;
+    T* get(size_t n) {
+        if (b.n < n) b.alloc(n);
+        return b.p;
+    }
+};
+
+class RocFrontBackend final : public DenseFrontBackend {
+public:
+    explicit RocFrontBackend(hipStream_t s) : s_(s) {
+        rb_check(rocblas_create_handle(&h_), "rocblas_create_handle");
+        rb_check(rocblas_set_stream(h_, s_), "rocblas_set_stream");
+        info_.alloc(2);
+    }
+    ~RocFrontBackend() override {
+        if (h_) (void)rocblas_destroy_handle(h_);
+    }
+    bool holds(int s) const override {
+        std::lock_guard<std::mutex> g(mu_);
+        return held_.count(s) > 0;
+    }
+    void factor(int s, int f, int p, const std::vector<int>& ai, const std::vector<int>& aj, const std::vector<double>& av,
+                const std::vector<Child>& kids, bool keep_update, std::vector<double>& Linv, std::vector<double>& LBP,
+                std::vector<double>& M, std::vector<double>* U) override {
+        std::lock_guard<std::mutex> g(mu_);
+        const int nb = f - p;
+        double* F = F_.get((size_t)f * f);
+        AA_HIP(hipMemsetAsync(F, 0, (size_t)f * f * sizeof(double), s_));
+        // ---- assembly
+        const int na = (int)ai.size();
+        if (na > 0) {
+            int* di = ii_.get(2 * (size_t)na);
+            double* dv = dv_.get(na);
+            AA_HIP(hipMemcpyAsync(di, ai.data(), na * sizeof(int), hipMemcpyHostToDevice, s_));
+            AA_HIP(hipMemcpyAsync(di + na, aj.data(), na * sizeof(int), hipMemcpyHostToDevice, s_));
+            AA_HIP(hipMemcpyAsync(dv, av.data(), na * sizeof(double), hipMemcpyHostToDevice, s_));
+            hipLaunchKernelGGL(k_scatter_coo, dim3(blocks_for(na)), dim3(kBlock), 0, s_, F, f, di, di + na, dv, na);
+            AA_CHECK_LAUNCH();
+            AA_HIP(hipStreamSynchronize(s_));   // the host vectors are the caller's
+        }
+        for (const Child& c : kids) {
+            if (c.m == 0) continue;
+            int* dmap = map_.get(c.m);
+            AA_HIP(hipMemcpyAsync(dmap, c.map, c.m * sizeof(int), hipMemcpyHostToDevice, s_));
+            const double* Usrc;
+            int rowmajor;
+            std::unique_ptr<DevBuf<double>> own;
+            if (c.U) {
+                double* du = up_.get((size_t)c.m * c.m);
+                AA_HIP(hipMemcpyAsync(du, c.U->data(), (size_t)c.m * c.m * sizeof(double), hipMemcpyHostToDevice, s_));
+                Usrc = du;
+                rowmajor = 1;
+            } else {
+                auto it = held_.find(c.id);
+                if (it == held_.end()) throw Error(ERR_STATE, "dense front backend: missing update matrix");
+                own = std::move(it->second);
+                held_.erase(it);
+                Usrc = own->p;
+                rowmajor = 0;
+            }
+            const dim3 blk(32, 8), grd((c.m + 31) / 32, (c.m + 7) / 8);
+            hipLaunchKernelGGL(k_extend_add, grd, blk, 0, s_, F, f, Usrc, c.m, rowmajor, dmap);
+            AA_CHECK_LAUNCH();
+            AA_HIP(hipStreamSynchronize(s_));   // before the staging buffers / held matrix are reused
+        }
+        // ---- partial factorization
+        const double one = 1.0, mone = -1.0;
+        rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
+        if (nb > 0) {
+            rb_check(rocblas_dtrsm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                                   rocblas_diagonal_non_unit, nb, p, &one, F, f, F + p, f), "rocblas_dtrsm");
+            rb_check(rocblas_dsyrk(h_, rocblas_fill_lower, rocblas_operation_none, nb, p, &mone, F + p, f, &one,
+                                   F + (size_t)p * f + p, f), "rocblas_dsyrk");
+        }
+        double* L = L_.get((size_t)p * p);
+        AA_HIP(hipMemcpy2DAsync(L, p * sizeof(double), F, f * sizeof(double), p * sizeof(double), p,
+                                hipMemcpyDeviceToDevice, s_));
+        rb_check(rocsolver_dtrtri(h_, rocblas_fill_lower, rocblas_diagonal_non_unit, p, L, p, info_.p + 1),
+                 "rocsolver_dtrtri");
+        double* Md = nullptr;
+        if (nb > 0) {
+            Md = M_.get((size_t)nb * p);
+            rb_check(rocblas_dtrmm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_none,
+                                   rocblas_diagonal_non_unit, nb, p, &one, L, p, F + p, f, Md, nb), "rocblas_dtrmm");
+        }
+        int info[2] = {0, 0};
+        AA_HIP(hipMemcpyAsync(info, info_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s_));
+        AA_HIP(hipStreamSynchronize(s_));
+        if (info[0] != 0) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite");
+        if (info[1] != 0) throw std::runtime_error("multifrontal_cholesky: singular diagonal block");
+        // ---- outputs in the host layouts
+        auto fetch = [&](std::vector<double>& out, const double* src, int ld, int rows, int cols, int lower) {
+            out.resize((size_t)rows * cols);
+            if (out.empty()) return;
+            double* t = T_.get(out.size());
+            const dim3 blk(32, 8), grd((cols + 31) / 32, (rows + 31) / 32);
+            hipLaunchKernelGGL(k_to_rowmajor, grd, blk, 0, s_, t, src, ld, rows, cols, lower);
+            AA_CHECK_LAUNCH();
+            AA_HIP(hipMemcpyAsync(out.data(), t, out.size() * sizeof(double), hipMemcpyDeviceToHost, s_));
+            AA_HIP(hipStreamSynchronize(s_));
+        };
+        fetch(Linv, L, p, p, p, 1);
+        fetch(LBP, F + p, f, nb, p, 0);
+        if (nb > 0) fetch(M, Md, nb, nb, p, 0);
+        else M.clear();
+        if (nb > 0) {
+            if (keep_update) {   // column-major nb x nb, for the parent's extend-add
+                auto u = std::make_unique<DevBuf<double>>((size_t)nb * nb);
+                AA_HIP(hipMemcpy2DAsync(u->p, nb * sizeof(double), F + (size_t)p * f + p, f * sizeof(double),
+                                        nb * sizeof(double), nb, hipMemcpyDeviceToDevice, s_));
+                AA_HIP(hipStreamSynchronize(s_));
+                held_[s] = std::move(u);
+            } else {
+                fetch(*U, F + (size_t)p * f + p, f, nb, nb, 1);
+            }
+        }
+    }
+
+private:
+    hipStream_t s_;
+    rocblas_handle h_ = nullptr;
+    mutable std::mutex mu_;
+    std::map<int, std::unique_ptr<DevBuf<double>>> held_;
+    DevBuf<int> info_;
+    Grow<double> F_, L_, M_, T_, dv_, up_;
+    Grow<int> ii_, map_;
+};
+
+}  // namespace
+
+std::unique_ptr<DenseFrontBackend> make_gpu_front_backend(hipStream_t s) {
+    auto b = std::unique_ptr<DenseFrontBackend>(new RocFrontBackend(s));
+    if (const char* e = std::getenv("AA_DENSE_MIN_FRONT")) b->min_front = std::max(1, std::atoi(e));
+    return b;
+}
+
+SupernodalFactor factor_on_device(const CsrMatrix& A, const NdTree& tree, hipStream_t s) {
+    const char* e = std::getenv("AA_DENSE_GPU");
+    if (e && e[0] == '0') return multifrontal_cholesky(A, tree, nullptr);
+    auto b = make_gpu_front_backend(s);
+    return multifrontal_cholesky(A, tree, b.get());
+}
+
+}  // namespace aa

@@ -548,8 +548,13 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             for (int c = ps; c < ld; ++c) gr[(size_t)r * ld + c] = 0.0;   // pad column
         for (int r = 0; r < ps; ++r)
             for (int c = 0; c < ps; ++c) gr[(size_t)r * ld + c] = c <= r ? Li[(size_t)r * ps + c] : 0.0;
+        const bool have_m = F.M.size() == (size_t)nn_ && F.M[sn].size() == (size_t)nbs * ps;
         for (int a = 0; a < nbs; ++a) {
             double* m = gr + (size_t)(ps + a) * ld;
+            if (have_m) {   // formed with the factor (dense backend)
+                std::copy(F.M[sn].begin() + (size_t)a * ps, F.M[sn].begin() + (size_t)(a + 1) * ps, m);
+                continue;
+            }
             for (int c = 0; c < ps; ++c) m[c] = 0.0;
             for (int k = 0; k < ps; ++k) {
                 const double l = LB[(size_t)a * ps + k];

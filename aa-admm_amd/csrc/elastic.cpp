@@ -16,6 +16,7 @@
 #include <numeric>
 #include <set>
 
+#include "dense_gpu.hpp"
 #include "spd_direct.hpp"
 
 namespace aa {
@@ -267,7 +268,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     }
     SupernodalFactor F;
     try {
-        F = multifrontal_cholesky(A, tree);
+        F = factor_on_device(A, tree, s());
     } catch (const std::runtime_error& e) {
         throw Error(ERR_NUMERIC, e.what());
     }

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <numeric>
 
+#include "dense_gpu.hpp"
 #include "spd_direct.hpp"
 
 namespace aa {
@@ -391,7 +392,7 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     }
     SupernodalFactor F;
     try {
-        F = multifrontal_cholesky(A, tree);
+        F = factor_on_device(A, tree, s());
     } catch (const std::runtime_error& e) {
         throw Error(ERR_NUMERIC, std::string("Error: SPD solver initialization failed: ") + e.what());
     }

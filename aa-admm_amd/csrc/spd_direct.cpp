@@ -215,17 +215,13 @@ NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_p
 }
 
 // ------------------------------------------------------------------ multifrontal Cholesky
-SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree) {
-    SupernodalFactor F;
-    const int n = A.n, nn = (int)tree.beg.size();
-    F.n = n; F.n_nodes = nn;
-    F.beg = tree.beg; F.end = tree.end; F.parent = tree.parent;
-    F.bnd.resize(nn); F.Linv.resize(nn); F.LBP.resize(nn); F.height.assign(nn, 0);
-    std::vector<std::vector<double>> U(nn);   // update matrices, freed when consumed
-    std::vector<int> pos(n, -1);
+namespace {
+
+// symbolic: boundary rows of every supernode (postorder: from A's columns and the children's)
+void symbolic(const CsrMatrix& A, const NdTree& tree, SupernodalFactor& F) {
+    const int nn = (int)tree.beg.size();
     for (int s = 0; s < nn; ++s) {
-        const int b0 = tree.beg[s], e0 = tree.end[s], p = e0 - b0;
-        // ---- symbolic: boundary rows
+        const int b0 = tree.beg[s], e0 = tree.end[s];
         std::vector<int> bnd;
         for (int j = b0; j < e0; ++j)
             for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) if (A.col[k] >= e0) bnd.push_back(A.col[k]);
@@ -235,77 +231,193 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree) {
         }
         std::sort(bnd.begin(), bnd.end());
         bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
-        const int nb = (int)bnd.size(), f = p + nb;
-        for (int j = b0; j < e0; ++j) pos[j] = j - b0;
-        for (int k = 0; k < nb; ++k) pos[bnd[k]] = p + k;
-        // ---- assemble front (lower triangle, column-major f x f: Fc(i,j) at j*f + i)
-        std::vector<double> Fc((size_t)f * f, 0.0);
-        auto FC = [&](int i, int j) -> double& { return Fc[(size_t)j * f + i]; };
+        F.bnd[s] = std::move(bnd);
+    }
+}
+
+struct FrontCtx {
+    const CsrMatrix& A;
+    const NdTree& tree;
+    SupernodalFactor& F;
+    std::vector<std::vector<double>>& U;   // host update matrices, freed when consumed
+    std::vector<double>& flops;
+    DenseFrontBackend* dense;
+};
+
+int front_order(const SupernodalFactor& F, int s) { return F.end[s] - F.beg[s] + (int)F.bnd[s].size(); }
+
+// numeric work of supernode s: assemble the front (A's pivot columns, then the children's update
+// matrices in child order), partial Cholesky of its first p columns, outputs. pos: n-sized scratch
+// (every entry read is written first). Fronts of order >= dense->min_front go to the backend.
+void factor_front(FrontCtx& C, int s, std::vector<int>& pos, bool inner_parallel) {
+    const CsrMatrix& A = C.A;
+    const NdTree& tree = C.tree;
+    SupernodalFactor& F = C.F;
+    const int b0 = tree.beg[s], e0 = tree.end[s], p = e0 - b0;
+    const std::vector<int>& bnd = F.bnd[s];
+    const int nb = (int)bnd.size(), f = p + nb;
+    for (int j = b0; j < e0; ++j) pos[j] = j - b0;
+    for (int k = 0; k < nb; ++k) pos[bnd[k]] = p + k;
+    double fl = 0;
+    for (int k = 0; k < p; ++k) fl += (double)(f - k) * (f - k);
+    C.flops[s] = fl;
+    if (C.dense && f >= C.dense->min_front) {
+        std::vector<int> ai, aj;
+        std::vector<double> av;
         for (int j = b0; j < e0; ++j)
             for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) {
-                int i = A.col[k];
+                const int i = A.col[k];
                 if (i < j) continue;
-                FC(pos[i], pos[j]) += A.val[k];
+                ai.push_back(pos[i]); aj.push_back(pos[j]); av.push_back(A.val[k]);
             }
-        for (int c : tree.children[s]) {
-            const std::vector<int>& cb = F.bnd[c];
-            const int m = (int)cb.size();
-            const std::vector<double>& Uc = U[c];
-            for (int a = 0; a < m; ++a)
-                for (int bb = 0; bb <= a; ++bb) {
-                    int ra = pos[cb[a]], rb = pos[cb[bb]];
-                    if (ra < rb) std::swap(ra, rb);
-                    FC(ra, rb) += Uc[(size_t)a * m + bb];
-                }
-            std::vector<double>().swap(U[c]);
+        std::vector<DenseFrontBackend::Child> kids;
+        std::vector<std::vector<int>> maps(tree.children[s].size());
+        for (size_t q = 0; q < tree.children[s].size(); ++q) {
+            const int c = tree.children[s][q];
+            for (int i : F.bnd[c]) maps[q].push_back(pos[i]);
+            kids.push_back({c, maps[q].data(), (int)maps[q].size(), C.dense->holds(c) ? nullptr : &C.U[c]});
         }
-        // ---- partial dense Cholesky (right-looking, column-major) of the first p columns
-        for (int k = 0; k < p; ++k) {
-            double* ck = &Fc[(size_t)k * f];
-            const double d = ck[k];
-            if (!(d > 0.0)) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite");
-            const double dk = std::sqrt(d);
-            ck[k] = dk;
-            const double inv = 1.0 / dk;
-            for (int i = k + 1; i < f; ++i) ck[i] *= inv;
-            const long long work = (long long)(f - k) * (f - k);
-            (void)work;   // (only read by the OpenMP if-clause on the host pass)
-#pragma omp parallel for schedule(dynamic, 16) if (work > 200000)
-            for (int j = k + 1; j < f; ++j) {
-                const double ljk = ck[j];
-                if (ljk == 0.0) continue;
-                double* cj = &Fc[(size_t)j * f];
-                for (int i = j; i < f; ++i) cj[i] -= ck[i] * ljk;
+        const int par = tree.parent[s];
+        const bool keep = par >= 0 && front_order(F, par) >= C.dense->min_front;
+        std::vector<double> Us;
+        C.dense->factor(s, f, p, ai, aj, av, kids, keep, F.Linv[s], F.LBP[s], F.M[s], keep ? nullptr : &Us);
+        for (int c : tree.children[s]) std::vector<double>().swap(C.U[c]);
+        if (nb > 0 && !keep) C.U[s] = std::move(Us);
+        return;
+    }
+    // ---- assemble front (lower triangle, column-major f x f: Fc(i,j) at j*f + i)
+    std::vector<double> Fc((size_t)f * f, 0.0);
+    auto FC = [&](int i, int j) -> double& { return Fc[(size_t)j * f + i]; };
+    for (int j = b0; j < e0; ++j)
+        for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) {
+            int i = A.col[k];
+            if (i < j) continue;
+            FC(pos[i], pos[j]) += A.val[k];
+        }
+    for (int c : tree.children[s]) {
+        const std::vector<int>& cb = F.bnd[c];
+        const int m = (int)cb.size();
+        if (C.dense && C.dense->holds(c)) throw std::runtime_error("multifrontal_cholesky: update matrix held by the backend");
+        const std::vector<double>& Uc = C.U[c];
+        for (int a = 0; a < m; ++a)
+            for (int bb = 0; bb <= a; ++bb) {
+                int ra = pos[cb[a]], rb = pos[cb[bb]];
+                if (ra < rb) std::swap(ra, rb);
+                FC(ra, rb) += Uc[(size_t)a * m + bb];
             }
-            F.flops += (double)(f - k) * (f - k);
+        std::vector<double>().swap(C.U[c]);
+    }
+    // ---- partial dense Cholesky (right-looking, column-major) of the first p columns
+    for (int k = 0; k < p; ++k) {
+        double* ck = &Fc[(size_t)k * f];
+        const double d = ck[k];
+        if (!(d > 0.0)) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite");
+        const double dk = std::sqrt(d);
+        ck[k] = dk;
+        const double inv = 1.0 / dk;
+        for (int i = k + 1; i < f; ++i) ck[i] *= inv;
+        const long long work = (long long)(f - k) * (f - k);
+        (void)work;   // (only read by the OpenMP if-clause)
+#pragma omp parallel for schedule(dynamic, 16) if (inner_parallel && work > 200000)
+        for (int j = k + 1; j < f; ++j) {
+            const double ljk = ck[j];
+            if (ljk == 0.0) continue;
+            double* cj = &Fc[(size_t)j * f];
+            for (int i = j; i < f; ++i) cj[i] -= ck[i] * ljk;
         }
-        // ---- outputs: Linv (p x p lower, row-major), LBP (nb x p, row-major), update matrix (nb x nb)
-        std::vector<double> Li((size_t)p * p, 0.0);
-#pragma omp parallel for schedule(dynamic, 8) if (p > 256)
-        for (int j = 0; j < p; ++j) {  // column j of L^-1: column-oriented forward substitution
-            std::vector<double> r((size_t)p, 0.0);
-            r[j] = 1.0;
-            for (int k = j; k < p; ++k) {
-                const double xk = r[k] / FC(k, k);
-                Li[(size_t)k * p + j] = xk;
-                if (xk == 0.0) continue;
-                const double* ck = &Fc[(size_t)k * f];
-                for (int i = k + 1; i < p; ++i) r[i] -= ck[i] * xk;
-            }
+    }
+    // ---- outputs: Linv (p x p lower, row-major), LBP (nb x p, row-major), update matrix (nb x nb)
+    std::vector<double> Li((size_t)p * p, 0.0);
+#pragma omp parallel for schedule(dynamic, 8) if (inner_parallel && p > 256)
+    for (int j = 0; j < p; ++j) {  // column j of L^-1: column-oriented forward substitution
+        std::vector<double> r((size_t)p, 0.0);
+        r[j] = 1.0;
+        for (int k = j; k < p; ++k) {
+            const double xk = r[k] / FC(k, k);
+            Li[(size_t)k * p + j] = xk;
+            if (xk == 0.0) continue;
+            const double* ck = &Fc[(size_t)k * f];
+            for (int i = k + 1; i < p; ++i) r[i] -= ck[i] * xk;
         }
-        F.Linv[s] = std::move(Li);
-        std::vector<double> LBP((size_t)nb * p);
+    }
+    F.Linv[s] = std::move(Li);
+    std::vector<double> LBP((size_t)nb * p);
+    for (int a = 0; a < nb; ++a)
+        for (int j = 0; j < p; ++j) LBP[(size_t)a * p + j] = FC(p + a, j);
+    F.LBP[s] = std::move(LBP);
+    if (nb > 0) {
+        std::vector<double> Us((size_t)nb * nb);
         for (int a = 0; a < nb; ++a)
-            for (int j = 0; j < p; ++j) LBP[(size_t)a * p + j] = FC(p + a, j);
-        F.LBP[s] = std::move(LBP);
-        if (nb > 0) {
-            std::vector<double> Us((size_t)nb * nb);
-            for (int a = 0; a < nb; ++a)
-                for (int bb = 0; bb <= a; ++bb) Us[(size_t)a * nb + bb] = FC(p + a, p + bb);
-            U[s] = std::move(Us);
+            for (int bb = 0; bb <= a; ++bb) Us[(size_t)a * nb + bb] = FC(p + a, p + bb);
+        C.U[s] = std::move(Us);
+    }
+}
+
+}  // namespace
+
+SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, DenseFrontBackend* dense) {
+    SupernodalFactor F;
+    const int n = A.n, nn = (int)tree.beg.size();
+    F.n = n; F.n_nodes = nn;
+    F.beg = tree.beg; F.end = tree.end; F.parent = tree.parent;
+    F.bnd.resize(nn); F.Linv.resize(nn); F.LBP.resize(nn); F.M.resize(nn); F.height.assign(nn, 0);
+    symbolic(A, tree, F);
+    std::vector<std::vector<double>> U(nn);
+    std::vector<double> flops(nn, 0.0);
+    FrontCtx C{A, tree, F, U, flops, dense};
+    if (!dense) {   // host only: postorder, parallel inside the large fronts
+        std::vector<int> pos(n, -1);
+        for (int s = 0; s < nn; ++s) factor_front(C, s, pos, true);
+    } else {
+        // tree-parallel: independent subtrees are OpenMP tasks (a front waits for its children),
+        // each host front is factored by one thread; the large fronts near the root go to the
+        // dense backend, one at a time (it serialises its calls)
+        std::vector<long long> sub(nn, 0);   // pivots in the subtree
+        for (int s = 0; s < nn; ++s) {
+            sub[s] += tree.end[s] - tree.beg[s];
+            if (tree.parent[s] >= 0) sub[tree.parent[s]] += sub[s];
         }
+        const long long grain = std::max<long long>(256, n / 1024);
+        std::string err;
+        std::function<void(int)> rec = [&](int s) {
+            for (int c : tree.children[s]) {
+                if (sub[c] > grain) {
+#pragma omp task firstprivate(c) shared(rec)
+                    rec(c);
+                } else {
+                    rec(c);
+                }
+            }
+#pragma omp taskwait
+            static thread_local std::vector<int> pos;
+            if ((int)pos.size() < n) pos.assign(n, -1);
+            bool failed;
+#pragma omp critical(aa_factor_err)
+            failed = !err.empty();
+            if (failed) return;
+            try {
+                factor_front(C, s, pos, false);
+            } catch (const std::exception& e) {
+#pragma omp critical(aa_factor_err)
+                if (err.empty()) err = e.what();
+            }
+        };
+#pragma omp parallel
+#pragma omp single
+        {
+            for (int s = 0; s < nn; ++s)
+                if (tree.parent[s] < 0) {
+#pragma omp task firstprivate(s) shared(rec)
+                    rec(s);
+                }
+#pragma omp taskwait
+        }
+        if (!err.empty()) throw std::runtime_error(err);
+    }
+    for (int s = 0; s < nn; ++s) {
+        const int p = tree.end[s] - tree.beg[s], nb = (int)F.bnd[s].size();
+        F.flops += flops[s];
         F.nnz_L += (size_t)p * (p + 1) / 2 + (size_t)p * nb;
-        F.bnd[s] = std::move(bnd);
         F.max_height = std::max(F.max_height, F.height[s]);
     }
     return F;

@@ -50,14 +50,43 @@ struct SupernodalFactor {
     std::vector<std::vector<int>> bnd;      // row structure below the diagonal block (new indices, ascending)
     std::vector<std::vector<double>> Linv;  // p x p row-major, inverse of the (lower) diagonal block L_PP
     std::vector<std::vector<double>> LBP;   // b x p row-major, L(bnd, P)
+    std::vector<std::vector<double>> M;     // b x p row-major, L(bnd, P) Linv -- when the dense
+                                            // backend computed it (empty: the solver forms it)
     int max_height = 0;
     double flops = 0;
     size_t nnz_L = 0;                       // scalar nnz(L) incl. diagonal blocks (lower)
 };
 
+// Dense assembly + partial factorization of one front on an accelerator (dense_gpu.hip: rocSOLVER
+// / rocBLAS on the solver's GPU). The front (order f = p + nb, column-major, lower triangle) is
+// assembled from A's pivot columns (COO in front-local indices, row >= column) and then the
+// children's update matrices in child order -- the host loop's order, so the same sums -- after
+// which its first p columns are factored (L11 = chol, L21 = F21 L11^-T, F22 -= L21 L21^T).
+// Outputs: Linv = L11^-1 (row-major p x p, zero above the diagonal), LBP = L21 (row-major
+// nb x p), M = L21 Linv (row-major nb x p), and the update matrix F22: kept by the backend
+// (keep_update: the parent is factored there too) or returned in *U (row-major nb x nb, lower).
+// Throws std::runtime_error when the block is not positive definite.
+struct DenseFrontBackend {
+    struct Child {
+        int id;                          // supernode
+        const int* map;                  // front-local row of each of its m boundary rows
+        int m;
+        const std::vector<double>* U;    // host update matrix (row-major lower); null: held
+    };
+    virtual ~DenseFrontBackend() = default;
+    virtual void factor(int s, int f, int p, const std::vector<int>& ai, const std::vector<int>& aj,
+                        const std::vector<double>& av, const std::vector<Child>& kids, bool keep_update,
+                        std::vector<double>& Linv, std::vector<double>& LBP, std::vector<double>& M,
+                        std::vector<double>* U) = 0;
+    virtual bool holds(int s) const = 0;   // s's update matrix is held by the backend
+    int min_front = 1024;                  // fronts of at least this order go to the backend
+};
+
 // Factor the matrix A (given in NEW ordering as a full-pattern CSR) along the tree.
 // Throws std::runtime_error if A is not positive definite.
-SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree);
+// dense == nullptr: everything on the host, supernodes in postorder. Otherwise independent
+// subtrees are factored in parallel (OpenMP tasks) and the large fronts by `dense`.
+SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, DenseFrontBackend* dense = nullptr);
 
 // Host reference solve with the factor (used by self-checks): x = A^-1 b, b is n x 3.
 void factor_solve_host(const SupernodalFactor& F, std::vector<double>& b3);
