@@ -12,6 +12,8 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <memory>
@@ -94,6 +96,12 @@ public:
                 const std::vector<Child>& kids, bool keep_update, std::vector<double>& Linv, std::vector<double>& LBP,
                 std::vector<double>& M, std::vector<double>* U) override {
         std::lock_guard<std::mutex> g(mu_);
+        const auto t0 = std::chrono::steady_clock::now();
+        struct Tally {   // time inside the backend (AA_SETUP_TIMES)
+            RocFrontBackend* b;
+            std::chrono::steady_clock::time_point t0;
+            ~Tally() { b->busy_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); ++b->fronts; }
+        } tally{this, t0};
         const int nb = f - p;
         double* F = F_.get((size_t)f * f);
         AA_HIP(hipMemsetAsync(F, 0, (size_t)f * f * sizeof(double), s_));
@@ -187,6 +195,9 @@ public:
         }
     }
 
+    double busy_ms = 0;
+    int fronts = 0;
+
 private:
     hipStream_t s_;
     rocblas_handle h_ = nullptr;
@@ -209,7 +220,15 @@ SupernodalFactor factor_on_device(const CsrMatrix& A, const NdTree& tree, hipStr
     const char* e = std::getenv("AA_DENSE_GPU");
     if (e && e[0] == '0') return multifrontal_cholesky(A, tree, nullptr);
     auto b = make_gpu_front_backend(s);
-    return multifrontal_cholesky(A, tree, b.get());
+    const auto t0 = std::chrono::steady_clock::now();
+    SupernodalFactor F = multifrontal_cholesky(A, tree, b.get());
+    if (const char* t = std::getenv("AA_SETUP_TIMES"); t && t[0] == '1') {
+        const auto* rb = static_cast<const RocFrontBackend*>(b.get());
+        std::fprintf(stderr, "[setup]   factor %.1f ms: %d fronts on the GPU (%.1f ms inside the backend), %.1f GFLOP\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), rb->fronts,
+                     rb->busy_ms, F.flops * 1e-9);
+    }
+    return F;
 }
 
 }  // namespace aa

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <string>
 
 namespace aa {
@@ -493,6 +494,23 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
     }
 }
 
+// column-major copy of the factor blocks: Gc[goff + c*R + r] = Gr[goff + r*ld + c] (32 x 32 tile
+// per workgroup through LDS: coalesced reads along the row, coalesced writes along the column)
+struct TrTile { long long goff; int R, ld, p, r0, c0; };
+__global__ void k_gr_to_gc(const TrTile* __restrict__ tiles, const double* __restrict__ Gr, double* __restrict__ Gc) {
+    __shared__ double t[32][33];
+    const TrTile T = tiles[blockIdx.x];
+    for (int q = threadIdx.y; q < 32; q += blockDim.y) {
+        const int r = T.r0 + q, c = T.c0 + threadIdx.x;
+        if (r < T.R && c < T.p) t[q][threadIdx.x] = Gr[T.goff + (size_t)r * T.ld + c];
+    }
+    __syncthreads();
+    for (int q = threadIdx.y; q < 32; q += blockDim.y) {
+        const int c = T.c0 + q, r = T.r0 + threadIdx.x;
+        if (r < T.R && c < T.p) Gc[T.goff + (size_t)c * T.R + r] = t[threadIdx.x][q];
+    }
+}
+
 }  // namespace
 
 void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::vector<int>* node_part, int my_part,
@@ -535,13 +553,14 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         piv += ps;
         bsum += nbs;
     }
-    // G_s = [Linv ; M], M = L_BP Linv (row-major copy Gr and column-major copy Gc)
-    std::vector<double> Gr(go), Gc(go);
+    // G_s = [Linv ; M], M = L_BP Linv: the row-major copy Gr is formed here (every entry written,
+    // so no zero fill of the 1 GB buffer), the column-major copy Gc on the device from it
+    std::unique_ptr<double[]> Gr(new double[std::max<long long>(go, 1)]);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int sn = 0; sn < nn_; ++sn) {
         if (!inc[sn]) continue;
         const int ps = p[sn], nbs = nb[sn], R = ps + nbs, ld = ldr[sn];
-        double* gr = Gr.data() + goff[sn];
+        double* gr = Gr.get() + goff[sn];
         const std::vector<double>& Li = F.Linv[sn];
         const std::vector<double>& LB = F.LBP[sn];
         for (int r = 0; r < R; ++r)
@@ -563,9 +582,6 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 for (int c = 0; c <= k; ++c) m[c] += l * lr[c];
             }
         }
-        double* gc = Gc.data() + goff[sn];
-        for (int r = 0; r < R; ++r)
-            for (int c = 0; c < ps; ++c) gc[(size_t)c * R + r] = gr[(size_t)r * ld + c];
     }
     // children lists and ELL pull lists (front row q of a parent <- child update entries, fixed order)
     // (partitioned: the children of the top that belong to other GPUs' parts contribute nothing
@@ -901,7 +917,24 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     if (n_sub_) kernels_ += 2;
     bnd_.upload(bnd, s);
     ell_.upload(ell, s);
-    Gr_.upload(Gr, s); Gc_.upload(Gc, s);
+    Gr_.upload(Gr.get(), (size_t)go, s);
+    Gc_.alloc((size_t)go);
+    {   // Gc (column-major R x p per supernode) = transpose of Gr (row-major R x ldr), 32 x 32 tiles
+        std::vector<TrTile> tt;
+        for (int sn = 0; sn < nn_; ++sn) {
+            if (!inc[sn]) continue;
+            const int R = p[sn] + nb[sn];
+            for (int r0 = 0; r0 < R; r0 += 32)
+                for (int c0 = 0; c0 < p[sn]; c0 += 32) tt.push_back(TrTile{goff[sn], R, ldr[sn], p[sn], r0, c0});
+        }
+        if (!tt.empty()) {
+            DevBuf<TrTile> dt;
+            dt.upload(tt, s);
+            hipLaunchKernelGGL(k_gr_to_gc, dim3((unsigned)tt.size()), dim3(32, 8), 0, s, dt.p, Gr_.p, Gc_.p);
+            AA_CHECK_LAUNCH();
+            AA_HIP(hipStreamSynchronize(s));
+        }
+    }
     tasks_.upload(tasks, s);
     btiles_.upload(btiles, s);
     ftiles_.upload(ftiles, s);

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -146,6 +147,10 @@ void ElasticSolver::set_pins(const int* inds, const double* pts3, int n) {
 
 void ElasticSolver::initialize(const aa_settings& s_in) {
     auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::pair<const char*, double>> phases;   // AA_SETUP_TIMES=1: printed to stderr
+    auto stamp = [&](const char* what) {
+        phases.push_back({what, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()});
+    };
     drop_graph();
     if (const char* g = std::getenv("AA_ADMM_NO_GRAPH")) use_graph_ = !(g[0] == '1');
     if (comm_ && !comm_->capturable()) use_graph_ = false;
@@ -204,7 +209,9 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     int levels = 0;
     while ((1 << levels) < P) ++levels;
     if ((1 << levels) != P) throw Error(ERR_ARG, "initialize: the number of ranks must be a power of two");
+    stamp("adjacency");
     NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, levels);
+    stamp("nested dissection");
     node2int_.assign(n, -1);
     int2node_.assign(n, -1);
     for (int q = 0; q < nf_; ++q) { node2int_[free_nodes[tree.perm[q]]] = q; int2node_[q] = free_nodes[tree.perm[q]]; }
@@ -229,43 +236,71 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     // ---- global matrix A_s = M + pdt2 * sum_e w^2 G^T G  (Solver.cpp:466-467)
     const double dt2 = st_.timestep_s * st_.timestep_s;
     pdt2_ = (st_.variant == AA_VARIANT_UX ? st_.penalty : 1.0) * dt2;
-    std::vector<std::vector<std::pair<int, double>>> rows(nf_);
-    for (int q = 0; q < nf_; ++q) rows[q].push_back({q, m3_[3 * (size_t)int2node_[q]]});
-    for (auto& g : hgroups_) {
-        const size_t cnt = g.idx.size() / g.nv;
-        for (size_t t = 0; t < cnt; ++t) {
-            const double w2 = g.w[t] * g.w[t];
-            const double* G = &g.G[t * g.ncol * g.nv];
+    // rows in parallel: each free node sums its mass and its incident elements' w^2 G^T G
+    // entries in (group, element) order -- a fixed order, independent of the thread count
+    struct Inc { int g, t, a; };
+    std::vector<int> iptr(nf_ + 1, 0);
+    for (auto& g : hgroups_)
+        for (size_t t = 0; t < g.idx.size() / g.nv; ++t)
             for (int a = 0; a < g.nv; ++a) {
                 const int qa = node2int_[g.idx[t * g.nv + a]];
-                if (qa >= nf_) continue;
-                for (int b = 0; b < g.nv; ++b) {
-                    const int qb = node2int_[g.idx[t * g.nv + b]];
-                    if (qb >= nf_) continue;
-                    double sacc = 0;
-                    for (int c = 0; c < g.ncol; ++c) sacc += G[c * g.nv + a] * G[c * g.nv + b];
-                    rows[qa].push_back({qb, pdt2_ * w2 * sacc});
-                }
+                if (qa < nf_) ++iptr[qa + 1];
             }
+    for (int q = 0; q < nf_; ++q) iptr[q + 1] += iptr[q];
+    std::vector<Inc> inc(iptr[nf_]);
+    {
+        std::vector<int> fill(iptr.begin(), iptr.end() - 1);
+        for (int gi = 0; gi < (int)hgroups_.size(); ++gi) {
+            const auto& g = hgroups_[gi];
+            for (size_t t = 0; t < g.idx.size() / g.nv; ++t)
+                for (int a = 0; a < g.nv; ++a) {
+                    const int qa = node2int_[g.idx[t * g.nv + a]];
+                    if (qa < nf_) inc[fill[qa]++] = Inc{gi, (int)t, a};
+                }
         }
     }
-    CsrMatrix A;
-    A.n = nf_;
-    A.ptr.assign(nf_ + 1, 0);
+    std::vector<std::vector<std::pair<int, double>>> rows(nf_);
+#pragma omp parallel for schedule(dynamic, 256)
     for (int q = 0; q < nf_; ++q) {
-        auto& r = rows[q];
-        std::sort(r.begin(), r.end(), [](const std::pair<int, double>& a, const std::pair<int, double>& b) { return a.first < b.first; });
+        std::vector<std::pair<int, double>> r;
+        r.reserve(1 + 4 * (size_t)(iptr[q + 1] - iptr[q]));
+        r.push_back({q, m3_[3 * (size_t)int2node_[q]]});
+        for (int k = iptr[q]; k < iptr[q + 1]; ++k) {
+            const auto& g = hgroups_[inc[k].g];
+            const size_t t = inc[k].t;
+            const int a = inc[k].a;
+            const double w2 = g.w[t] * g.w[t];
+            const double* G = &g.G[t * g.ncol * g.nv];
+            for (int b = 0; b < g.nv; ++b) {
+                const int qb = node2int_[g.idx[t * g.nv + b]];
+                if (qb >= nf_) continue;
+                double sacc = 0;
+                for (int c = 0; c < g.ncol; ++c) sacc += G[c * g.nv + a] * G[c * g.nv + b];
+                r.push_back({qb, pdt2_ * w2 * sacc});
+            }
+        }
+        std::stable_sort(r.begin(), r.end(), [](const std::pair<int, double>& x, const std::pair<int, double>& y) { return x.first < y.first; });
+        std::vector<std::pair<int, double>> out;
         for (size_t k = 0; k < r.size();) {
             size_t k2 = k;
             double v = 0;
             while (k2 < r.size() && r[k2].first == r[k].first) v += r[k2++].second;
-            A.col.push_back(r[k].first);
-            A.val.push_back(v);
+            out.push_back({r[k].first, v});
             k = k2;
         }
-        A.ptr[q + 1] = (int)A.col.size();
-        std::vector<std::pair<int, double>>().swap(r);
+        rows[q] = std::move(out);
     }
+    CsrMatrix A;
+    A.n = nf_;
+    A.ptr.assign(nf_ + 1, 0);
+    for (int q = 0; q < nf_; ++q) A.ptr[q + 1] = A.ptr[q] + (int)rows[q].size();
+    A.col.resize(A.ptr[nf_]);
+    A.val.resize(A.ptr[nf_]);
+#pragma omp parallel for schedule(static)
+    for (int q = 0; q < nf_; ++q)
+        for (size_t k = 0; k < rows[q].size(); ++k) { A.col[A.ptr[q] + k] = rows[q][k].first; A.val[A.ptr[q] + k] = rows[q][k].second; }
+    std::vector<std::vector<std::pair<int, double>>>().swap(rows);
+    stamp("assembly of A_s");
     SupernodalFactor F;
     try {
         F = factor_on_device(A, tree, s());
@@ -277,8 +312,10 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     pipe_z_ = st_.variant == AA_VARIANT_Z && st_.acceleration_type == 1;
     if (const char* e = std::getenv("AA_Z_PIPELINE")) pipe_z_ = pipe_z_ && e[0] != '0';
     // Z variant + Anderson: the two-set layout whether pipelined or not (same sums, same bits)
+    stamp("factor");
     solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_, pipe_z_ ? 2 : 1,
                   st_.variant == AA_VARIANT_Z && st_.acceleration_type == 1);
+    stamp("solver build + upload");
 
     // ---- element ownership (partitioned): an element touching a node of part r belongs to
     // rank r (it cannot touch another part: the separators split the mesh); elements whose free
@@ -450,6 +487,11 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     for (auto& g : groups_) rt_.n_elements += g.d.count;
     rt_.z_dim = (int)Z_;
     rt_.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stamp("elements + buffers");
+    if (const char* e = std::getenv("AA_SETUP_TIMES"); e && e[0] == '1') {
+        double prev = 0;
+        for (auto& ph : phases) { std::fprintf(stderr, "[setup] %-24s %8.1f ms\n", ph.first, ph.second - prev); prev = ph.second; }
+    }
     // algorithmic bytes per launch class (DESIGN.md "roofline accounting")
     kstats_.clear();
     double lz = 0, rs = 0;
