@@ -23,6 +23,7 @@ EXPORTS = [
     "aa_last_error", "aa_version", "aa_ctx_create", "aa_ctx_destroy", "aa_ctx_synchronize", "aa_lame_from_young",
     "aa_settings_default", "aa_elastic_create", "aa_elastic_destroy", "aa_elastic_add_nodes", "aa_elastic_add_tets",
     "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
+    "aa_elastic_add_obstacle", "aa_elastic_set_collisions", "aa_elastic_add_wind", "aa_elastic_set_wind",
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
     "aa_elastic_get_times", "aa_elastic_set_iterations", "aa_elastic_set_x",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats", "aa_elastic_local_stats",
@@ -233,6 +234,28 @@ class Solver:
             p = np.ascontiguousarray(points, np.float64).reshape(-1)
             _chk(lib().aa_elastic_set_pins(self.h, _ip(i), _dp(p), C.c_int(len(i))))
 
+    def add_obstacle(self, kind, params):
+        """Solver::add_obstacle with a PassiveObject.hpp shape (AA_OBS_*)."""
+        p = np.zeros(8)
+        q = np.asarray(params, np.float64).reshape(-1)
+        p[:len(q)] = q
+        _chk(lib().aa_elastic_add_obstacle(self.h, C.c_int(kind), _dp(p)))
+
+    def set_collisions(self, inds):
+        i = np.ascontiguousarray(inds, np.int32).reshape(-1)
+        _chk(lib().aa_elastic_set_collisions(self.h, _ip(i), C.c_int(len(i))))
+
+    def add_wind(self, tris, direction):
+        t = np.ascontiguousarray(tris, np.int32).reshape(-1)
+        d = np.ascontiguousarray(direction, np.float64).reshape(3)
+        k = C.c_int()
+        _chk(lib().aa_elastic_add_wind(self.h, _ip(t), C.c_int(len(t) // 3), _dp(d), C.byref(k)))
+        return k.value
+
+    def set_wind(self, wid, direction):
+        d = np.ascontiguousarray(direction, np.float64).reshape(3)
+        _chk(lib().aa_elastic_set_wind(self.h, C.c_int(wid), _dp(d)))
+
     def set_comm(self, comm):
         """Partition over comm's ranks at initialize() (every rank binds the same scene)."""
         self.comm = comm   # the communicator must outlive the solver
@@ -324,6 +347,12 @@ def solver_from_scene(ctx: Context, scene, comm=None) -> Solver:
         else:
             s.add_tris(scene.rest_x, g.idx, lame)
     s.set_pins(scene.pin_idx, scene.pin_pts)
+    for kind, prm in getattr(scene, "obstacles", []):
+        s.add_obstacle(kind, prm)
+    if getattr(scene, "collision_idx", None) is not None:
+        s.set_collisions(scene.collision_idx)
+    for tris, direction in getattr(scene, "winds", []):
+        s.add_wind(tris, direction)
     return s
 
 

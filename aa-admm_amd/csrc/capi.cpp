@@ -144,6 +144,31 @@ int aa_elastic_set_pins(aa_elastic h, const int* inds, const double* pts3, int n
     return guarded([&] { NEED(h, "null handle"); h->s->set_pins(inds, pts3, n); });
 }
 
+int aa_elastic_add_obstacle(aa_elastic h, int type, const double* params) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        h->s->add_obstacle(type, params);
+    });
+}
+
+int aa_elastic_set_collisions(aa_elastic h, const int* inds, int n) {
+    return guarded([&] { NEED(h, "null handle"); h->s->set_collisions(inds, n); });
+}
+
+int aa_elastic_add_wind(aa_elastic h, const int* tris3, int n_tris, const double dir3[3], int* id) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        AA_HIP(hipSetDevice(h->ctx->c.device));
+        const int k = h->s->add_wind(tris3, n_tris, dir3);
+        if (id) *id = k;
+    });
+}
+
+int aa_elastic_set_wind(aa_elastic h, int id, const double dir3[3]) {
+    return guarded([&] { NEED(h, "null handle"); h->s->set_wind(id, dir3); });
+}
+
 int aa_elastic_initialize(aa_elastic h, const aa_settings* s) {
     return guarded([&] {
         NEED(h && s, "null argument");

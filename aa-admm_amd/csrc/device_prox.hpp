@@ -19,6 +19,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "elastic_kernels.hpp"
+
 namespace aa {
 namespace dev {
 
@@ -224,6 +226,75 @@ __device__ __forceinline__ void tet_linear_grad(const double* z, double kvol, do
             const double p = U[r * 3 + 0] * V[c * 3 + 0] + U[r * 3 + 1] * V[c * 3 + 1] + U[r * 3 + 2] * V[c * 3 + 2];
             g[c * 3 + r] = kvol * (F[r * 3 + c] - p);
         }
+}
+
+// (1/w) * ((w x + u) - c) of an identity-reduction row, without FMA contraction (c = -w x_pin for
+// a pinned node, whose x enters through c: the same sum)
+__device__ inline void collision_candidate(const double* x, const double* u, double w, double* q) {
+#pragma clang fp contract(off)
+    const double iw = 1.0 / w;
+    for (int i = 0; i < 3; ++i) q[i] = iw * (w * x[i] + u[i]);
+}
+
+// Collision::prox (admm_anderson_hard_zxu/src/CollisionEnergyTerm.hpp:79-91): the candidate q is
+// tested against every passive obstacle in insertion order; an obstacle replaces the running
+// (dx, point) when its signed distance is <= the current one (PassiveObject.hpp's `if (dx >
+// p.dx) return;`), and q moves to the closest surface point when the final dx < 0. The
+// signed-distance functions restate PassiveObject.hpp:32-136 with the reference's operation
+// order (no FMA contraction, Eigen's norm / normalize: division by sqrt of the squared norm).
+// Obstacle table: obs[0] = count, then kObsStride doubles each: type, parameters.
+__device__ inline void collision_prox(const double* q, const double* obs, double* out) {
+#pragma clang fp contract(off)
+    double best = 1.79769313486231570815e+308;   // std::numeric_limits<double>::max()
+    double pt[3] = {0.0, 0.0, 0.0};
+    const int n = obs ? (int)obs[0] : 0;
+    auto sq3 = [](double a, double b, double c) { return (a * a + b * b) + c * c; };   // squaredNorm
+    for (int k = 0; k < n; ++k) {
+        const double* o = obs + 1 + k * kObsStride;
+        const int type = (int)o[0];
+        double dx, p0, p1, p2;
+        if (type == OBS_FLOOR) {                      // Floor(y)                   :32-45
+            dx = q[1] - o[1];
+            p0 = q[0]; p1 = o[1]; p2 = q[2];
+        } else if (type == OBS_SLIDE_FLOOR) {         // SlideFloor(center, normal) :47-62
+            const double l0 = q[0] - o[1], l1 = q[1] - o[2], l2 = q[2] - o[3];
+            dx = l0 * o[4] + l1 * o[5] + l2 * o[6];
+            p0 = q[0] - dx * o[4]; p1 = q[1] - dx * o[5]; p2 = q[2] - dx * o[6];
+        } else if (type == OBS_SPHERE) {              // Sphere(center, rad)        :64-80
+            double d0 = q[0] - o[1], d1 = q[1] - o[2], d2 = q[2] - o[3];
+            const double z2 = sq3(d0, d1, d2), nrm = sqrt(z2);
+            dx = nrm - o[4];
+            if (dx > best) continue;
+            if (z2 > 0.0) { d0 /= nrm; d1 /= nrm; d2 /= nrm; }
+            p0 = o[1] + d0 * o[4]; p1 = o[2] + d1 * o[4]; p2 = o[3] + d2 * o[4];
+        } else if (type == OBS_PLANE_HALF_SPHERE) {   // PlaneAndHalfSphere         :82-116
+            const double dc = sqrt(sq3(q[0] - o[1], 0.0, q[2] - o[3])) - o[4];
+            if (dc > 0) {
+                dx = q[1] - o[2];
+                p0 = q[0]; p1 = o[2]; p2 = q[2];
+            } else {
+                const double dpl = q[1] - o[2];
+                double d0 = q[0] - o[1], d1 = q[1] - o[2], d2 = q[2] - o[3];
+                const double z2 = sq3(d0, d1, d2), nrm = sqrt(z2);
+                dx = dpl > 0 ? nrm + o[4] : o[4] - nrm;
+                if (dx > best) continue;
+                if (z2 > 0.0) { d0 /= nrm; d1 /= nrm; d2 /= nrm; }
+                p0 = o[1] + d0 * o[4]; p1 = o[2] + d1 * o[4]; p2 = o[3] + d2 * o[4];
+            }
+        } else {                                      // Cylinder(center, rad), axis z :118-136
+            double d0 = q[0] - o[1], d1 = q[1] - o[2], d2 = 0.0 - o[3];
+            const double z2 = sq3(d0, d1, d2), nrm = sqrt(z2);
+            dx = nrm - o[4];
+            if (dx > best) continue;
+            if (z2 > 0.0) { d0 /= nrm; d1 /= nrm; d2 /= nrm; }
+            p0 = o[1] + d0 * o[4] + 0.0; p1 = o[2] + d1 * o[4] + 0.0; p2 = o[3] + d2 * o[4] + q[2];
+        }
+        if (dx > best) continue;
+        best = dx;
+        pt[0] = p0; pt[1] = p1; pt[2] = p2;
+    }
+    if (best < 0) { out[0] = pt[0]; out[1] = pt[1]; out[2] = pt[2]; }
+    else { out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; }
 }
 
 }  // namespace dev

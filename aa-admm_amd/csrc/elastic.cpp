@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <numeric>
 #include <set>
 
@@ -120,6 +121,99 @@ void ElasticSolver::add_elements(int kind, int material, const double* verts3, c
     hgroups_.push_back(std::move(g));
 }
 
+// Solver::add_obstacle (admm_anderson_hard_zxu/src/Solver.cpp:346-348) with the passive objects of
+// PassiveObject.hpp:32-136. The collision terms read the obstacle table every iteration, so
+// obstacles may be added after initialize (as in the reference, whose prox walks the collider's
+// list each time).
+void ElasticSolver::add_obstacle(int type, const double* prm) {
+    if (!prm) throw Error(ERR_ARG, "add_obstacle: null parameters");
+    if (type < OBS_FLOOR || type > OBS_CYLINDER) throw Error(ERR_ARG, "add_obstacle: unknown obstacle type");
+    if ((int)obstacles_.size() >= kMaxObstacles) throw Error(ERR_ARG, "add_obstacle: too many obstacles");
+    std::array<double, kObsStride> o{};
+    o[0] = type;
+    const int np = type == OBS_FLOOR ? 1 : (type == OBS_SLIDE_FLOOR ? 6 : 4);
+    for (int k = 0; k < np; ++k) o[1 + k] = prm[k];
+    if (type == OBS_SLIDE_FLOOR) {   // SlideFloor ctor: normal.normalize() (Eigen: / sqrt(squaredNorm))
+        const double z2 = (o[4] * o[4] + o[5] * o[5]) + o[6] * o[6];
+        if (z2 > 0.0) { const double nr = std::sqrt(z2); o[4] /= nr; o[5] /= nr; o[6] /= nr; }
+    }
+    obstacles_.push_back(o);
+    if (initialized_) upload_obstacles();
+}
+
+void ElasticSolver::upload_obstacles() {
+    if (!obs_dev_.p) return;
+    std::vector<double> h(1 + kObsStride * obstacles_.size());
+    h[0] = (double)obstacles_.size();
+    for (size_t k = 0; k < obstacles_.size(); ++k) std::copy(obstacles_[k].begin(), obstacles_[k].end(), h.begin() + 1 + kObsStride * k);
+    AA_HIP(hipMemcpyAsync(obs_dev_.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s()));
+    AA_HIP(hipStreamSynchronize(s()));
+}
+
+// Solver::set_collisions (admm_anderson_hard_zxu/src/Solver.cpp:318-344): one Collision term
+// (CollisionEnergyTerm.hpp:41-117) per listed node, created at initialize after the other
+// terms, in node order (the reference's std::map). Called after initialize it changes nothing
+// (the reference only re-activates the terms it already made).
+void ElasticSolver::set_collisions(const int* inds, int n) {
+    if (n < 0 || (n > 0 && !inds)) throw Error(ERR_ARG, "**Solver::set_collisions Error: Bad input.");
+    const int nodes = num_nodes();
+    std::set<int> s;
+    for (int i = 0; i < n; ++i) {
+        if (inds[i] < 0 || inds[i] >= nodes) throw Error(ERR_ARG, "**Solver::set_collisions Error: Bad input.");
+        s.insert(inds[i]);
+    }
+    if (initialized_) return;
+    coll_nodes_.assign(s.begin(), s.end());
+}
+
+// WindForce (admm_anderson_hard_zxu/src/ExplicitForce.{hpp,cpp}) pushed to Solver::ext_forces:
+// applied to v at the start of every step, before gravity (Solver.cpp:49-53)
+int ElasticSolver::add_wind(const int* tris3, int ntris, const double* dir3) {
+    if (ntris < 0 || (ntris > 0 && !tris3) || !dir3) throw Error(ERR_ARG, "add_wind: bad input");
+    const int nodes = num_nodes();
+    auto w = std::make_unique<Wind>();
+    w->tris.assign(tris3, tris3 + 3 * (size_t)ntris);
+    for (int i : w->tris) if (i < 0 || i >= nodes) throw Error(ERR_ARG, "add_wind: triangle references a node that does not exist");
+    for (int c = 0; c < 3; ++c) w->dir[c] = dir3[c];
+    if (initialized_) build_wind(*w);
+    winds_.push_back(std::move(w));
+    return (int)winds_.size() - 1;
+}
+
+void ElasticSolver::set_wind(int id, const double* dir3) {
+    if (id < 0 || id >= (int)winds_.size() || !dir3) throw Error(ERR_ARG, "set_wind: bad wind id");
+    for (int c = 0; c < 3; ++c) winds_[id]->dir[c] = dir3[c];
+}
+
+// level schedule of the triangles (internal node ids): level(t) = 1 + the highest level of an
+// earlier triangle sharing one of its vertices
+void ElasticSolver::build_wind(Wind& w) {
+    const int nt = (int)(w.tris.size() / 3);
+    std::vector<int> tri(3 * (size_t)nt), lvl(nt), last(num_nodes(), -1);
+    int nl = 0;
+    for (int t = 0; t < nt; ++t) {
+        int l = 0;
+        for (int j = 0; j < 3; ++j) {
+            const int q = node2int_[w.tris[3 * (size_t)t + j]];
+            tri[3 * (size_t)t + j] = q;
+            l = std::max(l, last[q] + 1);
+        }
+        for (int j = 0; j < 3; ++j) last[tri[3 * (size_t)t + j]] = l;
+        lvl[t] = l;
+        nl = std::max(nl, l + 1);
+    }
+    std::vector<int> ptr(nl + 1, 0), ord(nt);
+    for (int t = 0; t < nt; ++t) ++ptr[lvl[t] + 1];
+    for (int l = 0; l < nl; ++l) ptr[l + 1] += ptr[l];
+    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+    for (int t = 0; t < nt; ++t) ord[fill[lvl[t]]++] = t;
+    w.dtris.upload(tri, s());
+    w.dord.upload(ord, s());
+    w.dlvl.upload(ptr, s());
+    w.nlvl = nl;
+    AA_HIP(hipStreamSynchronize(s()));
+}
+
 // Solver::set_pins (admm_anderson_hard_zxu/src/Solver.cpp:280-315). Pins are kept in a map
 // (like ConstraintSet::pins); each pinned node gets ITS OWN point. (The reference pairs the
 // i-th given point with the i-th pin in sorted order -- identical whenever inds are sorted.)
@@ -167,6 +261,29 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     if (st_.variant != AA_VARIANT_Z && st_.variant != AA_VARIANT_UX) throw Error(ERR_ARG, "initialize: bad variant");
     if (st_.admm_iters < 0) throw Error(ERR_ARG, "initialize: admm_iters < 0");
     std::fill(v_.begin(), v_.end(), 0.0);
+    if (st_.variant == AA_VARIANT_Z && !obstacles_.empty())   // admm_anderson_xzu/src/Solver.cpp:485-489
+        throw Error(ERR_ARG, "**Solver::add_obstacle Error: No collisions with LDLT solver");
+    if (st_.variant == AA_VARIANT_Z && !coll_nodes_.empty())
+        throw Error(ERR_ARG, "set_collisions: energy-based collisions exist in the (u,x) variant only (admm_anderson_hard_zxu)");
+    // collision terms (Solver.cpp:386-392): after the other terms, one per node in node order;
+    // Lame::soft_rubber (EnergyTerm.hpp:38), weight sqrt(2 k), volume 2 (CollisionEnergyTerm.hpp:63-70)
+    hgroups_.erase(std::remove_if(hgroups_.begin(), hgroups_.end(), [](const HostGroup& g) { return g.kind == 2; }),
+                   hgroups_.end());
+    if (!coll_nodes_.empty()) {
+        HostGroup g;
+        g.kind = 2; g.material = AA_LINEAR; g.nv = 1; g.ncol = 1;
+        const double E = 10000000.0, nu = 0.399;
+        g.lame = aa_lame{};
+        g.lame.mu = E / (2.0 * (1.0 + nu));
+        g.lame.lambda = E * nu / ((1.0 + nu) * (1.0 - 2.0 * nu));
+        g.lame.limit_min = -100.0; g.lame.limit_max = 100.0;
+        const double wt = std::sqrt((g.lame.lambda + (2.0 / 3.0) * g.lame.mu) * 2.0);
+        g.idx = coll_nodes_;
+        g.G.assign(coll_nodes_.size(), 1.0);
+        g.vol.assign(coll_nodes_.size(), 2.0);
+        g.w.assign(coll_nodes_.size(), wt);
+        hgroups_.push_back(std::move(g));
+    }
 
     n_ = n;
     np_ = (int)pins_.size();
@@ -384,6 +501,12 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
         d.idx = dg.idx.p; d.G = dg.G.p; d.w = dg.w.p; d.vol = dg.vol.p;
         d.mu = hg.lame.mu; d.lambda = hg.lame.lambda; d.k = hg.lame.lambda + (2.0 / 3.0) * hg.lame.mu;
         d.lmin = hg.lame.limit_min; d.lmax = hg.lame.limit_max;
+        if (hg.kind == 2) {   // the obstacle table the collision prox reads (fixed address: graph-safe)
+            if (!obs_dev_.p) obs_dev_.alloc(1 + (size_t)kObsStride * kMaxObstacles);
+            d.obs = obs_dev_.p;
+        } else {
+            d.obs = nullptr;
+        }
         zoff += (long long)d.dim * cnt;
         yrow += (long long)d.nv * cnt;
         red_blocks_ += blocks_for(cnt);
@@ -479,6 +602,8 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     }
     AA_HIP(hipStreamSynchronize(s()));
     initialized_ = true;
+    upload_obstacles();
+    for (auto& w : winds_) build_wind(*w);
     pins_dirty_ = true;
     rt_ = aa_runtime{};
     rt_.nnz_factor = (long long)F.nnz_L;
@@ -599,6 +724,9 @@ void ElasticSolver::prologue() {
     c.eps_rel = st_.eps_rel;
     AA_HIP(hipMemcpyAsync(ctrl_.p, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s()));
     launch_stamp(ctrl_.p, s());
+    for (auto& w : winds_)   // explicit forces before gravity (Solver.cpp:49-53), on the step's start state
+        launch_wind(w->dtris.p, w->dord.p, w->dlvl.p, w->nlvl, xs_.p, vs_.p, w->dir[0], w->dir[1], w->dir[2],
+                    st_.timestep_s, s());
     launch_predict(n_, nf_, xs_.p, vs_.p, mass_.p, st_.timestep_s, st_.gravity, xbar_.p, Mxbar_.p, xfull_.p, s());
     // partitioned: the mass term of a shared separator row enters the right-hand side once
     // (rank 0); the other ranks contribute only their elements' D^T rows to it

@@ -29,6 +29,12 @@ public:
     void add_elements(int kind, int material, const double* verts3, const int* idx, int count, const aa_lame& lame,
                       int vertex_offset);
     void set_pins(const int* inds, const double* pts3, int n);
+    // energy-based collisions of the (u,x) variant (admm_anderson_hard_zxu Solver.cpp:318-348)
+    void add_obstacle(int type, const double* params);
+    void set_collisions(const int* inds, int n);
+    // WindForce (ExplicitForce.hpp:39-47) on the given triangles; returns its id
+    int add_wind(const int* tris3, int ntris, const double* dir3);
+    void set_wind(int id, const double* dir3);
     // multi-GPU: partition the mesh over comm's ranks at initialize(); every
     // rank passes the same scene. Not owned; must outlive the solver.
     void set_comm(Comm* c);
@@ -72,6 +78,18 @@ private:
     std::vector<double> x_, v_, m3_;
     std::vector<HostGroup> hgroups_;
     std::map<int, std::array<double, 3>> pins_;
+    std::vector<std::array<double, kObsStride>> obstacles_;
+    std::vector<int> coll_nodes_;   // collision-checked nodes (sorted, as the reference's map)
+    struct Wind {
+        std::vector<int> tris;      // user node ids
+        double dir[3];
+        DevBuf<int> dtris, dord, dlvl;
+        int nlvl = 0;
+    };
+    std::vector<std::unique_ptr<Wind>> winds_;
+    DevBuf<double> obs_dev_;
+    void upload_obstacles();
+    void build_wind(Wind& w);
     std::vector<int> pin_order_;
     aa_settings st_{};
     bool initialized_ = false;

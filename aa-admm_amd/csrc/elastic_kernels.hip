@@ -71,7 +71,7 @@ __device__ __forceinline__ bool gated(const Ctrl* c, int gate_reject) {
 template <int NV>
 __device__ __forceinline__ void gather_F(const GroupDev& g, int e, const double* __restrict__ xfull, int nf, double* F,
                                          double* Cp) {
-    constexpr int NC = NV - 1;
+    constexpr int NC = ncol_of(NV);
 #pragma unroll
     for (int i = 0; i < 3 * NC; ++i) { F[i] = 0; Cp[i] = 0; }
 #pragma unroll
@@ -90,7 +90,7 @@ __device__ __forceinline__ void gather_F(const GroupDev& g, int e, const double*
 
 template <int NV>
 __device__ __forceinline__ void gather_P(const GroupDev& g, int e, const double* __restrict__ xfull, double* F) {
-    constexpr int NC = NV - 1;
+    constexpr int NC = ncol_of(NV);
 #pragma unroll
     for (int i = 0; i < 3 * NC; ++i) F[i] = 0;
 #pragma unroll
@@ -112,7 +112,7 @@ __device__ __forceinline__ void gather_P(const GroupDev& g, int e, const double*
 template <int NV>
 __device__ __forceinline__ void write_slots(const GroupDev& g, int e, int nf, double w, const double* zz,
                                             const double* Cp, const double* uu, double* __restrict__ y) {
-    constexpr int NC = NV - 1;
+    constexpr int NC = ncol_of(NV);
     double yc[3 * NC];
 #pragma unroll
     for (int i = 0; i < 3 * NC; ++i) yc[i] = w * (w * zz[i] - w * Cp[i] - uu[i]);
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
                                                     double* red, int red_off) {
     if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
     __shared__ double sm[kBlock / 64];
-    constexpr int NC = NV - 1, D = 3 * NC;
+    constexpr int NC = ncol_of(NV), D = 3 * NC;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     double part = 0;
     if (e < g.count) {
@@ -151,7 +151,13 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
             uu[i] = u ? u[g.zoff + (size_t)i * g.count + e] : 0.0;
             vin[i] = F[i] + uu[i] / w;
         }
-        if constexpr (NV == 3) {
+        if constexpr (NV == 1) {
+            // the (u,x) variant's candidate exactly as EnergyTerm::update_z forms it for an identity
+            // row (EnergyTerm.hpp:166-178: z = W^-1 (W x + u - c), W^-1 stored as 1/w): the
+            // contact decision is discrete, so the candidate is rounded like the reference's
+            if (variant == 1) dev::collision_candidate(F, uu, w, vin);
+            dev::collision_prox(vin, g.obs, zz);
+        } else if constexpr (NV == 3) {
             dev::tri_prox(vin, zz, variant, g.lmin, g.lmax);
         } else if constexpr (HYPER == 0) {
             dev::tet_linear_prox(vin, zz);
@@ -284,7 +290,7 @@ __global__ __launch_bounds__(kBlock) void k_resid_u(GroupDev g, const double* __
                                                     double* red_b, int red_off) {
     if (gated(ctrl, 0)) return;
     __shared__ double sm[kBlock / 64];
-    constexpr int NC = NV - 1, D = 3 * NC;
+    constexpr int NC = ncol_of(NV), D = 3 * NC;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     double pa = 0, pb = 0;
     if (e < g.count) {
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_u_and_y(GroupDev g, const double* __
                                                     const double* __restrict__ z, double* __restrict__ u,
                                                     double* __restrict__ y, int nf, int mode, int redo, Ctrl* ctrl) {
     if (gated(ctrl, redo)) return;
-    constexpr int NC = NV - 1, D = 3 * NC;
+    constexpr int NC = ncol_of(NV), D = 3 * NC;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= g.count) return;
     double F[D], Cp[D], zz[D], uu[D];
@@ -330,8 +336,9 @@ __global__ __launch_bounds__(kBlock) void k_u_and_y(GroupDev g, const double* __
         for (int i = 0; i < D; ++i) uu[i] += w * F[i] - w * zz[i];
     } else if (mode == 1) {
         double gr[D];
-        if constexpr (NV == 3) {
-            if (ctrl) ctrl->fail = 2;   // TriEnergyTerm::get_gradient throws in the reference
+        if constexpr (NV == 3 || NV == 1) {
+            // TriEnergyTerm::get_gradient / Collision::get_gradient throw in the reference
+            if (ctrl) ctrl->fail = 2;
 #pragma unroll
             for (int i = 0; i < D; ++i) gr[i] = 0;
         } else if constexpr (HYPER == 0) {
@@ -358,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_prim_z(GroupDev g, const double* __r
                                                    int red_off) {
     if (gated(ctrl, redo)) return;
     __shared__ double sm[kBlock / 64];
-    constexpr int NC = NV - 1, D = 3 * NC;
+    constexpr int NC = ncol_of(NV), D = 3 * NC;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     double pa = 0, pb = 0;
     if (e < g.count) {
@@ -381,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void k_prim_z(GroupDev g, const double* __r
 
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_init_z(GroupDev g, const double* __restrict__ xfull, double* __restrict__ z) {
-    constexpr int NC = NV - 1, D = 3 * NC;
+    constexpr int NC = ncol_of(NV), D = 3 * NC;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= g.count) return;
     double F[D];
@@ -1008,7 +1015,8 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
         AA_CHECK_LAUNCH();
         return;
     }
-    if (g.kind == 1) hipLaunchKernelGGL((k_local_z<3, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
+    if (g.kind == 2) hipLaunchKernelGGL((k_local_z<1, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
+    else if (g.kind == 1) hipLaunchKernelGGL((k_local_z<3, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
     else if (g.mat == 0) hipLaunchKernelGGL((k_local_z<4, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
     else hipLaunchKernelGGL((k_local_z<4, 1>), dim3(nb), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, variant, mode, ctrl, red, red_off);
     AA_CHECK_LAUNCH();
@@ -1018,7 +1026,8 @@ void launch_resid_update_u(const GroupDev& g, const double* xfull, const double*
                            int nf, Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s) {
     if (g.count == 0) return;
     const int nb = blocks_for(g.count);
-    if (g.kind == 1) hipLaunchKernelGGL(k_resid_u<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, xlast, z, u, nf, ctrl, red_a, red_b, red_off);
+    if (g.kind == 2) hipLaunchKernelGGL(k_resid_u<1>, dim3(nb), dim3(kBlock), 0, s, g, xfull, xlast, z, u, nf, ctrl, red_a, red_b, red_off);
+    else if (g.kind == 1) hipLaunchKernelGGL(k_resid_u<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, xlast, z, u, nf, ctrl, red_a, red_b, red_off);
     else hipLaunchKernelGGL(k_resid_u<4>, dim3(nb), dim3(kBlock), 0, s, g, xfull, xlast, z, u, nf, ctrl, red_a, red_b, red_off);
     AA_CHECK_LAUNCH();
 }
@@ -1027,7 +1036,8 @@ void launch_u_and_y(const GroupDev& g, const double* xfull, const double* z, dou
                     int redo, Ctrl* ctrl, hipStream_t s) {
     if (g.count == 0) return;
     const int nb = blocks_for(g.count);
-    if (g.kind == 1) hipLaunchKernelGGL((k_u_and_y<3, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, z, u, y, nf, mode, redo, ctrl);
+    if (g.kind == 2) hipLaunchKernelGGL((k_u_and_y<1, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, z, u, y, nf, mode, redo, ctrl);
+    else if (g.kind == 1) hipLaunchKernelGGL((k_u_and_y<3, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, z, u, y, nf, mode, redo, ctrl);
     else if (g.mat == 0) hipLaunchKernelGGL((k_u_and_y<4, 0>), dim3(nb), dim3(kBlock), 0, s, g, xfull, z, u, y, nf, mode, redo, ctrl);
     else hipLaunchKernelGGL((k_u_and_y<4, 1>), dim3(nb), dim3(kBlock), 0, s, g, xfull, z, u, y, nf, mode, redo, ctrl);
     AA_CHECK_LAUNCH();
@@ -1037,7 +1047,8 @@ void launch_prim_z(const GroupDev& g, const double* xfull, const double* z, cons
                    Ctrl* ctrl, double* red_a, double* red_b, int red_off, hipStream_t s) {
     if (g.count == 0) return;
     const int nb = blocks_for(g.count);
-    if (g.kind == 1) hipLaunchKernelGGL(k_prim_z<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z, zref, nf, redo, ctrl, red_a, red_b, red_off);
+    if (g.kind == 2) hipLaunchKernelGGL(k_prim_z<1>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z, zref, nf, redo, ctrl, red_a, red_b, red_off);
+    else if (g.kind == 1) hipLaunchKernelGGL(k_prim_z<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z, zref, nf, redo, ctrl, red_a, red_b, red_off);
     else hipLaunchKernelGGL(k_prim_z<4>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z, zref, nf, redo, ctrl, red_a, red_b, red_off);
     AA_CHECK_LAUNCH();
 }
@@ -1045,7 +1056,8 @@ void launch_prim_z(const GroupDev& g, const double* xfull, const double* z, cons
 void launch_init_z(const GroupDev& g, const double* xfull, double* z, hipStream_t s) {
     if (g.count == 0) return;
     const int nb = blocks_for(g.count);
-    if (g.kind == 1) hipLaunchKernelGGL(k_init_z<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z);
+    if (g.kind == 2) hipLaunchKernelGGL(k_init_z<1>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z);
+    else if (g.kind == 1) hipLaunchKernelGGL(k_init_z<3>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z);
     else hipLaunchKernelGGL(k_init_z<4>, dim3(nb), dim3(kBlock), 0, s, g, xfull, z);
     AA_CHECK_LAUNCH();
 }
@@ -1066,6 +1078,43 @@ void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b
 }
 
 __global__ void k_stamp(Ctrl* ctrl) { ctrl->clock0 = (long long)wall_clock64(); }
+
+// WindForce::project (ExplicitForce.cpp:47-104; helper::triangle_norm :28-39), Wejchert-Haumann
+// normal force, one workgroup sweeping the triangle levels (see launch_wind); Eigen's operation
+// order (squaredNorm (a + b) + c, normalized = n / sqrt(squaredNorm), dot (a + b) + c), no FMA.
+__global__ __launch_bounds__(1024) void k_wind(const int* __restrict__ tris3, const int* __restrict__ ord,
+                                               const int* __restrict__ lvl_ptr, int nlvl, const double* __restrict__ x,
+                                               double* __restrict__ v, double d0, double d1, double d2, double dt) {
+#pragma clang fp contract(off)
+    const double dir[3] = {d0, d1, d2};
+    for (int l = 0; l < nlvl; ++l) {
+        for (int k = lvl_ptr[l] + (int)threadIdx.x; k < lvl_ptr[l + 1]; k += blockDim.x) {
+            const int t = ord[k];
+            const size_t i0 = 3 * (size_t)tris3[3 * t], i1 = 3 * (size_t)tris3[3 * t + 1], i2 = 3 * (size_t)tris3[3 * t + 2];
+            double vr[3], a[3], b[3];
+            for (int c = 0; c < 3; ++c) {
+                vr[c] = (v[i0 + c] + v[i1 + c] + v[i2 + c]) / 3.0 - dir[c];
+                a[c] = x[i1 + c] - x[i0 + c];
+                b[c] = x[i2 + c] - x[i0 + c];
+            }
+            double n[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+            const double z2 = (n[0] * n[0] + n[1] * n[1]) + n[2] * n[2];
+            const double nrm = sqrt(z2);
+            double nu[3] = {n[0], n[1], n[2]};
+            if (z2 > 0.0) { nu[0] = n[0] / nrm; nu[1] = n[1] / nrm; nu[2] = n[2] / nrm; }
+            const double area = 0.5 * nrm;
+            const double alpha_n = 1000.0;
+            const double vn = (nu[0] * vr[0] + nu[1] * vr[1]) + nu[2] * vr[2];
+            const double sc = -alpha_n * area * vn * fabs(vn);
+            double f[3];
+            for (int c = 0; c < 3; ++c) { f[c] = sc * nu[c]; f[c] *= 0.33; f[c] *= dt; }
+            for (int c = 0; c < 3; ++c) v[i0 + c] += f[c];
+            for (int c = 0; c < 3; ++c) v[i1 + c] += f[c];
+            for (int c = 0; c < 3; ++c) v[i2 + c] += f[c];
+        }
+        __syncthreads();
+    }
+}
 
 void launch_stamp(Ctrl* ctrl, hipStream_t s) {
     hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, s, ctrl);
@@ -1155,6 +1204,13 @@ void launch_test_prox(int op, const double* prm4, const double* in, int n, doubl
 
 void launch_test_cod(int n, const double* M, const double* b, double* x, hipStream_t s) {
     hipLaunchKernelGGL(k_test_cod, dim3(1), dim3(kSolveBlock), 0, s, n, M, b, x);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_wind(const int* tris3, const int* tri_ord, const int* lvl_ptr, int nlvl, const double* x, double* v,
+                 double dir0, double dir1, double dir2, double dt, hipStream_t s) {
+    if (nlvl <= 0) return;
+    hipLaunchKernelGGL(k_wind, dim3(1), dim3(1024), 0, s, tris3, tri_ord, lvl_ptr, nlvl, x, v, dir0, dir1, dir2, dt);
     AA_CHECK_LAUNCH();
 }
 

@@ -9,7 +9,7 @@ constexpr double kCombEps = 1e-20; // Solver.cpp:93 eps
 
 // One homogeneous block of energy terms (same kind / material / Lame), SoA on device.
 struct GroupDev {
-    int kind;            // 0 tet, 1 tri
+    int kind;            // 0 tet, 1 tri, 2 collision point (CollisionEnergyTerm.hpp:41-117)
     int mat;             // 0 linear, 1 NeoHookean, 2 StVK
     int count;           // elements
     int nv, ncol, dim;   // 4/3/9 for tets, 3/2/6 for tris
@@ -21,7 +21,12 @@ struct GroupDev {
     const double* w;     // [count] ADMM weights sqrt(k*vol)
     const double* vol;   // [count]
     double mu, lambda, k, lmin, lmax;
+    const double* obs;   // collision points: the obstacle table (obs[0] = count, then kObsStride per obstacle)
 };
+// passive obstacles of the collision terms (PassiveObject.hpp:32-136): type, then up to 7 parameters
+enum ObsType { OBS_FLOOR = 0, OBS_SLIDE_FLOOR = 1, OBS_SPHERE = 2, OBS_PLANE_HALF_SPHERE = 3, OBS_CYLINDER = 4 };
+constexpr int kObsStride = 8, kMaxObstacles = 256;
+__host__ __device__ constexpr int ncol_of(int nv) { return nv > 1 ? nv - 1 : 1; }   // 1 vertex: identity reduction
 
 // Device-side control block: residual bookkeeping, reject/done flags, Anderson state.
 struct Ctrl {
@@ -117,6 +122,13 @@ void launch_init_z(const GroupDev& g, const double* xfull, double* z, hipStream_
 // new state: x = xsrc (free) / xfull (pinned); v = (x_new - x_old)/dt
 void launch_finalize(int n, int nf, const double* xsrc, const double* xfull, double* xstate, double* vstate, double dt,
                      hipStream_t s);
+// WindForce::project (ExplicitForce.cpp:47-104) on the step's start state: v += dt 0.33 f_n per
+// triangle vertex, triangles in the given order. lvl_ptr[l]..lvl_ptr[l+1] index tri_ord: a level's
+// triangles share no vertex with each other, and every earlier triangle sharing a vertex with one
+// of them sits in an earlier level -- so one workgroup sweeping the levels reproduces the
+// sequential loop (the reference's single-thread order) exactly.
+void launch_wind(const int* tris3, const int* tri_ord, const int* lvl_ptr, int nlvl, const double* x, double* v,
+                 double dir0, double dir1, double dir2, double dt, hipStream_t s);
 
 // ---- Anderson acceleration (device-side AndersonAcceleration::compute_impl) -----------
 // G: the fixed-point map output (2 segments); cur: the stored current iterate (current_u_);

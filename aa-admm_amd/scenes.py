@@ -30,6 +30,8 @@ from typing import List, Optional
 import numpy as np
 
 TET, TRI = 0, 1
+# passive obstacles (PassiveObject.hpp:32-136; include/aa_admm.h AA_OBS_*)
+OBS_FLOOR, OBS_SLIDE_FLOOR, OBS_SPHERE, OBS_PLANE_HALF_SPHERE, OBS_CYLINDER = 0, 1, 2, 3, 4
 LINEAR, NEOHOOKEAN, STVK = 0, 1, 2
 VARIANT_X, VARIANT_H = 0, 1  # admm_anderson_xzu (z-AA) / admm_anderson_hard_zxu ((u,x)-AA)
 
@@ -70,6 +72,12 @@ class Scene:
     n_steps: int = 1
     name: str = "scene"
     rest: Optional[np.ndarray] = None   # (n, 3) rest positions of the elements; None = x
+    # (u,x) variant extras (admm_anderson_hard_zxu): passive obstacles [(type, params)] and the
+    # collision-checked nodes (Solver::add_obstacle / set_collisions), and WindForces
+    # [(tris (t, 3) int32, direction (3,))] (Solver::ext_forces)
+    obstacles: list = dataclasses.field(default_factory=list)
+    collision_idx: Optional[np.ndarray] = None
+    winds: list = dataclasses.field(default_factory=list)
 
     @property
     def rest_x(self) -> np.ndarray:
@@ -231,3 +239,154 @@ def beams(dim=3, *, variant=VARIANT_X, aa_m=6, iters=100, n_steps=1, accel=1, ma
     return Scene(x=x, masses=m, groups=groups, pin_idx=np.array(pins, np.int32), pin_pts=np.array(pts),
                  pin_vel=np.array(vel), variant=variant, iters=iters, aa_m=aa_m, n_steps=n_steps, accel=accel,
                  name=f"beams{dim}")
+
+
+# ----------------------------------------------------------------------------------------
+# tet-mesh files and the sample binding (f2)
+# ----------------------------------------------------------------------------------------
+
+def load_elenode(path: str):
+    """mcl::meshio::load_elenode (deps/mclscene/include/MCL/MeshIO.hpp:180-290): `path`.ele and
+    `path`.node (TetGen format); 1-based files are detected from the first record's index, as the
+    reference does. Vertices come back as float32 (mcl::TetMesh stores Vec3f), tets as int32."""
+    def records(fname):
+        with open(fname) as f:
+            lines = [ln.split("#", 1)[0].split() for ln in f]
+        lines = [ln for ln in lines if ln]
+        return int(lines[0][0]), lines[1:]
+    n_tets, rows = records(path + ".ele")
+    tets = np.zeros((n_tets, 4), np.int32)
+    seen = np.zeros(n_tets, bool)
+    one = False
+    for i, r in enumerate(rows[:n_tets]):
+        idx, ids = int(r[0]), [int(v) for v in r[1:5]]
+        if i == 0 and idx == 1:
+            one = True
+        if one:
+            idx -= 1
+            ids = [v - 1 for v in ids]
+        if idx >= n_tets:
+            raise ValueError("**TetMesh Error: Your indices are bad for file " + path + ".ele")
+        tets[idx] = ids
+        seen[idx] = True
+    if not seen.all():
+        raise ValueError("**TetMesh Error: Your indices are bad for file " + path + ".ele")
+    n_nodes, rows = records(path + ".node")
+    verts = np.zeros((n_nodes, 3), np.float32)
+    seen = np.zeros(n_nodes, bool)
+    one = False
+    for i, r in enumerate(rows[:n_nodes]):
+        idx = int(r[0])
+        if i == 0 and idx == 1:
+            one = True
+        if one:
+            idx -= 1
+        if idx >= n_nodes:
+            raise ValueError("**TetMesh Error: Your indices are bad for file " + path + ".node")
+        verts[idx] = np.array([float(r[1]), float(r[2]), float(r[3])], np.float64).astype(np.float32)
+        seen[idx] = True
+    if not seen.all():
+        raise ValueError("**TetMesh Error: Your indices are bad for file " + path + ".node")
+    return verts, tets
+
+
+def xform_scale_trans(verts32: np.ndarray, scale, trans) -> np.ndarray:
+    """mesh->apply_xform(make_trans(t) * make_scale(s)) in float32 (mcl::XForm<float>): v' = s v + t."""
+    s = np.asarray(scale, np.float32).reshape(1, 3)
+    t = np.asarray(trans, np.float32).reshape(1, 3)
+    return (verts32.astype(np.float32) * s + t).astype(np.float32)
+
+
+def tetmesh_masses32(verts32: np.ndarray, tets: np.ndarray, density: float = 1522.0) -> np.ndarray:
+    """TetMesh::weighted_masses (TetMesh.hpp:297-315) in float32, tets in order: |det(E)/6| * density / 4
+    added to each corner, det of the edge matrix by Eigen's 3x3 cofactor expansion."""
+    v = verts32.astype(np.float32)
+    m = np.zeros(len(v), np.float32)
+    dens = np.float32(density)
+    six, four = np.float32(6.0), np.float32(4.0)
+    e1 = v[tets[:, 1]] - v[tets[:, 0]]
+    e2 = v[tets[:, 2]] - v[tets[:, 0]]
+    e3 = v[tets[:, 3]] - v[tets[:, 0]]
+    # columns are the edges: m(r, c) = e_c[r]
+    m00, m10, m20 = e1[:, 0], e1[:, 1], e1[:, 2]
+    m01, m11, m21 = e2[:, 0], e2[:, 1], e2[:, 2]
+    m02, m12, m22 = e3[:, 0], e3[:, 1], e3[:, 2]
+    # Eigen determinant_impl<3>: first-row expansion (Eigen/src/LU/Determinant.h)
+    det = (m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20)) + m02 * (m10 * m21 - m11 * m20)
+    tm = (dens * np.abs(det / six)).astype(np.float32) / four
+    for t in range(len(tets)):          # float accumulation in tet order
+        for a in range(4):
+            m[tets[t, a]] = np.float32(m[tets[t, a]] + tm[t])
+    return m
+
+
+def tetmesh_scene(verts32, tets, material=LINEAR, E=1e7, nu=0.499, **kw) -> Scene:
+    """binding::add_tetmesh (samples/utils/AddMeshes.hpp:97-178) for one mesh: positions and the
+    element rest shape are the float32 vertices (create_tets_from_mesh<float, ...>), masses
+    TetMesh::weighted_masses(1522) per node x3 (zero mass throws, as the binding does)."""
+    m = tetmesh_masses32(verts32, tets)
+    if np.any(m <= 0):
+        raise ValueError("TetMesh Error: Zero mass")
+    x = verts32.astype(np.float64)
+    return Scene(x=x, masses=m.astype(np.float64), groups=[ElementGroup(TET, material, E, nu, np.asarray(tets, np.int32))],
+                 pin_idx=np.zeros(0, np.int32), pin_pts=np.zeros((0, 3)), pin_vel=np.zeros((0, 3)), **kw)
+
+
+# ----------------------------------------------------------------------------------------
+# collision / wind scenes of the (u,x) variant (samples/Asia2019/plinko*.cpp, windyflag.cpp)
+# ----------------------------------------------------------------------------------------
+
+def plinko_hit(verts32, tets, *, y0=-1.0, iters=13, accel=0, aa_m=2, n_steps=20, dt=1.0 / 30.0, squash=0.95) -> Scene:
+    """plinkohit.cpp:39-103: a linear-rubber tet mesh (Lame::rubber, `binding::LINEAR`) scaled by 13
+    and moved to (0.25, y0, 0), dropped on PlaneAndHalfSphere(center (0,-3,0), radius 1) with every
+    node collision-checked; admm_iters 13 and the other Solver::Settings defaults (dt 1/30, no
+    acceleration, m = 2). y0 = 2.5 in the sample; lower here so contact starts within a few steps.
+    The initial pose is the rest shape squashed to `squash` in y (rest kept for the elements), so
+    the residuals carry signal before the first contact (an unstressed free fall is all rounding
+    noise, which Anderson mixing then amplifies differently from run to run of any two codes)."""
+    v = xform_scale_trans(verts32, (13.0, 13.0, 13.0), (0.25, y0, 0.0))
+    sc = tetmesh_scene(v, tets, LINEAR, 10000000.0, 0.499, variant=VARIANT_H, iters=iters, accel=accel, aa_m=aa_m,
+                       n_steps=n_steps, dt=dt, name="plinkohit")
+    _squash(sc, squash)
+    sc.obstacles = [(OBS_PLANE_HALF_SPHERE, (0.0, float(np.float32(-3.0)), 0.0, float(np.float32(1.0))))]
+    sc.collision_idx = np.arange(sc.n_nodes, dtype=np.int32)
+    return sc
+
+
+def obstacle_course(verts32, tets, *, iters=15, accel=1, aa_m=5, n_steps=18, dt=1.0 / 30.0, squash=0.95) -> Scene:
+    """Every PassiveObject.hpp shape at once under a falling rubber mesh (plinkopony.cpp:54-117
+    uses Cylinder and SlideFloor, plinkohit PlaneAndHalfSphere): a sphere and two z-axis cylinders
+    the mesh hits first, then a tilted SlideFloor, a Floor and a PlaneAndHalfSphere below."""
+    v = xform_scale_trans(verts32, (13.0, 13.0, 13.0), (0.0, 0.2, 0.0))
+    sc = tetmesh_scene(v, tets, LINEAR, 10000000.0, 0.499, variant=VARIANT_H, iters=iters, accel=accel, aa_m=aa_m,
+                       n_steps=n_steps, dt=dt, name="obstacles")
+    _squash(sc, squash)
+    sc.obstacles = [
+        (OBS_SPHERE, (0.3, -1.2, 0.1, 0.45)),
+        (OBS_CYLINDER, (-0.6, -1.0, 0.0, 0.3)),
+        (OBS_CYLINDER, (0.9, -1.4, 0.0, 0.25)),
+        (OBS_SLIDE_FLOOR, (0.0, -2.0, 0.0, 0.5, 3.0 ** 0.5 / 2.0, 0.0)),
+        (OBS_FLOOR, (-2.3,)),
+        (OBS_PLANE_HALF_SPHERE, (0.2, -2.6, 0.0, 0.8)),
+    ]
+    sc.collision_idx = np.arange(sc.n_nodes, dtype=np.int32)
+    return sc
+
+
+def _squash(sc: Scene, f: float) -> None:
+    """initial pose = rest squashed by f in y about its centre (tet_drop's recipe); rest unchanged"""
+    if f == 1.0:
+        return
+    sc.rest = sc.x.copy()
+    c = 0.5 * (sc.x[:, 1].min() + sc.x[:, 1].max())
+    sc.x = sc.x.copy()
+    sc.x[:, 1] = c + f * (sc.x[:, 1] - c)
+
+
+def windy_cloth(nx=12, ny=12, *, iters=30, aa_m=6, accel=1, n_steps=3, direction=(25.0, 0.0, 5.0)) -> Scene:
+    """windyflag.cpp:63-127 headless: the C2 cloth (two pinned corners) with a WindForce on all of
+    its faces, direction = orig_wind (10, 0, 2) * 2.5."""
+    sc = cloth(nx, ny, iters=iters, n_steps=n_steps, aa_m=aa_m, accel=accel)
+    sc.winds = [(np.asarray(sc.groups[0].idx, np.int32), np.asarray(direction, np.float64))]
+    sc.name = f"windycloth{nx}x{ny}"
+    return sc

@@ -94,6 +94,32 @@ int aa_elastic_add_tris(aa_elastic h, const double* verts3, const int* tris3, in
                         int vertex_offset);
 /* Solver::set_pins(inds, points): points3 == NULL pins in place (Solver.cpp:280-315). */
 int aa_elastic_set_pins(aa_elastic h, const int* inds, const double* points3, int n_pins);
+
+/* Passive obstacles (admm_anderson_hard_zxu/src/PassiveObject.hpp:32-136), Solver::add_obstacle
+ * (Solver.cpp:346-348). params: FLOOR {y}; SLIDE_FLOOR {cx,cy,cz, nx,ny,nz} (the normal is
+ * normalised, as the SlideFloor constructor does); SPHERE / PLANE_HALF_SPHERE / CYLINDER
+ * {cx,cy,cz, r} (the cylinder's axis is z). The collision terms test every obstacle in insertion
+ * order each iteration; obstacles may be added after initialize. The z-AA variant rejects
+ * obstacles at initialize (admm_anderson_xzu/src/Solver.cpp:485-489). The BVH mesh obstacle
+ * (PassiveMesh) is not provided. */
+#define AA_OBS_FLOOR 0
+#define AA_OBS_SLIDE_FLOOR 1
+#define AA_OBS_SPHERE 2
+#define AA_OBS_PLANE_HALF_SPHERE 3
+#define AA_OBS_CYLINDER 4
+int aa_elastic_add_obstacle(aa_elastic h, int type, const double* params);
+/* Solver::set_collisions(inds, points) (admm_anderson_hard_zxu/src/Solver.cpp:318-344): one
+ * Collision energy term (CollisionEnergyTerm.hpp:41-117: identity reduction, weight
+ * sqrt(2 k(soft rubber)), prox = closest obstacle surface point when inside one) per listed node,
+ * created at initialize after the other terms in node order. The reference's points are never read
+ * by the prox and are not taken here. (u,x) variant only; after initialize it changes nothing. */
+int aa_elastic_set_collisions(aa_elastic h, const int* inds, int n);
+/* WindForce (ExplicitForce.hpp:39-47, ExplicitForce.cpp:47-104) pushed to Solver::ext_forces:
+ * every step, before gravity, v += 0.33 dt f_n on the vertices of each listed triangle (the
+ * Wejchert-Haumann normal force of the relative velocity v - dir), triangles in the given order
+ * (the reference's loop run on one thread). *id names it for aa_elastic_set_wind. */
+int aa_elastic_add_wind(aa_elastic h, const int* tris3, int n_tris, const double dir3[3], int* id);
+int aa_elastic_set_wind(aa_elastic h, int id, const double dir3[3]);   /* WindForce::direction */
 int aa_elastic_initialize(aa_elastic h, const aa_settings* settings);    /* Solver::initialize */
 int aa_elastic_step(aa_elastic h);                                       /* Solver::step       */
 int aa_elastic_num_nodes(aa_elastic h, int* n);

@@ -8,6 +8,8 @@
 //   admm::create_tets_from_mesh<float, admm::NeoHookeanTet>(solver.energyterms, verts, inds, n, lame, off);
 //   admm::create_tris_from_mesh<float, admm::TriEnergyTerm>(solver.energyterms, verts, inds, n, lame, off);
 //   solver.set_pins(pins, points);                     // Solver::set_pins
+//   solver.add_obstacle(std::make_shared<admm::Floor>(-1.0)); solver.set_collisions(inds);  // (u,x) variant
+//   solver.ext_forces.push_back(std::make_shared<admm::WindForce>(faces));                    // wind
 //   solver.initialize(settings);                       // Solver::initialize (returns bool)
 //   solver.step();                                     // Solver::step; solver.m_x / m_v updated
 //
@@ -95,6 +97,58 @@ inline void create_tris_from_mesh(std::vector<std::shared_ptr<EnergyTerm>>& ener
     energyterms.push_back(e);
 }
 
+typedef std::array<double, 3> Vec3d;
+
+// Passive obstacles (admm_anderson_hard_zxu/src/PassiveObject.hpp:32-136, Collider.hpp:63-82):
+// shape descriptors, tested on the device by the collision terms
+class PassiveCollision {
+public:
+    virtual ~PassiveCollision() {}
+    int type = AA_OBS_FLOOR;
+    double params[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+class Floor : public PassiveCollision {
+public:
+    explicit Floor(double y) { type = AA_OBS_FLOOR; params[0] = y; }
+};
+class SlideFloor : public PassiveCollision {
+public:
+    SlideFloor(const Vec3d& c, const Vec3d& n) {
+        type = AA_OBS_SLIDE_FLOOR;
+        for (int i = 0; i < 3; ++i) { params[i] = c[i]; params[3 + i] = n[i]; }
+    }
+};
+class Sphere : public PassiveCollision {
+public:
+    Sphere(const Vec3d& c, double r) { type = AA_OBS_SPHERE; for (int i = 0; i < 3; ++i) params[i] = c[i]; params[3] = r; }
+};
+class PlaneAndHalfSphere : public PassiveCollision {
+public:
+    PlaneAndHalfSphere(const Vec3d& c, double r) {
+        type = AA_OBS_PLANE_HALF_SPHERE;
+        for (int i = 0; i < 3; ++i) params[i] = c[i];
+        params[3] = r;
+    }
+};
+class Cylinder : public PassiveCollision {
+public:
+    Cylinder(const Vec3d& c, double r) { type = AA_OBS_CYLINDER; for (int i = 0; i < 3; ++i) params[i] = c[i]; params[3] = r; }
+};
+
+// Explicit forces (ExplicitForce.hpp:33-47): WindForce on a list of triangles (flat, 3 per face);
+// `direction` may be changed between steps (windyflag.cpp's intensity keys)
+class ExplicitForce {
+public:
+    virtual ~ExplicitForce() {}
+};
+class WindForce : public ExplicitForce {
+public:
+    explicit WindForce(std::vector<int>& tris_) : tris(tris_), direction{{0, 0, 0}} {}
+    std::vector<int> tris;
+    Vec3d direction;
+    int id = -1;   // device handle once registered
+};
+
 class Solver {
 public:
     typedef std::vector<double> VecX;      // Eigen::VectorXd in the reference (no Eigen dependency here)
@@ -119,6 +173,7 @@ public:
 
     VecX m_x, m_v, m_masses;   // scaled x3, as the reference
     std::vector<std::shared_ptr<EnergyTerm>> energyterms;
+    std::vector<std::shared_ptr<ExplicitForce>> ext_forces;   // Solver.hpp:90
 
     explicit Solver(int device = 0) {
         check(aa_ctx_create(device, &ctx_));
@@ -147,6 +202,14 @@ public:
         if (points.size() == inds.size())
             for (auto& p : points) { pin_pts_.push_back(p[0]); pin_pts_.push_back(p[1]); pin_pts_.push_back(p[2]); }
         if (initialized_) push_pins();
+    }
+
+    // Solver::add_obstacle (Solver.cpp:346-348): takes effect at once, also between steps
+    void add_obstacle(std::shared_ptr<PassiveCollision> obj) { check(aa_elastic_add_obstacle(h_, obj->type, obj->params)); }
+    // Solver::set_collisions (Solver.cpp:318-344): the points are not used by the prox
+    void set_collisions(const std::vector<int>& inds, const std::vector<Vec3>& points = std::vector<Vec3>()) {
+        (void)points;
+        check(aa_elastic_set_collisions(h_, inds.data(), (int)inds.size()));
     }
 
     // Nodes and energy terms are handed to the device solver on the FIRST initialize(); a later
@@ -179,6 +242,12 @@ public:
     // m_x / m_v edited by the caller between steps (the reference reads them directly) are pushed
     // to the device first.
     void step() {
+        for (auto& f : ext_forces) {   // register new forces, push the current wind directions
+            auto w = std::dynamic_pointer_cast<WindForce>(f);
+            if (!w) throw std::runtime_error("ext_forces: only WindForce is provided");
+            if (w->id < 0) check(aa_elastic_add_wind(h_, w->tris.data(), (int)w->tris.size() / 3, w->direction.data(), &w->id));
+            else check(aa_elastic_set_wind(h_, w->id, w->direction.data()));
+        }
         if (!x_seen_.empty() && x_seen_ != m_x) check(aa_elastic_set_x(h_, m_x.data()));
         if (!v_seen_.empty() && v_seen_ != m_v) check(aa_elastic_set_v(h_, m_v.data()));
         check(aa_elastic_step(h_));

@@ -19,6 +19,10 @@
 #include "Solver.hpp"
 #include "TetEnergyTerm.hpp"
 #include "TriEnergyTerm.hpp"
+#include "ExplicitForce.hpp"
+#ifdef REF_VARIANT_H
+#include "PassiveObject.hpp"
+#endif
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -87,6 +91,32 @@ int main(int argc, char** argv) {
     r.arr(pin_vel, 3 * (size_t)n_pins);
     const double dt = r.get<double>(), gravity = r.get<double>(), penalty = r.get<double>();
     const int iters = r.get<int>(), accel = r.get<int>(), aa_m = r.get<int>(), n_steps = r.get<int>();
+    // optional extras (AAEXTRA1): passive obstacles, collision nodes, wind forces
+    struct Obs { int type; double p[8]; };
+    std::vector<Obs> obstacles;
+    std::vector<int> coll;
+    std::vector<std::pair<std::vector<int>, std::vector<double>>> winds;
+    char emagic[8];
+    if (fread(emagic, 1, 8, f) == 8 && memcmp(emagic, "AAEXTRA1", 8) == 0) {
+        const int no = r.get<int>();
+        for (int k = 0; k < no; ++k) {
+            Obs o;
+            o.type = r.get<int>();
+            for (double& v : o.p) v = r.get<double>();
+            obstacles.push_back(o);
+        }
+        const int nc = r.get<int>();
+        r.arr(coll, nc);
+        const int nw = r.get<int>();
+        for (int k = 0; k < nw; ++k) {
+            const int nt = r.get<int>();
+            std::vector<int> tr;
+            std::vector<double> d;
+            r.arr(tr, 3 * (size_t)nt);
+            r.arr(d, 3);
+            winds.push_back({tr, d});
+        }
+    }
     fclose(f);
 #ifdef REF_VARIANT_H
     if (variant != 1) { fprintf(stderr, "scene asks for the z-AA (X) variant; this is the H build\n"); return 2; }
@@ -119,6 +149,32 @@ int main(int argc, char** argv) {
         return pts;
     };
     solver.set_pins(pin_idx, pins_at(0));
+    // (plinkohit.cpp:81-96, plinkopony.cpp:54-117: add_obstacle + set_collisions with the node
+    // positions; windyflag.cpp:104-127: WindForce on the cloth's faces)
+#ifdef REF_VARIANT_H
+    for (const Obs& o : obstacles) {
+        typedef admm::Solver::Vec3 V3;
+        std::shared_ptr<admm::PassiveCollision> obj;
+        if (o.type == 0) obj = std::make_shared<admm::Floor>(o.p[0]);
+        else if (o.type == 1) obj = std::make_shared<admm::SlideFloor>(V3(o.p[0], o.p[1], o.p[2]), V3(o.p[3], o.p[4], o.p[5]));
+        else if (o.type == 2) obj = std::make_shared<admm::Sphere>(V3(o.p[0], o.p[1], o.p[2]), o.p[3]);
+        else if (o.type == 3) obj = std::make_shared<admm::PlaneAndHalfSphere>(V3(o.p[0], o.p[1], o.p[2]), o.p[3]);
+        else obj = std::make_shared<admm::Cylinder>(V3(o.p[0], o.p[1], o.p[2]), o.p[3]);
+        solver.add_obstacle(obj);
+    }
+    if (!coll.empty()) {
+        std::vector<admm::Solver::Vec3> pts;
+        for (int i : coll) pts.push_back(admm::Solver::Vec3(x[3 * (size_t)i], x[3 * (size_t)i + 1], x[3 * (size_t)i + 2]));
+        solver.set_collisions(coll, pts);
+    }
+#else
+    if (!obstacles.empty() || !coll.empty()) { fprintf(stderr, "obstacles / collisions: H variant only\n"); return 2; }
+#endif
+    for (auto& w : winds) {
+        auto wf = std::make_shared<admm::WindForce>(w.first);
+        wf->direction = Eigen::Vector3d(w.second[0], w.second[1], w.second[2]);
+        solver.ext_forces.push_back(wf);
+    }
 
     admm::Solver::Settings st;
     st.timestep_s = dt;

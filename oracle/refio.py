@@ -36,6 +36,27 @@ def write_scene(scene: Scene, path: str) -> None:
         f.write(np.ascontiguousarray(scene.pin_vel, dtype="<f8").tobytes())
         f.write(struct.pack("<dddiiii", scene.dt, scene.gravity, scene.penalty, scene.iters, scene.accel,
                             scene.aa_m, scene.n_steps))
+        obs = getattr(scene, "obstacles", [])
+        coll = getattr(scene, "collision_idx", None)
+        winds = getattr(scene, "winds", [])
+        if obs or coll is not None or winds:
+            f.write(b"AAEXTRA1")
+            f.write(struct.pack("<i", len(obs)))
+            for kind, prm in obs:
+                p = np.zeros(8)
+                q = np.asarray(prm, np.float64).reshape(-1)
+                p[:len(q)] = q
+                f.write(struct.pack("<i", kind))
+                f.write(p.astype("<f8").tobytes())
+            c = np.zeros(0, np.int32) if coll is None else np.asarray(coll, np.int32).reshape(-1)
+            f.write(struct.pack("<i", len(c)))
+            f.write(c.astype("<i4").tobytes())
+            f.write(struct.pack("<i", len(winds)))
+            for tris, d in winds:
+                t = np.asarray(tris, np.int32).reshape(-1, 3)
+                f.write(struct.pack("<i", len(t)))
+                f.write(t.astype("<i4").tobytes())
+                f.write(np.asarray(d, np.float64).reshape(3).astype("<f8").tobytes())
 
 
 def read_ref_result(path: str, n_nodes: int):

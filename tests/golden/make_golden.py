@@ -47,7 +47,45 @@ def cases():
                                       penalty=4.0),
         # C4 recipe at small size: NeoHookean block free fall from a squashed pose (rest != initial)
         "drop6_z_nh_aa6": S.tet_drop(6, 2, 3, iters=40, n_steps=2),
+        # collision terms + obstacles (the plinko samples' horse759 mesh) and wind (windyflag)
+        "plinkohit_ux_noaa": S.plinko_hit(*horse(), n_steps=20),
+        "plinkohit_ux_aa2": S.plinko_hit(*horse(), n_steps=16, accel=1, aa_m=2),
+        "obstacles_ux_aa5": S.obstacle_course(*horse()),
+        "windycloth12_ux_aa6": S.windy_cloth(12, 12),
+        "windycloth12_z_noaa": _with(S.windy_cloth(12, 12, accel=0, iters=30), variant=S.VARIANT_X),
     }
+
+
+HORSE = "/root/reference/admm_anderson_hard_zxu/samples/data/horse759"
+
+
+def horse():
+    """The plinko samples' tet mesh (samples/data/horse759.{ele,node}, read with the
+    load_elenode restatement) -- kept as input data in mesh_horse759.npz, so the GPU tests do
+    not need the reference tree. The same file pins the loader and binding::add_tetmesh's
+    masses: the node coordinates as parsed (float64), and the reference's own mcl loader +
+    apply_xform + TetMesh::weighted_masses output (oracle/_ref/ref_tetmesh) for the plinkohit
+    transform."""
+    path = os.path.join(HERE, "mesh_horse759.npz")
+    if os.path.exists(HORSE + ".ele"):
+        v, t = scenes.load_elenode(HORSE)
+        with open(HORSE + ".node") as f:
+            rows = [ln.split() for ln in f if ln.split() and not ln.lstrip().startswith("#")][1:]
+        nodes64 = np.array([[float(r[1]), float(r[2]), float(r[3])] for r in rows[:len(v)]], np.float64)
+        xf = np.array([13.0, 13.0, 13.0, 0.25, -1.0, 0.0])
+        with tempfile.TemporaryDirectory() as tmp:
+            out = os.path.join(tmp, "m.bin")
+            subprocess.run([os.path.join(REF, "ref_tetmesh"), HORSE] + [repr(float(a)) for a in xf] + [out], check=True)
+            d = open(out, "rb").read()
+        nv, nt = np.frombuffer(d, "<i4", 2)
+        o = 8
+        rv = np.frombuffer(d, "<f4", nv * 3, o).reshape(-1, 3); o += nv * 12
+        rt = np.frombuffer(d, "<i4", nt * 4, o).reshape(-1, 4); o += nt * 16
+        rm = np.frombuffer(d, "<f4", nv, o)
+        np.savez_compressed(path, verts=v, tets=t, nodes64=nodes64, xform=xf, ref_verts_xf=rv, ref_tets=rt,
+                            ref_masses_xf=rm)
+    d = np.load(path)
+    return d["verts"], d["tets"]
 
 
 def _with(scene, **kw):
@@ -61,7 +99,10 @@ def run_ref(scene, tmp):
     path_out = os.path.join(tmp, "out.bin")
     refio.write_scene(scene, path_in)
     drv = os.path.join(REF, "ref_elastic_h" if scene.variant == scenes.VARIANT_H else "ref_elastic_x")
-    r = subprocess.run([drv, path_in, path_out], cwd=tmp, capture_output=True, text=True)
+    env = dict(os.environ)
+    if getattr(scene, "winds", None):   # WindForce::project updates v in place inside an OpenMP loop:
+        env["OMP_NUM_THREADS"] = "1"     # one thread = its sequential (reproducible) order
+    r = subprocess.run([drv, path_in, path_out], cwd=tmp, capture_output=True, text=True, env=env)
     if r.returncode != 0:
         raise RuntimeError(r.stderr)
     return refio.read_ref_result(path_out, scene.n_nodes)

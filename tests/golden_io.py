@@ -31,6 +31,19 @@ def save_case(path, sc, steps):
         d[f"g{i}_idx"] = g.idx
     if sc.rest is not None:
         d["rest"] = sc.rest
+    obs = getattr(sc, "obstacles", [])
+    if obs:
+        o = np.zeros((len(obs), 9))
+        for k, (kind, prm) in enumerate(obs):
+            q = np.asarray(prm, np.float64).reshape(-1)
+            o[k, 0] = kind
+            o[k, 1:1 + len(q)] = q
+        d["obstacles"] = o
+    if getattr(sc, "collision_idx", None) is not None:
+        d["collision_idx"] = np.asarray(sc.collision_idx, np.int32)
+    for k, (tris, direction) in enumerate(getattr(sc, "winds", [])):
+        d[f"wind{k}_tris"] = np.asarray(tris, np.int32)
+        d[f"wind{k}_dir"] = np.asarray(direction, np.float64)
     np.savez_compressed(path, **d)
 
 
@@ -45,6 +58,14 @@ def load_case(name):
                       gravity=float(st[2]), penalty=float(st[3]), iters=int(st[4]), accel=int(st[5]),
                       aa_m=int(st[6]), n_steps=int(st[7]), name=name,
                       rest=d["rest"] if "rest" in d.files else None)
+    if "obstacles" in d.files:
+        sc.obstacles = [(int(r[0]), r[1:].copy()) for r in d["obstacles"]]
+    if "collision_idx" in d.files:
+        sc.collision_idx = d["collision_idx"].astype(np.int32)
+    k = 0
+    while f"wind{k}_tris" in d.files:
+        sc.winds.append((d[f"wind{k}_tris"].astype(np.int32), d[f"wind{k}_dir"]))
+        k += 1
     steps, o = [], 0
     for k, n in enumerate(d["nrec"]):
         steps.append(dict(prim=d["prim"][o:o + n], comb=d["comb"][o:o + n], reject=d["reject"][o:o + n],
@@ -53,10 +74,21 @@ def load_case(name):
     return sc, steps
 
 
-def case_names():
-    return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and f not in ("elements.npz", "geom_elements.npz")
-                  and not f.startswith(("geom_", "full_")))
+def case_names(extras=True):
+    """Elastic trajectory fixtures; extras=False leaves out the scenes with obstacles, collision
+    terms or wind (the oracle restates the core path only; those are pinned to the reference's
+    own outputs directly)."""
+    names = sorted(f[:-4] for f in os.listdir(GOLDEN)
+                   if f.endswith(".npz") and f not in ("elements.npz", "geom_elements.npz")
+                   and not f.startswith(("geom_", "full_", "mesh_")))
+    if extras:
+        return names
+    out = []
+    for n in names:
+        with np.load(os.path.join(GOLDEN, n + ".npz")) as d:
+            if not any(k in d.files for k in ("obstacles", "collision_idx", "wind0_tris")):
+                out.append(n)
+    return out
 
 
 # ---------------------------------------------------------------------------- Geometry (ALM)

@@ -13,7 +13,7 @@ def tolerances(name):
     return (1e-6, 1e-6) if hyper else (1e-9, 1e-9)
 
 
-@pytest.mark.parametrize("name", case_names())
+@pytest.mark.parametrize("name", case_names(extras=False))
 def test_oracle_matches_reference_trajectory(name, oracle):
     sc, ref = load_case(name)
     got = oracle.run_elastic(sc)
