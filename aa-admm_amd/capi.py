@@ -263,6 +263,18 @@ class Solver:
 
     def initialize(self, settings: Settings):
         _chk(lib().aa_elastic_initialize(self.h, C.byref(settings)))
+        self.settings = settings
+
+    def save(self, result_dir="./result"):
+        """Solver::save() (Solver.hpp:130-155): result_dir/residual-<m>.txt (residual-no.txt
+        without acceleration), one row per iteration of the last step -- time (ms since the step
+        started, device clock), prim, comb and, for the (u,x) variant (admm_anderson_hard_zxu),
+        the reject flag; numbers as `ofs << setprecision(16)` writes them (%.16g)."""
+        st = self.settings
+        h = self.history()
+        t = self.times()
+        rej = h["reject"] if st.variant == AA_VARIANT_UX else None
+        return write_residual_file(result_dir, st.anderson_m if st.acceleration_type else 0, t, h["prim"], h["comb"], rej)
 
     def step(self):
         _chk(lib().aa_elastic_step(self.h))
@@ -383,6 +395,20 @@ def run_scene(ctx: Context, scene, n_steps=None, comm=None):
 # Geometry: ALMGeometrySolver<3> (Geometry/ALMGeometrySolver.h)
 # ------------------------------------------------------------------------------------------
 
+def write_residual_file(result_dir, anderson_m, *cols):
+    """The residual-<m>.txt / residual-no.txt writer shared by Solver.save and GeomSolver.save:
+    tab-separated columns, floats as %.16g (C++ setprecision(16), default float format), ints
+    as %d; a None column is left out."""
+    cols = [c for c in cols if c is not None]
+    n = min(len(c) for c in cols)
+    path = os.path.join(result_dir, f"residual-{anderson_m}.txt" if anderson_m > 0 else "residual-no.txt")
+    with open(path, "w") as f:
+        for i in range(n):
+            f.write("\t".join(("%d" % c[i]) if np.issubdtype(np.asarray(c).dtype, np.integer) else ("%.16g" % c[i])
+                              for c in cols) + "\n")
+    return path
+
+
 class GeomRuntime(C.Structure):
     _fields_ = [("setup_ms", C.c_double), ("factor_ms", C.c_double), ("solve_ms", C.c_double),
                 ("iterations", C.c_int), ("accepted", C.c_int), ("rejects", C.c_int), ("n_points", C.c_int),
@@ -465,6 +491,12 @@ class GeomSolver:
         c, t = np.zeros(max(k, 1)), np.zeros(max(k, 1))
         _chk(lib().aa_geom_get_history(self.h, _dp(c), _dp(t), C.c_int(k), C.byref(n)))
         return dict(comb=c[:k].copy(), time_s=t[:k].copy())
+
+    def save(self, anderson_m, result_dir="./result"):
+        """ALMGeometrySolver::save(Anderson_m) (ALMGeometrySolver.h:343-365; GeometrySolver.h
+        likewise): "elapsed_time_ <tab> function_values_" per recorded iteration."""
+        h = self.history()
+        return write_residual_file(result_dir, anderson_m, h["time_s"], h["comb"])
 
     def runtime(self) -> GeomRuntime:
         rt = GeomRuntime()

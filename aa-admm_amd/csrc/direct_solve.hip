@@ -13,6 +13,11 @@ namespace aa {
 
 namespace {
 
+// loads per chunk of the pipelined row / column products (dot_pipe; build-time A/B knob)
+#ifndef AA_ROW_CHUNK
+#define AA_ROW_CHUNK 8
+#endif
+
 __device__ __forceinline__ bool solve_gated(const Ctrl* c, int gate_reject) {
     if (!c) return false;
     if (c->done) return true;
@@ -73,6 +78,43 @@ __device__ __forceinline__ void zero(double* a) {
     for (int k = 0; k < NR; ++k) a[k] = 0;
 }
 
+// a[m] += sum_{i < n} G[(c0 + i) * stride] * V[NR * (c0 + i) + m], i in order: a dot product
+// of one factor row (or column) with an LDS vector, software-pipelined -- chunks of C loads,
+// two chunks in flight, the loads unconditional (index clamped to the last one; the clamped
+// terms add zero) so none waits behind a branch. Same sums in the same order as the plain loop.
+template <int NR, int C>
+__device__ __forceinline__ void dot_pipe(const double* __restrict__ G, size_t stride, int c0, int n,
+                                         const double* __restrict__ V, double* a) {
+    if (n <= 0) return;
+    double ga[C], gb[C];
+    auto ld = [&](double* g, int k) {
+#pragma unroll
+        for (int q = 0; q < C; ++q) g[q] = G[(size_t)(c0 + min(k * C + q, n - 1)) * stride];
+    };
+    auto use = [&](const double* g, int k) {
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            const int i = k * C + q;
+            const bool in = i < n;
+            const double gq = in ? g[q] : 0.0;
+            const double* v = V + NR * (c0 + (in ? i : n - 1));
+#pragma unroll
+            for (int m = 0; m < NR; ++m) a[m] += gq * v[m];
+        }
+    };
+    const int nch = (n + C - 1) / C;
+    ld(ga, 0);
+    if (nch > 1) ld(gb, 1);
+    for (int k = 0; k < nch; k += 2) {
+        use(ga, k);
+        if (k + 2 < nch) ld(ga, k + 2);
+        if (k + 1 < nch) {
+            use(gb, k + 1);
+            if (k + 3 < nch) ld(gb, k + 3);
+        }
+    }
+}
+
 // front row q of a supernode (any record with beg, p, ell_w, ell_off): [b_P ; 0]_q + the
 // children's update entries landing on it (ELL pull list: ell_w offsets into U per row, -1 =
 // none; fixed order -> deterministic)
@@ -114,12 +156,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
     const int cmax = r < p ? r + 1 : p;
     double a[NR];
     zero<NR>(a);
-#pragma unroll 8
-    for (int c = 0; c < cmax; ++c) {
-        const double v = G[(size_t)c * R];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
-    }
+    dot_pipe<NR, AA_ROW_CHUNK>(G, (size_t)R, 0, cmax, f, a);
     if (r < p) {
         double* y = Y + NR * (size_t)(t.beg + r);
 #pragma unroll
@@ -169,12 +206,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
     const int ld = t.ldr;
     double a[NR];
     zero<NR>(a);
-#pragma unroll 8
-    for (int r = j; r < R; ++r) {
-        const double g = G[(size_t)r * ld];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
-    }
+    dot_pipe<NR, AA_ROW_CHUNK>(G, (size_t)ld, j, R - j, v, a);
     st_ext<NR>(X0, X1, (size_t)(t.beg + j), a);
 }
 
@@ -185,10 +217,14 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
 // 128 x NR partial per tile; the last tile of a column block to finish sums the block's partials
 // in tile order (deterministic; hand-off protocol above). Gives (columns/128) x (rows/kBwdTileRows)
 // workgroups per supernode instead of one wave per column with a serial loop over all R rows.
+// minimum waves per SIMD the split-K tiles' register budget is set for (build-time A/B knob)
+#ifndef AA_TILE_MINW
+#define AA_TILE_MINW 1
+#endif
 using BTile = DirectSolver::BTile;
 using BRed = DirectSolver::BRed;
-template <int NR, int kBwdPrefetch, int kBwdTileRows>
-__global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tiles, int first, const double* __restrict__ Gr,
+template <int NR, int CH, int kBwdTileRows>
+__global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_tile(const BTile* __restrict__ tiles, int first, const double* __restrict__ Gr,
                                                   const int* __restrict__ bnd, const double* __restrict__ Y,
                                                   double* __restrict__ X0, double* __restrict__ X1,
                                                   double* __restrict__ part, const BRed* __restrict__ reds,
@@ -202,42 +238,51 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
     const int lane = tid & 63, w = tid >> 6;
     const int c = t.c0 + 2 * lane;   // columns c, c+1 (c+1 may be the zero pad column)
     constexpr int per = kBwdTileRows / 4;
-    constexpr int kPf = kBwdPrefetch < per ? kBwdPrefetch : per;
-    const int i0 = w * per, i1 = min(i0 + per, t.nr);
-    // the first kPf rows of this lane's G slice are loaded before the vector slice is
-    // staged, so their latency overlaps the gathers of bwd_row and the barrier
-    const double2* G = reinterpret_cast<const double2*>(Gr + t.goff + (size_t)t.r0 * t.ldr + c);
+    constexpr int C = CH < per ? CH : per;
+    constexpr int NC = per / C;
+    const int i0 = w * per;
+    const int nloc = min(per, t.nr - i0);   // rows of this wave's slice (<= 0: none)
+    const bool live = c < t.p && nloc > 0;
+    // software pipeline over chunks of C rows, two chunks in flight: the first two are issued
+    // before the vector slice is staged (their latency overlaps the gathers and the barrier),
+    // chunk k + 2 right after chunk k is consumed. Loads are unconditional (row index clamped to
+    // the slice; the extra rows count zero), so no load waits behind a branch.
+    const double2* G = reinterpret_cast<const double2*>(Gr + t.goff + (size_t)(t.r0 + i0) * t.ldr + (live ? c : 0));
     const int ld2 = t.ldr / 2;
-    double2 gp[kPf > 0 ? kPf : 1];
-    if (c < t.p) {
+    double2 ga[C], gb[C];
+    auto ld = [&](double2* g, int k) {
 #pragma unroll
-        for (int q = 0; q < kPf; ++q)
-            if (i0 + q < i1) gp[q] = G[(size_t)(i0 + q) * ld2];
+        for (int q = 0; q < C; ++q) g[q] = G[(size_t)min(k * C + q, nloc - 1) * ld2];
+    };
+    if (live) {
+        ld(ga, 0);
+        if (NC > 1) ld(gb, 1);
     }
-    for (int i = tid; i < t.nr; i += 256) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
+    for (int i = tid; i < kBwdTileRows; i += 256) {
+        if (i < t.nr) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
+        else zero<NR>(v + NR * i);   // rows past the tile: finite zeros (their G entries are zeroed too)
+    }
     __syncthreads();
     double a[W];
     zero<W>(a);
-    if (c < t.p) {
+    if (live) {
+        auto use = [&](const double2* g, int k) {
 #pragma unroll
-        for (int q = 0; q < kPf; ++q) {
-            if (i0 + q >= i1) break;
+            for (int q = 0; q < C; ++q) {
+                const int i = k * C + q;
+                const double2 gq = i < nloc ? g[q] : make_double2(0.0, 0.0);
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const double vk = v[NR * (i0 + q) + k];
-                a[k] += gp[q].x * vk;
-                a[NR + k] += gp[q].y * vk;
+                for (int m = 0; m < NR; ++m) {
+                    const double vk = v[NR * (i0 + i) + m];
+                    a[m] += gq.x * vk;
+                    a[NR + m] += gq.y * vk;
+                }
             }
-        }
-#pragma unroll 8
-        for (int i = i0 + kPf; i < i1; ++i) {
-            const double2 g = G[(size_t)i * ld2];
+        };
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const double vk = v[NR * i + k];
-                a[k] += g.x * vk;
-                a[NR + k] += g.y * vk;
-            }
+        for (int k = 0; k < NC; ++k) {
+            if (k & 1) { use(gb, k); if (k + 2 < NC) ld(gb, k + 2); }
+            else       { use(ga, k); if (k + 2 < NC) ld(ga, k + 2); }
         }
     }
     if (w > 0)
@@ -278,8 +323,8 @@ __global__ __launch_bounds__(256) void k_bwd_tile(const BTile* __restrict__ tile
 // u = f_B - M f_P.
 using FTile = DirectSolver::FTile;
 using FRed = DirectSolver::FRed;
-template <int NR, int kFwdPrefetch, int kFwdTileCols>
-__global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tiles, int first, const double* __restrict__ Gc,
+template <int NR, int CH, int kFwdTileCols>
+__global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __restrict__ tiles, int first, const double* __restrict__ Gc,
                                                   const long long* __restrict__ ell, const double* __restrict__ B0,
                                                   const double* __restrict__ B1, double* __restrict__ part,
                                                   const FRed* __restrict__ reds, int* __restrict__ cnt,
@@ -293,34 +338,45 @@ __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tile
     const int lane = tid & 63, w = tid >> 6;
     const int r = t.r0 + lane;
     constexpr int per = kFwdTileCols / 4;
-    constexpr int kPf = kFwdPrefetch < per ? kFwdPrefetch : per;
-    const int i0 = w * per, i1 = min(i0 + per, t.nc);
-    // the first kPf columns of this lane's G slice are loaded before the front slice is
-    // assembled, so their latency overlaps the extend-add gathers and the barrier
-    const double* G = Gc + t.goff + (size_t)t.c0 * t.R + r;
-    double gp[kPf > 0 ? kPf : 1];
-    if (r < t.R) {
+    constexpr int C = CH < per ? CH : per;
+    constexpr int NC = per / C;
+    const int i0 = w * per;
+    const int nloc = min(per, t.nc - i0);   // columns of this wave's slice (<= 0: none)
+    const bool live = r < t.R && nloc > 0;
+    // software pipeline over chunks of C columns, two chunks in flight (see k_bwd_tile); the
+    // first two overlap the extend-add gathers that assemble the front slice
+    const double* G = Gc + t.goff + (size_t)(t.c0 + i0) * t.R + (live ? r : 0);
+    double ga[C], gb[C];
+    auto ld = [&](double* g, int k) {
 #pragma unroll
-        for (int q = 0; q < kPf; ++q)
-            if (i0 + q < i1) gp[q] = G[(size_t)(i0 + q) * t.R];
+        for (int q = 0; q < C; ++q) g[q] = G[(size_t)min(k * C + q, nloc - 1) * t.R];
+    };
+    if (live) {
+        ld(ga, 0);
+        if (NC > 1) ld(gb, 1);
     }
     // this tile's slice of the front f_P = b_P + extend-add of the children's update vectors
-    for (int i = tid; i < t.nc; i += 256) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i);
+    for (int i = tid; i < kFwdTileCols; i += 256) {
+        if (i < t.nc) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i);
+        else zero<NR>(f + NR * i);   // columns past the tile: finite zeros
+    }
     __syncthreads();
     double a[NR];
     zero<NR>(a);
-    if (r < t.R) {
+    if (live) {
+        auto use = [&](const double* g, int k) {
 #pragma unroll
-        for (int q = 0; q < kPf; ++q) {
-            if (i0 + q >= i1) break;
+            for (int q = 0; q < C; ++q) {
+                const int i = k * C + q;
+                const double gq = i < nloc ? g[q] : 0.0;
 #pragma unroll
-            for (int k = 0; k < NR; ++k) a[k] += gp[q] * f[NR * (i0 + q) + k];
-        }
-#pragma unroll 8
-        for (int i = i0 + kPf; i < i1; ++i) {
-            const double g = G[(size_t)i * t.R];
+                for (int m = 0; m < NR; ++m) a[m] += gq * f[NR * (i0 + i) + m];
+            }
+        };
 #pragma unroll
-            for (int k = 0; k < NR; ++k) a[k] += g * f[NR * i + k];
+        for (int k = 0; k < NC; ++k) {
+            if (k & 1) { use(gb, k); if (k + 2 < NC) ld(gb, k + 2); }
+            else       { use(ga, k); if (k + 2 < NC) ld(ga, k + 2); }
         }
     }
     if (w > 0)
@@ -363,6 +419,37 @@ __global__ __launch_bounds__(256) void k_fwd_tile(const FTile* __restrict__ tile
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// partitioned dense top: this GPU's share of the top front f_T = b_T + its own children's
+// update vectors (thread per row), written set-major [set][3 * p] for the all-reduce
+template <int NR>
+__global__ __launch_bounds__(256) void k_top_front(const Task* __restrict__ top, const long long* __restrict__ ell,
+                                                   const double* __restrict__ B0, const double* __restrict__ B1,
+                                                   const double* __restrict__ U, double* __restrict__ F,
+                                                   const Ctrl* ctrl, int gate_reject) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    const Task t = *top;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= t.p) return;
+    double a[NR];
+    front_row<NR>(t, q, ell, B0, B1, U, a);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) F[(size_t)(k / 3) * 3 * t.p + 3 * (size_t)q + k % 3] = a[k];
+}
+// ... and the summed x_top (set-major) back into the caller's x rows
+template <int NR>
+__global__ __launch_bounds__(256) void k_top_scatter(const Task* __restrict__ top, const double* __restrict__ X,
+                                                     double* __restrict__ X0, double* __restrict__ X1, const Ctrl* ctrl,
+                                                     int gate_reject) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    const Task t = *top;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= t.p) return;
+    double a[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) a[k] = X[(size_t)(k / 3) * 3 * t.p + 3 * (size_t)q + k % 3];
+    st_ext<NR>(X0, X1, (size_t)(t.beg + q), a);
+}
+
 using SubNode = DirectSolver::SubNode;
 using SubLevel = DirectSolver::SubLevel;
 using SubTree = DirectSolver::SubTree;
@@ -398,12 +485,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             const int cmax = r < p ? r + 1 : p;
             double a[NR];
             zero<NR>(a);
-#pragma unroll 8
-            for (int c = 0; c < cmax; ++c) {
-                const double v = G[(size_t)c * R];
-#pragma unroll
-                for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
-            }
+            dot_pipe<NR, AA_ROW_CHUNK>(G, (size_t)R, 0, cmax, f, a);
             if (r < p) {
                 double* y = Y + NR * (size_t)(nd.beg + r);
 #pragma unroll
@@ -463,12 +545,8 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             const int r1 = min(R, (seg + 1) * kSubSegRows);
             double a[NR];
             zero<NR>(a);
-#pragma unroll 8
-            for (int r = max(j, seg * kSubSegRows); r < r1; ++r) {
-                const double g = G[(size_t)r * ld];
-#pragma unroll
-                for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
-            }
+            const int rs = max(j, seg * kSubSegRows);
+            dot_pipe<NR, AA_ROW_CHUNK>(G, (size_t)ld, rs, r1 - rs, v, a);
             double* q = lds + K * nd.slot + NR * (sub_seg_off(seg, p) + j);
 #pragma unroll
             for (int k = 0; k < NR; ++k) q[k] = a[k];
@@ -759,6 +837,20 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 if (fused[sn]) { by += 8.0 * (0.5 * p[sn] * (p[sn] + 1.0) + (double)p[sn] * nb[sn]); ++nsn; }
             std::fprintf(stderr, "[solve] fused subtrees: %d (cut height %d), %d supernodes, %.2f MB/sweep, lds f %d b %d\n",
                          n_sub_, cut_height_, nsn, by / 1e6, sub_lds_f_, sub_lds_b_);
+            // per height inside the subtrees: supernodes, rows, the longest forward row loop (p)
+            // and bytes -- a level's time is bounded below by its longest serial loop
+            for (int h = 0; h <= cut_height_; ++h) {
+                long long cnt = 0, rows = 0, maxp = 0, maxR = 0;
+                double bh = 0;
+                for (int sn = 0; sn < nn_; ++sn) {
+                    if (!fused[sn] || F.height[sn] != h) continue;
+                    ++cnt; rows += p[sn] + nb[sn];
+                    maxp = std::max<long long>(maxp, p[sn]); maxR = std::max<long long>(maxR, p[sn] + nb[sn]);
+                    bh += 8.0 * (0.5 * p[sn] * (p[sn] + 1.0) + (double)p[sn] * nb[sn]);
+                }
+                std::fprintf(stderr, "[solve]   sub height %d: %lld supernodes, %.1f rows/subtree, max p %lld, max R %lld, %.2f MB\n",
+                             h, cnt, n_sub_ ? (double)rows / n_sub_ : 0.0, maxp, maxR, bh / 1e6);
+            }
         }
         sub_nodes_.upload(snodes, s);
         sub_levels_.upload(slevels, s);
@@ -767,8 +859,19 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         sub_items2_.upload(items2, s);
     }
     // levels by height and their row tasks
+    // partitioned: the shared top as ONE dense root supernode (nested_dissection merge_top) is
+    // split over the GPUs by rows instead of being solved whole on each
+    top_sn_ = -1;
+    if (comm_) {
+        int ntop = 0, cand = -1;
+        for (int sn = 0; sn < nn_; ++sn)
+            if ((*node_part)[sn] == -1 && p[sn] > 0) { ++ntop; cand = sn; }
+        if (ntop == 1 && F.parent[cand] < 0 && nb[cand] == 0 && beg[cand] == top_beg_ && p[cand] == n_ - top_beg_ &&
+            !fused[cand])
+            top_sn_ = cand;
+    }
     std::vector<std::vector<int>> hl(F.max_height + 1);
-    for (int sn = 0; sn < nn_; ++sn) if (!fused[sn] && inc[sn]) hl[F.height[sn]].push_back(sn);
+    for (int sn = 0; sn < nn_; ++sn) if (!fused[sn] && inc[sn] && sn != top_sn_) hl[F.height[sn]].push_back(sn);
     std::vector<Task> tasks;
     std::vector<BTile> btiles;
     std::vector<BRed> breds;
@@ -914,6 +1017,78 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                          L.bwd_count, L.bblock, L.bt_count, L.btw);
         }
     }
+    if (top_sn_ >= 0) {
+        // rows [top_r0_, top_r1_) of the top triangle, in kTopBlk blocks, equal areas per GPU
+        const int sn = top_sn_, P = comm_->size(), me = comm_->rank(), pt = p[sn];
+        const int nblk = (pt + kTopBlk - 1) / kTopBlk;
+        const double total = 0.5 * pt * (pt + 1.0);
+        std::vector<int> cut(P + 1, nblk);
+        cut[0] = 0;
+        double acc = 0;
+        int r = 1;
+        for (int b = 0; b < nblk && r < P; ++b) {
+            const double r0 = (double)b * kTopBlk, r1 = std::min<double>(pt, r0 + kTopBlk);
+            acc += 0.5 * (r1 * (r1 + 1) - r0 * (r0 + 1));
+            while (r < P && acc >= total * r / P) cut[r++] = b + 1;
+        }
+        top_p_ = pt;
+        top_r0_ = std::min(pt, cut[me] * kTopBlk);
+        top_r1_ = std::min(pt, cut[me + 1] * kTopBlk);
+        top_task_ = mk(sn, 0, pt);
+        top_ftw_ = tw ? (std::atoi(tw) >= 256 ? 256 : (std::atoi(tw) >= 128 ? 128 : 64)) : 256;
+        top_btw_ = top_ftw_;
+        // forward tiles of the own rows (64-row blocks); the front is read summed from top_f_
+        top_ft_first_ = (int)ftiles.size();
+        for (int r0 = top_r0_; r0 < top_r1_; r0 += 64) {
+            FRed rd{};
+            rd.beg = beg[sn]; rd.p = pt; rd.r0 = r0; rd.nr = std::min(64, top_r1_ - r0);
+            rd.uoff = uoff[sn]; rd.ell_off = 0; rd.ell_w = 0; rd.poff = poff;
+            for (int c0 = 0; c0 < pt; c0 += top_ftw_) {
+                if (r0 + 63 < c0) break;
+                FTile ft{};
+                ft.beg = beg[sn]; ft.p = pt; ft.R = pt; ft.c0 = c0; ft.r0 = r0;
+                ft.nc = std::min(top_ftw_, pt - c0);
+                ft.goff = goff[sn]; ft.ell_off = 0; ft.ell_w = 0; ft.poff = poff;
+                ft.rid = (int)freds.size();
+                poff += 3 * 64;
+                ftiles.push_back(ft);
+                ++rd.nt;
+            }
+            freds.push_back(rd);
+        }
+        top_ft_count_ = (int)ftiles.size() - top_ft_first_;
+        // backward: the products of the own rows only (partial x_top, summed over the GPUs)
+        top_bt_first_ = (int)btiles.size();
+        for (int c0 = 0; c0 < top_r1_; c0 += 128) {
+            const int rs = std::max(c0, top_r0_);
+            if (rs >= top_r1_) continue;
+            BRed rd{};
+            rd.beg = beg[sn]; rd.c0 = c0; rd.nc = std::min(128, pt - c0); rd.poff = poff;
+            for (int r0 = rs; r0 < top_r1_; r0 += top_btw_) {
+                BTile bt{};
+                bt.beg = beg[sn]; bt.p = pt; bt.nb = 0; bt.bnd_off = bnd_off[sn];
+                bt.c0 = c0; bt.r0 = r0; bt.nr = std::min(top_btw_, top_r1_ - r0);
+                bt.goff = goff[sn]; bt.poff = poff; bt.ldr = ldr[sn];
+                bt.rid = (int)breds.size();
+                poff += 6 * 64;
+                btiles.push_back(bt);
+                ++rd.nt;
+            }
+            breds.push_back(rd);
+        }
+        top_bt_count_ = (int)btiles.size() - top_bt_first_;
+        kernels_ += 4;
+        // bytes: this GPU streams its row slice of the triangle (twice), not the whole top
+        const double whole = 0.5 * pt * (pt + 1.0), a0 = top_r0_, a1 = top_r1_;
+        dense -= whole;
+        dense += 0.5 * (a1 * (a1 + 1) - a0 * (a0 + 1));
+        top_task_d_.upload(std::vector<Task>{top_task_}, s);
+        top_f_.alloc(3 * (size_t)KS * pt);
+        top_x_.alloc(3 * (size_t)KS * pt);
+        if (stats)
+            std::fprintf(stderr, "[solve] dense top: %d rows, this GPU rows [%d, %d), fwd tiles %d, bwd tiles %d\n", pt,
+                         top_r0_, top_r1_, top_ft_count_, top_bt_count_);
+    }
     if (n_sub_) kernels_ += 2;
     bnd_.upload(bnd, s);
     ell_.upload(ell, s);
@@ -1000,8 +1175,37 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     // and in the update vectors); their sum over the GPUs is the full forward result. When the
     // solve is gated off the stale rows are summed too -- harmless, the next forward rewrites
     // them and the backward sweep is gated alike on every GPU.
-    if (comm_ && top_beg_ < n_)
+    if (top_sn_ >= 0) {
+        // dense top: sum the front over the GPUs, forward of the own rows, backward products of
+        // the own rows into a partial x_top, sum it, scatter it into x
+        const int pt = top_p_;
+        const unsigned nb = (unsigned)((pt + 255) / 256);
+        hipLaunchKernelGGL((k_top_front<NR>), dim3(nb), dim3(256), 0, s, top_task_d_.p, ell_.p, b0, b1, U_.p, top_f_.p,
+                           ctrl, gate_reject);
+        comm_->allreduce_sum(top_f_.p, top_f_.p, 3 * (size_t)K * pt, s);
+        // the tiles address the front / x by global row beg + q: shift the set-major buffers
+        const size_t sh = 3 * (size_t)top_task_.beg;
+        const double* F0 = top_f_.p - sh;
+        const double* F1 = top_f_.p + 3 * (size_t)pt - sh;
+        if (top_ft_count_) {
+            auto kf = top_ftw_ == 256 ? k_fwd_tile<NR, 16, 256> : (top_ftw_ == 128 ? k_fwd_tile<NR, 16, 128> : k_fwd_tile<NR, 16, 64>);
+            hipLaunchKernelGGL(kf, dim3(top_ft_count_), dim3(256), 0, s, ftiles_.p, top_ft_first_, Gc_.p, ell_.p, F0, F1,
+                               bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
+        }
+        AA_HIP(hipMemsetAsync(top_x_.p, 0, sizeof(double) * 3 * (size_t)K * pt, s));
+        double* Xs0 = top_x_.p - sh;
+        double* Xs1 = top_x_.p + 3 * (size_t)pt - sh;
+        if (top_bt_count_) {
+            auto kb = top_btw_ == 256 ? k_bwd_tile<NR, 8, 256> : (top_btw_ == 128 ? k_bwd_tile<NR, 8, 128> : k_bwd_tile<NR, 8, 64>);
+            hipLaunchKernelGGL(kb, dim3(top_bt_count_), dim3(256), 0, s, btiles_.p, top_bt_first_, Gr_.p, bnd_.p, Y_.p,
+                               Xs0, Xs1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
+        }
+        comm_->allreduce_sum(top_x_.p, top_x_.p, 3 * (size_t)K * pt, s);
+        hipLaunchKernelGGL((k_top_scatter<NR>), dim3(nb), dim3(256), 0, s, top_task_d_.p, top_x_.p, x0, x1, ctrl,
+                           gate_reject);
+    } else if (comm_ && top_beg_ < n_) {
         comm_->allreduce_sum(Y_.p + NR * (size_t)top_beg_, Y_.p + NR * (size_t)top_beg_, NR * (size_t)(n_ - top_beg_), s);
+    }
     for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
         const Level& L = *it;
 #define BWD(BL) hipLaunchKernelGGL((k_bwd<BL, NR>), dim3(L.bwd_count), dim3(BL), K * L.lds_bwd, s, T, L.bwd_first, Gr_.p, \

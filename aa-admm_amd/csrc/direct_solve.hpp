@@ -110,6 +110,16 @@ private:
     DevBuf<int> fcnt_, bcnt_;   // tiles finished per reduction task (reset by the last tile)
     DevBuf<double> bpart_;
     std::vector<Level> levels_;
+    // partitioned with a dense shared top (nested_dissection merge_top): the top root supernode
+    // top_sn_ is solved outside the levels -- its front assembled locally and summed over the
+    // GPUs, then each GPU runs the forward rows [top_r0_, top_r1_) and the backward products of
+    // those rows (a partial x_top), and one more sum gives every GPU the whole x_top.
+    static constexpr int kTopBlk = 64;   // row granularity of the split (the forward tiles' rows)
+    int top_sn_ = -1, top_p_ = 0, top_r0_ = 0, top_r1_ = 0;
+    int top_ft_first_ = 0, top_ft_count_ = 0, top_bt_first_ = 0, top_bt_count_ = 0, top_ftw_ = 256, top_btw_ = 256;
+    Task top_task_{};
+    DevBuf<Task> top_task_d_;
+    DevBuf<double> top_f_, top_x_;   // [set][3 * top_p_]: summed front, partial then summed x_top
     // fused bottom subtrees
     int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1, sub_block_ = 256;
     int wave_p_ = kWaveP, wave_r_ = kWaveR;   // row-task / split-K thresholds (AA_SOLVE_WAVEP / _WAVER)

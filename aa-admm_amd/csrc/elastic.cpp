@@ -319,15 +319,15 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     std::vector<double> coords(3 * (size_t)nf_);
     for (int k = 0; k < nf_; ++k)
         for (int j = 0; j < 3; ++j) coords[3 * k + j] = x_[3 * (size_t)free_nodes[k] + j];
-    // partitioned: the first log2(P) bisections of the nested dissection are
+    // partitioned: the top bisections of the nested dissection (P parts, any P) are
     // forced; part r (a contiguous range of free nodes) belongs to rank r, the separators of
     // those bisections (the "top") are shared by all ranks
     const int P = comm_ ? comm_->size() : 1;
-    int levels = 0;
-    while ((1 << levels) < P) ++levels;
-    if ((1 << levels) != P) throw Error(ERR_ARG, "initialize: the number of ranks must be a power of two");
+    // the shared top separators as one dense root split over the ranks (AA_TOP_DENSE=0: one
+    // supernode per separator, replicated on every rank -- the round-1 layout)
+    const bool top_dense = !(std::getenv("AA_TOP_DENSE") && std::getenv("AA_TOP_DENSE")[0] == '0');
     stamp("adjacency");
-    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, levels);
+    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, P > 1 ? P : 0, top_dense);
     stamp("nested dissection");
     node2int_.assign(n, -1);
     int2node_.assign(n, -1);

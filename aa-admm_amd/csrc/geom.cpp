@@ -357,12 +357,12 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
         }
         aptr[i + 1] = (int)aj.size();
     }
-    // partitioned: the first log2(P) bisections are forced; part r (a contiguous
+    // partitioned: the top bisections (P parts) are forced; part r (a contiguous
     // range of points) belongs to rank r, the separators ("top") are shared
     const int P = comm_ ? comm_->size() : 1;
-    int levels = 0;
-    while ((1 << levels) < P) ++levels;
-    if ((1 << levels) != P) throw Error(ERR_ARG, "solve_ADMM: the number of ranks must be a power of two");
+    // the shared top separators as one dense root split over the ranks (AA_TOP_DENSE=0: one
+    // supernode per separator, replicated on every rank -- the round-1 layout)
+    const bool top_dense = !(std::getenv("AA_TOP_DENSE") && std::getenv("AA_TOP_DENSE")[0] == '0');
     if (P > 1) {   // every rank must have been handed the same problem
         double h[4] = {(double)n_, (double)hgroups_.size(), 0, 0};
         for (auto& g : hgroups_) h[2] += (double)g.idx.size();
@@ -373,7 +373,7 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
             if (std::fabs(r[i] - P * h[i]) > 1e-12 * std::fabs(P * h[i]))
                 throw Error(ERR_ARG, "solve_ADMM: the ranks were given different problems");
     }
-    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, levels);
+    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, P > 1 ? P : 0, top_dense);
     top_beg_ = P > 1 ? tree.top_beg : n_;
     own_beg_ = P > 1 ? tree.part_beg[rank_] : 0;
     own_end_ = P > 1 ? tree.part_end[rank_] : n_;

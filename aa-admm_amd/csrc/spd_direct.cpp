@@ -28,16 +28,18 @@ struct NdBuilder {
     NdBuilder(int n_, const double* x_, const std::vector<int>& p_, const std::vector<int>& j_, int l_)
         : n(n_), xyz(x_), ap(p_), aj(j_), leaf(l_), mark(n_, 0), side(n_, 0) {}
 
-    // one bisection step: median split along the longest bounding-box axis, then the vertices of
-    // the lower half adjacent to the upper half form the (one-sided) vertex separator
-    void split(std::vector<int>& verts, std::vector<int>& left, std::vector<int>& right, std::vector<int>& sep) {
+    // one bisection step: median split (or, for an uneven part count, a split at the fraction
+    // num/den of the vertices) along the longest bounding-box axis, then the vertices of the lower
+    // side adjacent to the upper side form the (one-sided) vertex separator
+    void split(std::vector<int>& verts, std::vector<int>& left, std::vector<int>& right, std::vector<int>& sep,
+               int num = 1, int den = 2) {
         double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
         for (int v : verts)
             for (int d = 0; d < 3; ++d) { lo[d] = std::min(lo[d], xyz[3 * v + d]); hi[d] = std::max(hi[d], xyz[3 * v + d]); }
         int ax = 0;
         for (int d = 1; d < 3; ++d) if (hi[d] - lo[d] > hi[ax] - lo[ax]) ax = d;
         auto key = [&](int v) { return xyz[3 * v + ax]; };
-        const size_t half = verts.size() / 2;
+        const size_t half = den == 2 * num ? verts.size() / 2 : (size_t)((long long)verts.size() * num / den);
         std::nth_element(verts.begin(), verts.begin() + half, verts.end(), [&](int a, int b) {
             double ka = key(a), kb = key(b);
             return ka < kb || (ka == kb && a < b);
@@ -77,11 +79,12 @@ struct NdBuilder {
         return {add_node(std::move(sep), roots)};
     }
 
-    // the top `levels` bisections are forced (one part per leaf of the top, in left-to-right
-    // order); each part is then dissected by build(). part_of[node] = part id, -1 = top separator
+    // the top bisections are forced until there are `parts` parts (one per leaf of the top, in
+    // left-to-right order; an odd count is split floor(parts/2) : ceil(parts/2) by vertex count);
+    // each part is then dissected by build(). part_of[node] = part id, -1 = top separator
     std::vector<int> part_of;
-    std::vector<int> build_parts(std::vector<int> verts, int levels, int& next_part) {
-        if (levels == 0) {
+    std::vector<int> build_parts(std::vector<int> verts, int parts, int& next_part) {
+        if (parts <= 1) {
             const int id = next_part++;
             const size_t first = piv.size();
             std::vector<int> r = build(std::move(verts));
@@ -90,10 +93,11 @@ struct NdBuilder {
             return r;
         }
         std::vector<int> left, right, sep;
-        if (!verts.empty()) split(verts, left, right, sep);
+        const int pl = parts / 2, pr = parts - pl;
+        if (!verts.empty()) split(verts, left, right, sep, pl, parts);
         if (left.empty() && right.empty() && !sep.empty()) std::swap(left, sep);   // tiny: keep it in a part
-        std::vector<int> roots = build_parts(std::move(left), levels - 1, next_part);
-        std::vector<int> r2 = build_parts(std::move(right), levels - 1, next_part);
+        std::vector<int> roots = build_parts(std::move(left), pl, next_part);
+        std::vector<int> r2 = build_parts(std::move(right), pr, next_part);
         roots.insert(roots.end(), r2.begin(), r2.end());
         if (sep.empty()) return roots;
         const int s = add_node(std::move(sep), roots);
@@ -104,16 +108,37 @@ struct NdBuilder {
 }  // namespace
 
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                         int leaf_size, int top_rows, int part_levels) {
+                         int leaf_size, int top_rows, int n_parts, bool merge_top) {
     NdBuilder b(n, xyz, adj_ptr, adj, std::max(1, leaf_size));
     std::vector<int> all(n);
     std::iota(all.begin(), all.end(), 0);
     int nparts = 0;
-    std::vector<int> roots = part_levels > 0 ? b.build_parts(all, part_levels, nparts) : b.build(all);
+    const int part_levels = n_parts > 1 ? 1 : 0;   // (flag) partitioned ordering
+    std::vector<int> roots = part_levels > 0 ? b.build_parts(all, n_parts, nparts) : b.build(all);
     std::vector<std::vector<int>> piv = std::move(b.piv), kids = std::move(b.kids);
     std::vector<int> part_of = std::move(b.part_of);
     part_of.resize(piv.size(), part_levels > 0 ? -1 : 0);
     if (part_levels > 0) top_rows = 0;   // the partition roots must stay separate supernodes
+    // ---- partitioned, merge_top: all shared top separators become ONE dense root supernode
+    // (children = the parts' roots). Its two sweeps are then dense GEMVs the GPUs split by rows
+    // (DirectSolver::build) instead of a replicated level-by-level solve.
+    if (part_levels > 0 && merge_top && roots.size() == 1 && part_of[roots[0]] < 0) {
+        std::vector<int> merged, below;
+        std::function<void(int)> post = [&](int s) {   // postorder over the top separators
+            for (int c : kids[s]) {
+                if (part_of[c] < 0) post(c);
+                else below.push_back(c);
+            }
+            merged.insert(merged.end(), piv[s].begin(), piv[s].end());
+            piv[s].clear();
+            kids[s].clear();
+        };
+        post(roots[0]);
+        piv.push_back(merged);
+        kids.push_back(below);
+        part_of.push_back(-1);
+        roots = {(int)piv.size() - 1};
+    }
     // ---- amalgamate the top of the tree into one dense supernode: the upper levels have few,
     // mid-sized supernodes whose level-by-level solve is pure latency; as one dense block they
     // are a single wide GEMV per sweep.

@@ -37,11 +37,12 @@ struct NdTree {
     int top_beg = 0;
 };
 // top_rows > 0: the upper levels of the tree (up to top_rows pivots) are amalgamated into
-// one dense root supernode. part_levels = L > 0: the first L bisections are forced and give
-// 2^L parts (one per GPU of the partitioned solver); their separators form the "top" of the
-// tree (part -1) and no amalgamation is done.
+// one dense root supernode. n_parts = P > 1: the top bisections are forced until there are P
+// parts (one per GPU of the partitioned solver; any P, uneven counts split by vertex count);
+// their separators form the "top" of the tree (part -1): with merge_top one dense root
+// supernode, else one supernode per separator. No top_rows amalgamation when partitioned.
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                         int leaf_size, int top_rows = 0, int part_levels = 0);
+                         int leaf_size, int top_rows = 0, int n_parts = 0, bool merge_top = true);
 
 struct SupernodalFactor {
     int n = 0;

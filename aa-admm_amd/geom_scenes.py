@@ -310,6 +310,87 @@ def wire_from_mesh(V, faces, refV, refF, edge_length, *, iters=100, aa_m=20, pen
     return sc
 
 
+def subdivide_and_smooth(V, faces):
+    """subdivide_and_smooth_mesh (Geometry/MeshTypes.h:214-342), the pre-processing of
+    WireMeshOpt's main (WireMeshOpt.cpp:364): one subdivision step and a Laplacian smoothing.
+
+    Topology (OpenMesh's add_face order): the output vertices are the input vertices, then one
+    midpoint (p_from + p_to) * 0.5 per edge in edge-creation order, then one centroid per face
+    (sum of its vertices in face order / n). Face i of the input (v_0..v_{n-1}) yields n quads
+    [e(v_{j-1}, v_j), v_j, e(v_j, v_{j+1}), centroid] -- OpenMesh's face half-edge is the last
+    one, (v_{n-1}, v_0), so its circulation starts at v_0.
+    Smoothing: a uniform Laplacian row for every interior vertex (all neighbours) and for every
+    boundary vertex whose two boundary edges belong to different faces (its two boundary
+    neighbours); the input vertices are fixed and the others minimise |L x|^2 (the reference
+    solves (A^T A) x_free = -(A^T L) x_fixed with A = L restricted to the free columns, by
+    SimplicialLDLT -- a sparse direct solve here). Returns (V_out, faces_out)."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+
+    V = np.asarray(V, np.float64)
+    nv = len(V)
+    edges, _ = edges_of(faces)
+    eid = {(min(u, v), max(u, v)): k for k, (u, v) in enumerate(edges)}
+    ne = len(edges)
+    out = [V]
+    e = np.array(edges, np.int64).reshape(-1, 2)
+    out.append((V[e[:, 0]] + V[e[:, 1]]) * 0.5)
+    cents, newf = [], []
+    for fi, f in enumerate(faces):
+        c = np.zeros(3)
+        for v in f:
+            c = c + V[v]
+        cents.append(c / float(len(f)))
+        fv = nv + ne + fi
+        n = len(f)
+        for j in range(n):
+            a, b, cc = f[j - 1], f[j], f[(j + 1) % n]
+            newf.append([nv + eid[(min(a, b), max(a, b))], b, nv + eid[(min(b, cc), max(b, cc))], fv])
+    X = np.vstack(out + [np.array(cents).reshape(-1, 3)])
+    n_out = len(X)
+    # Laplacian rows (MeshTypes.h:264-296)
+    edges2, efaces2 = edges_of(newf)
+    nbrs = [set() for _ in range(n_out)]
+    bnd = [[] for _ in range(n_out)]   # (neighbour, face) per boundary edge
+    for (u, v), fl in zip(edges2, efaces2):
+        nbrs[u].add(v); nbrs[v].add(u)
+        if len(fl) == 1:
+            bnd[u].append((v, fl[0])); bnd[v].append((u, fl[0]))
+    rows, cols, vals = [], [], []
+    r = 0
+    for v in range(n_out):
+        if bnd[v]:
+            if len(bnd[v]) == 2 and bnd[v][0][1] != bnd[v][1][1]:
+                lap = [v] + [w for w, _ in bnd[v]]
+            else:
+                continue
+        else:
+            lap = [v] + sorted(nbrs[v])
+        k = len(lap)
+        rows += [r] * k; cols += lap; vals += [1.0] + [-1.0 / float(k - 1)] * (k - 1)
+        r += 1
+    L = sp.csr_matrix((vals, (rows, cols)), shape=(r, n_out))
+    fixed = np.zeros((n_out, 3))
+    fixed[:nv] = V
+    free = np.arange(nv, n_out)
+    A = L[:, free]
+    M = (A.T @ A).tocsc()
+    rhs = -(A.T @ L) @ fixed
+    sol = np.column_stack([spla.spsolve(M, rhs[:, d]) for d in range(3)]) if len(free) else np.zeros((0, 3))
+    X = fixed.copy()
+    X[free] = sol
+    return X, newf
+
+
+def wire_from_polymesh(V, faces, refV, refF, **kw) -> GeomScene:
+    """WireMeshOpt's main (Geometry/WireMeshOpt.cpp:341-391) from a polygon mesh: target edge
+    length = half the input's average edge length, the mesh subdivided and smoothed
+    (subdivide_and_smooth), then the optimize_mesh recipe (wire_from_mesh)."""
+    L = 0.5 * average_edge_length(np.asarray(V, np.float64), faces)
+    SV, SF = subdivide_and_smooth(V, faces)
+    return wire_from_mesh(SV, SF, refV, refF, L, **kw)
+
+
 def wire_grid(nx=707, ny=707, *, iters=100, aa_m=20, shear=1.2, ref_factor=2, **kw) -> GeomScene:
     """configs[4]: wire-mesh optimisation of a sheared height-field quad grid (501 264 points
     at 707 x 707). The in-plane shear drives corner angles below 45 degrees over part of the

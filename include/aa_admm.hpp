@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdio>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -255,6 +256,35 @@ public:
         check(aa_elastic_get_v(h_, m_v.data()));
         x_seen_ = m_x;
         v_seen_ = m_v;
+        save(true);
+    }
+
+    // Solver::save() (Solver.hpp:130-155, called at the end of every step, Solver.cpp:232/262):
+    // ./result/residual-<m>.txt (or residual-no.txt) with one row per iteration of the last step:
+    // time (ms since the step started; device clock), prim, comb and -- (u,x) variant
+    // (admm_anderson_hard_zxu) only -- the reject flag, %.16g as `ofs << setprecision(16)`.
+    // quiet: skip silently when ./result does not exist (the reference prints "Cannot open").
+    bool save(bool quiet = false) const {
+        const std::string file = settings_.acceleration_type ? "./result/residual-" + std::to_string(settings_.Anderson_m) + ".txt"
+                                                             : std::string("./result/residual-no.txt");
+        std::FILE* f = std::fopen(file.c_str(), "w");
+        if (!f) {
+            if (!quiet) std::printf("Cannot open: %s\n", file.c_str());
+            return false;
+        }
+        std::vector<double> prim, comb, t;
+        std::vector<int> rej;
+        const int n = history(prim, comb, rej);
+        int nt = 0;
+        check(aa_elastic_get_times(h_, nullptr, 0, &nt));
+        t.assign(std::max(n, nt), 0.0);
+        if (nt) check(aa_elastic_get_times(h_, t.data(), nt, &nt));
+        for (int i = 0; i < n; ++i) {
+            if (settings_.variant == AA_VARIANT_UX) std::fprintf(f, "%.16g\t%.16g\t%.16g\t%d\n", t[i], prim[i], comb[i], rej[i]);
+            else std::fprintf(f, "%.16g\t%.16g\t%.16g\n", t[i], prim[i], comb[i]);
+        }
+        std::fclose(f);
+        return true;
     }
 
     const Settings& settings() const { return settings_; }

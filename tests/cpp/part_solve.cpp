@@ -2,14 +2,22 @@
 //
 // Builds an SPD matrix with the structure of the elastic global matrix A_s (lumped mass +
 // dt^2 * tet-mesh stiffness pattern) on a structured block, orders it by nested dissection
-// with the first L bisections forced (2^L parts), factors it once, and then runs the solve the
-// way P GPUs do: each "rank" (a thread here) forward-sweeps its own part plus the shared top
-// separators on a PARTIAL right-hand side (own rows complete, top rows split between the
-// ranks arbitrarily), the top rows of the forward results are summed (the all-reduce), and
-// each rank back-substitutes the top and its own part. The assembled solution must match the
-// unpartitioned solve and A x = b.
+// with the top bisections forced (P parts, P = 1, 2, 3, 4, 8), factors it once, and then runs
+// the solve the way P GPUs do, on a PARTIAL right-hand side (own rows complete, top rows split
+// between the ranks arbitrarily), each "rank" a thread:
+//  * separate top separators (merge_top = false, the round-1 layout): each rank forward-sweeps
+//    its own part plus the top, the top rows of the forward results are summed (the
+//    all-reduce), and each rank back-substitutes the top and its own part;
+//  * one dense top root (merge_top = true, DirectSolver's default): each rank forward-sweeps its
+//    own part, the top front is summed, each rank computes its row slice of y_top = Linv f_top
+//    (equal triangle areas in blocks of kBlk rows, as DirectSolver::build) and the backward
+//    products of those rows (a partial x_top), x_top is summed, each rank back-substitutes its
+//    own part.
+// The assembled solution must match the unpartitioned solve and A x = b.
 //   g++ -O2 -std=c++17 -fopenmp tests/cpp/part_solve.cpp aa-admm_amd/csrc/spd_direct.cpp
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstdio>
 #include <mutex>
@@ -23,20 +31,89 @@ namespace {
 
 struct SumBarrier {   // all-reduce (sum) of equal-length vectors across P threads
     int P, arrived = 0, gen = 0;
-    std::vector<double> acc;
+    std::vector<double> acc[2];   // by generation parity: a thread already in the next reduce
+                                  // must not clear the sum the others are still copying out
     std::mutex mu;
     std::condition_variable cv;
     explicit SumBarrier(int p) : P(p) {}
     void reduce(double* v, size_t n) {
         std::unique_lock<std::mutex> lk(mu);
-        if (arrived == 0) acc.assign(n, 0.0);
-        for (size_t i = 0; i < n; ++i) acc[i] += v[i];   // order of arrival differs: compare to tolerance
         const int g = gen;
+        std::vector<double>& a = acc[g & 1];
+        if (arrived == 0) a.assign(n, 0.0);
+        for (size_t i = 0; i < n; ++i) a[i] += v[i];   // order of arrival differs: compare to tolerance
         if (++arrived == P) { arrived = 0; ++gen; cv.notify_all(); }
         else cv.wait(lk, [&] { return gen != g; });
-        for (size_t i = 0; i < n; ++i) v[i] = acc[i];
+        for (size_t i = 0; i < n; ++i) v[i] = a[i];
     }
 };
+
+// restatement of DirectSolver's dense-top partitioned solve (direct_solve.hip, solve_nr)
+constexpr int kBlk = 8;   // row block of the split (DirectSolver: kFwdRows = 128; small here so every rank gets rows)
+void solve_dense_top(const aa::SupernodalFactor& F, const aa::NdTree& T, int part, int P, std::vector<double>& b,
+                     SumBarrier& bar) {
+    const int nn = F.n_nodes;
+    int top = -1;
+    for (int s = 0; s < nn; ++s)
+        if (T.part[s] == -1 && F.end[s] > F.beg[s]) { if (top >= 0) std::abort(); top = s; }
+    if (top < 0 || F.parent[top] >= 0 || !F.bnd[top].empty()) std::abort();
+    auto own = [&](int s) { return T.part[s] == part; };
+    std::vector<double> t;
+    for (int s = 0; s < nn; ++s) {   // forward over the own part
+        if (!own(s)) continue;
+        const int b0 = F.beg[s], p = F.end[s] - b0, nb = (int)F.bnd[s].size();
+        t.assign((size_t)p * 3, 0.0);
+        for (int i = 0; i < p; ++i)
+            for (int k = 0; k <= i; ++k)
+                for (int c = 0; c < 3; ++c) t[3 * i + c] += F.Linv[s][(size_t)i * p + k] * b[3 * (size_t)(b0 + k) + c];
+        for (int i = 0; i < p; ++i) for (int c = 0; c < 3; ++c) b[3 * (size_t)(b0 + i) + c] = t[3 * i + c];
+        for (int a = 0; a < nb; ++a)
+            for (int j = 0; j < p; ++j)
+                for (int c = 0; c < 3; ++c) b[3 * (size_t)F.bnd[s][a] + c] -= F.LBP[s][(size_t)a * p + j] * t[3 * j + c];
+    }
+    const int tb = F.beg[top], pt = F.end[top] - tb;
+    double* f = b.data() + 3 * (size_t)tb;
+    bar.reduce(f, 3 * (size_t)pt);   // the summed top front
+    // this rank's rows: equal triangle areas in kBlk-row blocks
+    const int nblk = (pt + kBlk - 1) / kBlk;
+    const double total = 0.5 * pt * (pt + 1.0);
+    std::vector<int> cut(P + 1, nblk);
+    cut[0] = 0;
+    double acc = 0;
+    for (int bk = 0, r = 1; bk < nblk && r < P; ++bk) {
+        const double r0 = (double)bk * kBlk, r1 = std::min<double>(pt, r0 + kBlk);
+        acc += 0.5 * (r1 * (r1 + 1) - r0 * (r0 + 1));
+        while (r < P && acc >= total * r / P) cut[r++] = bk + 1;
+    }
+    const int a0 = std::min(pt, cut[part] * kBlk), a1 = std::min(pt, cut[part + 1] * kBlk);
+    const std::vector<double>& L = F.Linv[top];
+    std::vector<double> y(3 * (size_t)pt, 0.0), x(3 * (size_t)pt, 0.0);
+    for (int i = a0; i < a1; ++i)
+        for (int k = 0; k <= i; ++k)
+            for (int c = 0; c < 3; ++c) y[3 * i + c] += L[(size_t)i * pt + k] * f[3 * k + c];
+    for (int j = 0; j < a1; ++j)
+        for (int i = std::max(j, a0); i < a1; ++i)
+            for (int c = 0; c < 3; ++c) x[3 * j + c] += L[(size_t)i * pt + j] * y[3 * i + c];
+    bar.reduce(x.data(), x.size());   // the summed x_top
+    std::copy(x.begin(), x.end(), f);
+    for (int s = nn - 1; s >= 0; --s) {   // backward over the own part
+        if (!own(s)) continue;
+        const int b0 = F.beg[s], p = F.end[s] - b0, nb = (int)F.bnd[s].size();
+        t.assign((size_t)p * 3, 0.0);
+        for (int j = 0; j < p; ++j)
+            for (int c = 0; c < 3; ++c) {
+                double v = b[3 * (size_t)(b0 + j) + c];
+                for (int a = 0; a < nb; ++a) v -= F.LBP[s][(size_t)a * p + j] * b[3 * (size_t)F.bnd[s][a] + c];
+                t[3 * j + c] = v;
+            }
+        for (int j = 0; j < p; ++j)
+            for (int c = 0; c < 3; ++c) {
+                double v = 0;
+                for (int i = j; i < p; ++i) v += F.Linv[s][(size_t)i * p + j] * t[3 * i + c];
+                b[3 * (size_t)(b0 + j) + c] = v;
+            }
+    }
+}
 
 }  // namespace
 
@@ -87,9 +164,11 @@ int main(int argc, char** argv) {
     for (auto& v : b0) v = N01(rng);
 
     int fails = 0;
-    for (int L = 0; L <= 3; ++L) {
-        const int P = 1 << L;
-        aa::NdTree T = aa::nested_dissection(n, xyz.data(), aptr, aj, 8, 0, L);
+    const int cases[][2] = {{1, 0}, {2, 0}, {4, 0}, {8, 0}, {2, 1}, {3, 1}, {4, 1}, {8, 1}};   // (P, dense top)
+    for (const auto& cs : cases) {
+        const int P = cs[0];
+        const bool dense = cs[1] != 0;
+        aa::NdTree T = aa::nested_dissection(n, xyz.data(), aptr, aj, 8, 0, P > 1 ? P : 0, dense);
         std::vector<int> inv(n);
         for (int q = 0; q < n; ++q) inv[T.perm[q]] = q;
         aa::CsrMatrix A;
@@ -137,8 +216,9 @@ int main(int argc, char** argv) {
         std::vector<std::thread> th;
         for (int pp = 0; pp < P; ++pp)
             th.emplace_back([&, pp] {
-                aa::factor_solve_host_part(F, L > 0 ? &T : nullptr, L > 0 ? pp : -1, bp[pp],
-                                           [&](double* v, size_t m) { bar.reduce(v, m); });
+                if (dense) solve_dense_top(F, T, pp, P, bp[pp], bar);
+                else aa::factor_solve_host_part(F, P > 1 ? &T : nullptr, P > 1 ? pp : -1, bp[pp],
+                                                [&](double* v, size_t m) { bar.reduce(v, m); });
             });
         for (auto& t : th) t.join();
         double emax = 0, xmax = 0, tdiff = 0;
@@ -153,9 +233,12 @@ int main(int argc, char** argv) {
                     for (int pp = 1; pp < P; ++pp) tdiff = std::max(tdiff, std::fabs(bp[pp][3 * q + c] - bp[0][3 * q + c]));
             }
         }
-        const bool ok = rmax <= 1e-10 * bmax && emax <= 1e-10 * xmax && tdiff == 0.0 && (L == 0 || T.top_beg < n);
-        std::printf("parts=%d n=%d top_rows=%d nnzL=%zu |Ax-b|=%.2e |x_part-x|=%.2e top_spread=%.1e %s\n", P, n,
-                    n - T.top_beg, F.nnz_L, rmax / bmax, emax / xmax, tdiff, ok ? "OK" : "FAIL");
+        int ntop = 0;
+        for (int s = 0; s < F.n_nodes; ++s) ntop += T.part[s] == -1 && F.end[s] > F.beg[s];
+        const bool ok = rmax <= 1e-10 * bmax && emax <= 1e-10 * xmax && tdiff == 0.0 && (P == 1 || T.top_beg < n) &&
+                        (int)T.part_beg.size() == std::max(1, P) && (!dense || ntop == 1);
+        std::printf("parts=%d dense_top=%d n=%d top_rows=%d top_nodes=%d nnzL=%zu |Ax-b|=%.2e |x_part-x|=%.2e top_spread=%.1e %s\n",
+                    P, (int)dense, n, n - T.top_beg, ntop, F.nnz_L, rmax / bmax, emax / xmax, tdiff, ok ? "OK" : "FAIL");
         if (!ok) ++fails;
     }
     return fails ? 1 : 0;

@@ -191,7 +191,28 @@ def full_drop40(tmp):
     print("full_drop40_z_nh_aa6", [len(s["prim"]) for s in steps])
 
 
+def residual_files(tmp):
+    """The reference's own Solver::save() output (Solver.hpp:130-155: result/residual-<m>.txt,
+    written by every step()) for one (u,x)-variant and one z-variant scene, kept verbatim as data
+    (the last step's rows) -- pins the format of Solver.save()."""
+    for name, sc, out in (("cant8_ux_lin_aa6", cases()["cant8_ux_lin_aa6"], "ref_residual_h.txt"),
+                          ("cloth12_z_noaa", cases()["cloth12_z_noaa"], "ref_residual_x.txt")):
+        res = os.path.join(tmp, "result")
+        if os.path.isdir(res):
+            for f in os.listdir(res):
+                os.remove(os.path.join(res, f))
+        run_ref(sc, tmp)
+        (f,) = os.listdir(res)
+        with open(os.path.join(res, f)) as src, open(os.path.join(HERE, out), "w") as dst:
+            dst.write("# " + name + " " + f + "\n" + src.read())
+        print(out, f)
+
+
 def main(only=None):
+    if only == ["--residual-files"]:
+        with tempfile.TemporaryDirectory() as tmp:
+            residual_files(tmp)
+        return
     if only == ["--full"]:
         with tempfile.TemporaryDirectory() as tmp:
             full_drop40(tmp)

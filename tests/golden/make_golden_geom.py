@@ -111,8 +111,17 @@ def airport(iters=100, aa_m=10):
     return gs.planarity_from_mesh(V, F, RV, np.array(RF, np.int32), iters=iters, aa_m=aa_m, name="airport3k")
 
 
+def costa_wire(iters=60, aa_m=5):
+    """WireMeshOpt's main on the reference's costa2k files: subdivide_and_smooth, half the
+    average edge length, the optimize_mesh recipe (geom_scenes.wire_from_polymesh)."""
+    V, F = gs.read_obj(os.path.join(DATA, "polymesh", "costa2k_poly.obj"))
+    RV, RF = gs.read_obj(os.path.join(DATA, "trimesh", "costa2k_tri.obj"))
+    return gs.wire_from_polymesh(V, F, RV, np.array(RF, np.int32), iters=iters, aa_m=aa_m, name="costa2k_wire")
+
+
 def cases():
     return {
+        "geom_costa2k_wire_aa5": costa_wire(),
         "geom_pq12_aa10": gs.pq_heightfield(12, 12, iters=60, aa_m=10),
         "geom_pq12_noaa": gs.pq_heightfield(12, 12, iters=40, aa_m=0),
         "geom_wire12_aa20": gs.wire_grid(12, 12, iters=60, aa_m=20),
@@ -153,6 +162,46 @@ def run_planarity_app(tmp, iters, m):
     if r.returncode != 0:
         raise RuntimeError(r.stderr)
     return np.loadtxt(os.path.join(tmp, "result", f"residual-{m}.txt"))[:, 1]
+
+
+def run_wire_app(tmp, iters, m):
+    """The reference's own WireMeshOpt on its own costa2k files; returns the residual curve."""
+    os.makedirs(os.path.join(tmp, "result"), exist_ok=True)
+    with open(os.path.join(tmp, "opt.txt"), "w") as f:
+        f.write(f"Iterations {iters}\nAndersonM {max(m, 1)}\n")
+    r = subprocess.run([os.path.join(REF, "WireMeshOpt"), os.path.join(DATA, "polymesh", "costa2k_poly.obj"),
+                        os.path.join(DATA, "trimesh", "costa2k_tri.obj"), "opt.txt", "out.obj"], cwd=tmp,
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr)
+    return np.loadtxt(os.path.join(tmp, "result", f"residual-{m}.txt"))[:, 1]
+
+
+def subdiv_fixture(tmp):
+    """subdivide_and_smooth_mesh (MeshTypes.h:214-342) + average_edge_length of the reference on
+    costa2k_poly (oracle/_ref/ref_subdiv): output positions, faces and the edge length."""
+    out = os.path.join(tmp, "sub.bin")
+    r = subprocess.run([os.path.join(REF, "ref_subdiv"), os.path.join(DATA, "polymesh", "costa2k_poly.obj"), out],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr)
+    d = open(out, "rb").read()
+    nv, nf = struct.unpack("<ii", d[:8])
+    el = struct.unpack("<d", d[8:16])[0]
+    X = np.frombuffer(d[16:16 + 24 * nv], "<f8").reshape(-1, 3)
+    off, sizes, idx = 16 + 24 * nv, [], []
+    for _ in range(nf):
+        k = struct.unpack("<i", d[off:off + 4])[0]
+        off += 4
+        sizes.append(k)
+        idx += list(struct.unpack(f"<{k}i", d[off:off + 4 * k]))
+        off += 4 * k
+    V, F = gs.read_obj(os.path.join(DATA, "polymesh", "costa2k_poly.obj"))   # the input, as OpenMesh reads it
+    np.savez_compressed(os.path.join(HERE, "mesh_wire_subdiv_costa2k.npz"), x=X, face_sizes=np.array(sizes, np.int32),
+                        face_idx=np.array(idx, np.int32), edge_length=np.array(el), in_x=V,
+                        in_face_sizes=np.array([len(f) for f in F], np.int32),
+                        in_face_idx=np.array([v for f in F for v in f], np.int32))
+    print("mesh_wire_subdiv_costa2k", nv, nf, el)
 
 
 def element_tables(tmp):
@@ -250,8 +299,15 @@ def main():
             for name, sc in cases().items():
                 if name in only:
                     res = run_ref(sc, tmp)
-                    save_geom_case(os.path.join(HERE, name + ".npz"), sc, dict(comb=res["comb"], x=res["x"]))
+                    outputs = dict(comb=res["comb"], x=res["x"])
+                    if name.startswith("geom_costa2k_wire"):
+                        outputs["app_comb"] = run_wire_app(tmp, sc.iters, sc.aa_m)
+                    save_geom_case(os.path.join(HERE, name + ".npz"), sc, outputs)
                     print(name, sc.n_points, len(res["comb"]), f"comb {res['comb'][0]:.4e} -> {res['comb'][-1]:.4e}")
+        return
+    if "--subdiv" in sys.argv:
+        with tempfile.TemporaryDirectory() as tmp:
+            subdiv_fixture(tmp)
         return
     if "--full" in sys.argv:
         with tempfile.TemporaryDirectory() as tmp:
@@ -269,6 +325,8 @@ def main():
                 app = run_planarity_app(tmp, sc.iters, sc.aa_m)
                 if app is not None:
                     outputs["app_comb"] = app
+            if name.startswith("geom_costa2k_wire"):
+                outputs["app_comb"] = run_wire_app(tmp, sc.iters, sc.aa_m)
             save_geom_case(os.path.join(HERE, name + ".npz"), sc, outputs)
             print(name, sc.n_points, len(res["comb"]), f"comb {res['comb'][0]:.4e} -> {res['comb'][-1]:.4e}")
         et = element_tables(tmp)

@@ -31,9 +31,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(case, nranks, out, transport="host"):
+def run_ranks(case, nranks, out, transport="host", extra_env=None):
     env = dict(os.environ, AA_CASE=case, AA_OUT=str(out), AA_TRANSPORT=transport, AA_DEVICE="0",
-               OMP_NUM_THREADS="4")
+               OMP_NUM_THREADS="4", **(extra_env or {}))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
                         "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
                         os.path.join(REPO, "tests", "part_worker.py")],
@@ -46,13 +46,17 @@ def as_steps(d, n_steps):
     return [{k: d[f"{k}{i}"] for k in ("prim", "comb", "reject", "x", "v")} for i in range(n_steps)]
 
 
-@pytest.mark.parametrize("case,nranks", [("cloth_ux", 2), ("cloth_ux", 4), ("cant_ux", 2), ("drop_z", 2),
-                                         ("drop_z", 4), ("beams_z", 2), ("cant_z_noaa", 2)])
-def test_partitioned_matches_single_gpu(case, nranks, tmp_path, pkg, ctx):
+# 3 ranks: an uneven part count (proportional bisections); top=0: the round-1 layout with one
+# supernode per shared separator, solved whole on every rank (AA_TOP_DENSE=0) -- the default is
+# one dense top root split over the ranks by rows
+@pytest.mark.parametrize("case,nranks,top", [("cloth_ux", 2, 1), ("cloth_ux", 4, 1), ("cloth_ux", 3, 1), ("cant_ux", 2, 1),
+                                             ("drop_z", 2, 1), ("drop_z", 4, 1), ("drop_z", 3, 1), ("drop_z", 4, 0),
+                                             ("beams_z", 2, 1), ("cant_z_noaa", 2, 1)])
+def test_partitioned_matches_single_gpu(case, nranks, top, tmp_path, pkg, ctx):
     builder, tol = CASES[case]
     sc = builder()
     want, _ = pkg.capi.run_scene(ctx, sc)
-    ranks = run_ranks(case, nranks, tmp_path)
+    ranks = run_ranks(case, nranks, tmp_path, extra_env={"AA_TOP_DENSE": str(top)})
     # every element is owned by exactly one rank
     assert sum(int(r["n_elements"][0]) for r in ranks) == sc.n_elements()
     # all ranks hold the same bits
@@ -84,7 +88,7 @@ def test_rccl_transport_one_rank_is_identity(pkg, ctx):
     comm.close()
 
 
-@pytest.mark.parametrize("case,nranks", [("pq", 2), ("pq", 4), ("wire", 2), ("pq_noaa", 2)])
+@pytest.mark.parametrize("case,nranks", [("pq", 2), ("pq", 4), ("pq", 3), ("wire", 2), ("pq_noaa", 2)])
 def test_partitioned_geometry_matches_single_gpu(case, nranks, tmp_path, pkg, ctx):
     sc = GEOM_CASES[case]()
     want, g = pkg.capi.run_geom(ctx, sc)

@@ -43,3 +43,37 @@ def test_oracle_geom_elements(oracle):
         np.testing.assert_allclose(oracle.geom_project(gs.EDGE, 2, prm, X), Y, rtol=0, atol=1e-14)
     got = oracle.closest_point(d["closest_V"], d["closest_F"], d["closest_in"])
     np.testing.assert_allclose(got, d["closest_out"], rtol=0, atol=1e-13)
+
+
+def test_recipe_matches_reference_wiremesh_app(oracle):
+    """geom_scenes.wire_from_polymesh (subdivide_and_smooth + half the average edge length + the
+    optimize_mesh recipe) on costa2k reproduces the residual curve of the reference's own
+    WireMeshOpt run on its own data files (Geometry/WireMeshOpt.cpp:341-391)."""
+    sc, ref = load_geom_case("geom_costa2k_wire_aa5")
+    app = ref["app_comb"]
+    assert len(app) == len(ref["comb"])
+    dev = np.abs(app - ref["comb"]).max() / app[0]
+    assert dev < 1e-8, dev
+
+
+def test_subdivide_and_smooth_matches_reference():
+    """WireMeshOpt's pre-processing (subdivide_and_smooth_mesh, Geometry/MeshTypes.h:214-342)
+    against the reference's own output on costa2k_poly (oracle/_ref/ref_subdiv): the same faces
+    in the same order, positions to 1e-12 of the mesh scale (the smoothing solve is a sparse
+    direct solve here, SimplicialLDLT there), and average_edge_length (MeshTypes.h:143-156)."""
+    import importlib
+    gs = importlib.import_module("aa-admm_amd.geom_scenes")
+    d = np.load(os.path.join(GOLDEN, "mesh_wire_subdiv_costa2k.npz"))
+
+    def faces(sizes, idx):
+        out, o = [], 0
+        for k in sizes:
+            out.append([int(v) for v in idx[o:o + k]])
+            o += k
+        return out
+
+    V, F = d["in_x"], faces(d["in_face_sizes"], d["in_face_idx"])
+    X, SF = gs.subdivide_and_smooth(V, F)
+    assert SF == faces(d["face_sizes"], d["face_idx"])
+    np.testing.assert_allclose(X, d["x"], rtol=0, atol=1e-12 * np.abs(d["x"]).max())
+    assert abs(gs.average_edge_length(V, F) - float(d["edge_length"])) <= 1e-14 * float(d["edge_length"])
