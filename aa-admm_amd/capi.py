@@ -27,7 +27,7 @@ EXPORTS = [
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
     "aa_elastic_get_times", "aa_elastic_set_iterations", "aa_elastic_set_x",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats", "aa_elastic_local_stats",
-    "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_destroy", "aa_comm_info",
+    "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_create_solo", "aa_comm_destroy", "aa_comm_info",
     "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
     "aa_geom_create", "aa_geom_create_kind", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
     "aa_geom_add_closeness", "aa_geom_setup", "aa_geom_solve", "aa_geom_get_solution", "aa_geom_get_history",
@@ -165,6 +165,13 @@ class Comm:
         h = C.c_void_p()
         _chk(lib().aa_comm_create_host(cfn, None, C.c_int(rank), C.c_int(size), C.byref(h)))
         return cls(h, keep=cfn)
+
+    @classmethod
+    def solo(cls, rank: int, size: int):
+        """Timing rehearsal: one rank of a size-way partition alone (aa_comm_create_solo)."""
+        h = C.c_void_p()
+        _chk(lib().aa_comm_create_solo(C.c_int(rank), C.c_int(size), C.byref(h)))
+        return cls(h)
 
     def info(self):
         r, n = C.c_int(), C.c_int()

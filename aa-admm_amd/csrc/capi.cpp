@@ -254,6 +254,16 @@ int aa_comm_create_host(aa_host_allreduce_fn fn, void* user, int rank, int size,
     });
 }
 
+int aa_comm_create_solo(int rank, int size, aa_comm* out) {
+    return guarded([&] {
+        NEED(out, "aa_comm_create_solo: null out");
+        NEED(size >= 1 && rank >= 0 && rank < size, "aa_comm_create_solo: bad rank/size");
+        auto* c = new aa_comm_s;
+        c->c = aa::make_solo_comm(rank, size);
+        *out = c;
+    });
+}
+
 int aa_comm_destroy(aa_comm c) {
     return guarded([&] { delete c; });
 }

@@ -117,7 +117,27 @@ private:
     std::vector<double> buf_;
 };
 
+// Rehearsal transport: ONE rank of a P-way partition on its own GPU, every other rank absent.
+// A device all-reduce leaves the local values (dst = src), a host all-reduce multiplies by P
+// (as if every rank held the same values: the setup's scene-identity checks pass, agreement
+// flags stay set). The numbers it produces are not a solution -- it exists to time one rank's
+// kernels of a P-GPU run (bench.py --rehearse P) with the step graph captured as in production.
+class SoloComm final : public Comm {
+public:
+    SoloComm(int rank, int size) { rank_ = rank; size_ = size; }
+    void allreduce_sum(const double* src, double* dst, size_t n, hipStream_t s) override {
+        if (n && src != dst) AA_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    void allreduce_sum_host(double* buf, size_t n) override {
+        for (size_t i = 0; i < n; ++i) buf[i] *= size_;
+    }
+    bool capturable() const override { return true; }
+    bool rehearsal() const override { return true; }
+};
+
 }  // namespace
+
+std::unique_ptr<Comm> make_solo_comm(int rank, int size) { return std::unique_ptr<Comm>(new SoloComm(rank, size)); }
 
 void rccl_unique_id(unsigned char out[128]) {
     ncclUniqueId uid;

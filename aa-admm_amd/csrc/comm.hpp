@@ -34,6 +34,7 @@ public:
     // in-place SUM of a host array (setup-time agreements); blocking
     virtual void allreduce_sum_host(double* buf, size_t n) = 0;
     virtual bool capturable() const = 0;   // may be recorded into a hipGraph
+    virtual bool rehearsal() const { return false; }   // solo timing rehearsal: results are not a solution
 
 protected:
     int rank_ = 0, size_ = 1;
@@ -42,5 +43,6 @@ protected:
 void rccl_unique_id(unsigned char out[128]);
 std::unique_ptr<Comm> make_rccl_comm(const unsigned char id[128], int rank, int size);
 std::unique_ptr<Comm> make_host_comm(HostAllreduceFn fn, void* user, int rank, int size);
+std::unique_ptr<Comm> make_solo_comm(int rank, int size);   // timing rehearsal of one rank (comm.cpp)
 
 }  // namespace aa

@@ -13,11 +13,6 @@ namespace aa {
 
 namespace {
 
-// loads per chunk of the pipelined row / column products (dot_pipe; build-time A/B knob)
-#ifndef AA_ROW_CHUNK
-#define AA_ROW_CHUNK 8
-#endif
-
 __device__ __forceinline__ bool solve_gated(const Ctrl* c, int gate_reject) {
     if (!c) return false;
     if (c->done) return true;
@@ -78,43 +73,6 @@ __device__ __forceinline__ void zero(double* a) {
     for (int k = 0; k < NR; ++k) a[k] = 0;
 }
 
-// a[m] += sum_{i < n} G[(c0 + i) * stride] * V[NR * (c0 + i) + m], i in order: a dot product
-// of one factor row (or column) with an LDS vector, software-pipelined -- chunks of C loads,
-// two chunks in flight, the loads unconditional (index clamped to the last one; the clamped
-// terms add zero) so none waits behind a branch. Same sums in the same order as the plain loop.
-template <int NR, int C>
-__device__ __forceinline__ void dot_pipe(const double* __restrict__ G, size_t stride, int c0, int n,
-                                         const double* __restrict__ V, double* a) {
-    if (n <= 0) return;
-    double ga[C], gb[C];
-    auto ld = [&](double* g, int k) {
-#pragma unroll
-        for (int q = 0; q < C; ++q) g[q] = G[(size_t)(c0 + min(k * C + q, n - 1)) * stride];
-    };
-    auto use = [&](const double* g, int k) {
-#pragma unroll
-        for (int q = 0; q < C; ++q) {
-            const int i = k * C + q;
-            const bool in = i < n;
-            const double gq = in ? g[q] : 0.0;
-            const double* v = V + NR * (c0 + (in ? i : n - 1));
-#pragma unroll
-            for (int m = 0; m < NR; ++m) a[m] += gq * v[m];
-        }
-    };
-    const int nch = (n + C - 1) / C;
-    ld(ga, 0);
-    if (nch > 1) ld(gb, 1);
-    for (int k = 0; k < nch; k += 2) {
-        use(ga, k);
-        if (k + 2 < nch) ld(ga, k + 2);
-        if (k + 1 < nch) {
-            use(gb, k + 1);
-            if (k + 3 < nch) ld(gb, k + 3);
-        }
-    }
-}
-
 // front row q of a supernode (any record with beg, p, ell_w, ell_off): [b_P ; 0]_q + the
 // children's update entries landing on it (ELL pull list: ell_w offsets into U per row, -1 =
 // none; fixed order -> deterministic)
@@ -156,7 +114,12 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
     const int cmax = r < p ? r + 1 : p;
     double a[NR];
     zero<NR>(a);
-    dot_pipe<NR, AA_ROW_CHUNK>(G, (size_t)R, 0, cmax, f, a);
+#pragma unroll 8
+    for (int c = 0; c < cmax; ++c) {
+        const double v = G[(size_t)c * R];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
+    }
     if (r < p) {
         double* y = Y + NR * (size_t)(t.beg + r);
 #pragma unroll
@@ -206,7 +169,12 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
     const int ld = t.ldr;
     double a[NR];
     zero<NR>(a);
-    dot_pipe<NR, AA_ROW_CHUNK>(G, (size_t)ld, j, R - j, v, a);
+#pragma unroll 8
+    for (int r = j; r < R; ++r) {
+        const double g = G[(size_t)r * ld];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
+    }
     st_ext<NR>(X0, X1, (size_t)(t.beg + j), a);
 }
 
@@ -485,7 +453,12 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             const int cmax = r < p ? r + 1 : p;
             double a[NR];
             zero<NR>(a);
-            dot_pipe<NR, AA_ROW_CHUNK>(G, (size_t)R, 0, cmax, f, a);
+#pragma unroll 8
+            for (int c = 0; c < cmax; ++c) {
+                const double v = G[(size_t)c * R];
+#pragma unroll
+                for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
+            }
             if (r < p) {
                 double* y = Y + NR * (size_t)(nd.beg + r);
 #pragma unroll
@@ -545,8 +518,12 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             const int r1 = min(R, (seg + 1) * kSubSegRows);
             double a[NR];
             zero<NR>(a);
-            const int rs = max(j, seg * kSubSegRows);
-            dot_pipe<NR, AA_ROW_CHUNK>(G, (size_t)ld, rs, r1 - rs, v, a);
+#pragma unroll 8
+            for (int r = max(j, seg * kSubSegRows); r < r1; ++r) {
+                const double g = G[(size_t)r * ld];
+#pragma unroll
+                for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
+            }
             double* q = lds + K * nd.slot + NR * (sub_seg_off(seg, p) + j);
 #pragma unroll
             for (int k = 0; k < NR; ++k) q[k] = a[k];

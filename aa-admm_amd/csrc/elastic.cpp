@@ -972,6 +972,7 @@ void ElasticSolver::fetch_results() {
         double f[2] = {c.fail == 1 ? 1.0 : 0.0, c.fail == 2 ? 1.0 : 0.0};
         comm_->allreduce_sum_host(f, 2);
         c.fail = f[0] > 0 ? 1 : (f[1] > 0 ? 2 : 0);
+        if (comm_->rehearsal()) c.fail = 0;   // the other parts are absent: positions are not physical
     }
     if (c.fail == 1) throw Error(ERR_NUMERIC, "the line search step became smaller than the minimum value allowed");
     if (c.fail == 2) throw Error(ERR_NUMERIC, "**TriEnergyTerm TODO: gradient function");

@@ -64,6 +64,11 @@ def parse():
     p.add_argument("--eps-cap", type=int, default=500)
     p.add_argument("--no-secondary", action="store_true",
                    help="c4 only: skip the secondary C3 (planar-quad, configs[2]) object in the same JSON line")
+    p.add_argument("--rehearse", type=int, default=0, metavar="P",
+                   help="c4/c2, one GPU: time ONE rank's share of a P-way mesh partition (aa_comm_create_solo: "
+                        "collectives replaced by local stand-ins, so the numbers are not a solution) -- the "
+                        "per-rank kernel time of a P-GPU run, for the DESIGN.md scaling projection")
+    p.add_argument("--rehearse-rank", type=int, default=0)
     p.add_argument("--lq-stats", action="store_true",
                    help="c4: count the local step's L-BFGS iterations per element and its work-queue trips over "
                         "the timed steps (AA_LQ_STATS=1; atomics in the kernel, so not for the timed number)")
@@ -180,6 +185,9 @@ def make_comm(pkg, ctx, args, world, rank):
     """Communicator of a mesh-partitioned run (None for replicas)."""
     part = args.partition if args.partition != "auto" else ("rccl" if world > 1 else "none")
     comm = None
+    if getattr(args, "rehearse", 0) > 1 and world == 1:
+        return (pkg.capi.Comm.solo(args.rehearse_rank, args.rehearse),
+                f"solo rehearsal: rank {args.rehearse_rank} of {args.rehearse}, collectives replaced")
     if part == "rccl":
         try:
             comm = pkg.dist.rccl_comm(ctx, rank, world)
@@ -433,6 +441,8 @@ def run_to_eps(solver, args, state0):
 
 def main():
     args = parse()
+    if args.rehearse > 1:   # a timing rehearsal is not a bench line: no baselines, no eps leg
+        args.no_cpu_baseline, args.no_secondary, args.eps_steps = True, True, 0
     world, rank, local, dist = dist_setup(args.gpus)
     if args.config in ("c3", "c5"):
         return main_geom(args, world, rank, local, dist)
@@ -573,6 +583,12 @@ def main():
         }
         if comm is not None:
             line["config"]["partition"] = {"elements_rank0": rt.n_elements, "z_dim_rank0": rt.z_dim}
+        if args.rehearse > 1:
+            line["metric"] = f"REHEARSAL (not a result): one rank's share of a {args.rehearse}-GPU partition"
+            line["rehearsal"] = {"P": args.rehearse, "rank": args.rehearse_rank,
+                                 "us_per_iter": round(elapsed_max * 1e6 / max(1, iters_run), 2),
+                                 "note": "collectives replaced by local stand-ins (aa_comm_create_solo); add the "
+                                         "all-reduce cost for a P-GPU estimate"}
         if lq is not None:
             line["local_step_queue"] = lq
         if secondary is not None:

@@ -155,6 +155,10 @@ int aa_comm_create_rccl(aa_ctx ctx, const unsigned char id[128], int rank, int s
 /* Host-staged transport through a caller callback (e.g. torch.distributed/gloo); lets several
  * ranks share one GPU (tests). Never captured into a hipGraph. */
 int aa_comm_create_host(aa_host_allreduce_fn fn, void* user, int rank, int size, aa_comm* out);
+/* Timing rehearsal (no reference counterpart): rank `rank` of a `size`-way partition alone on
+ * its GPU -- device all-reduces keep the local values, host all-reduces multiply by size. The
+ * results are NOT a solution; it times one rank's share of a multi-GPU step (bench.py --rehearse). */
+int aa_comm_create_solo(int rank, int size, aa_comm* out);
 int aa_comm_destroy(aa_comm c);
 int aa_comm_info(aa_comm c, int* rank, int* size);
 /* In-place SUM of a host array over the ranks (blocking; setup-time agreements, tests). */
