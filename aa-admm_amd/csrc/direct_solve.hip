@@ -112,6 +112,10 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
     const int r = t.r0 + tid;
     const double* G = Gc + t.goff + r;
     const int cmax = r < p ? r + 1 : p;
+    // a boundary row's own front value is gathered first: its two dependent loads overlap the
+    // factor stream instead of following it
+    double fr[NR];
+    if (r >= p) front_row<NR>(t, r, ell, B0, B1, U, fr);
     double a[NR];
     zero<NR>(a);
 #pragma unroll 8
@@ -125,8 +129,6 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
 #pragma unroll
         for (int k = 0; k < NR; ++k) y[k] = a[k];
     } else {
-        double fr[NR];
-        front_row<NR>(t, r, ell, B0, B1, U, fr);
         double* u = U + (NR / 3) * t.uoff + NR * (size_t)(r - p);
 #pragma unroll
         for (int k = 0; k < NR; ++k) u[k] = fr[k] - a[k];
@@ -364,6 +366,9 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // last tile of the row block: sum its partials in tile order (deterministic)
     if (lane < rd.nr) {
+        const int rr = rd.r0 + lane;
+        double fr[NR];   // a boundary row's front value: gathered before the partials are summed
+        if (rr >= rd.p) front_row<NR>(rd, rr, ell, B0, B1, U, fr);
         double b[NR];
         zero<NR>(b);
         const double* q = part + (NR / 3) * rd.poff + NR * lane;
@@ -371,14 +376,11 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
         for (int k = 0; k < rd.nt; ++k, q += NR * 64)
 #pragma unroll
             for (int m = 0; m < NR; ++m) b[m] += q[m];
-        const int rr = rd.r0 + lane;
         if (rr < rd.p) {
             double* y = Y + NR * (size_t)(rd.beg + rr);
 #pragma unroll
             for (int k = 0; k < NR; ++k) y[k] = b[k];
         } else {
-            double fr[NR];
-            front_row<NR>(rd, rr, ell, B0, B1, U, fr);
             double* u = U + (NR / 3) * rd.uoff + NR * (size_t)(rr - rd.p);
 #pragma unroll
             for (int k = 0; k < NR; ++k) u[k] = fr[k] - b[k];
@@ -429,12 +431,15 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
                                                  const double* __restrict__ Gc, const long long* __restrict__ ell,
                                                  const double* __restrict__ B0, const double* __restrict__ B1,
                                                  double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
-                                                 int gate_reject) {
+                                                 int gate_reject, long long* clk, int clk_stride) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int K = NR / 3;
     const SubTree T = trees[blockIdx.x];
     const int tid = threadIdx.x;
+    // optional phase clock (AA_SUB_TIMING): kernel start, then after every barrier
+    long long* ck = clk ? clk + (size_t)blockIdx.x * clk_stride : nullptr;
+    if (ck && tid == 0) ck[0] = (long long)__builtin_amdgcn_s_memrealtime();
     for (int l = 0; l < T.nlvl; ++l) {
         const SubLevel L = lvls[T.lvl0 + l];
         for (int i = tid; i < L.nfa; i += BLOCK) {          // front vectors f_P of the level's supernodes
@@ -444,6 +449,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             front_row<NR>(nd, c, ell, B0, B1, U, lds + K * nd.lds + NR * c);
         }
         __syncthreads();
+        if (ck && tid == 0) ck[1 + 2 * l] = (long long)__builtin_amdgcn_s_memrealtime();
         for (int i = tid; i < L.nfr; i += BLOCK) {          // rows of G . f_P
             const int it = items[L.fr0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
@@ -472,6 +478,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             }
         }
         __syncthreads();
+        if (ck && tid == 0) ck[2 + 2 * l] = (long long)__builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -493,12 +500,16 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
                                                  const long long* __restrict__ items2,
                                                  const double* __restrict__ Gr, const int* __restrict__ bnd,
                                                  const double* __restrict__ Y, double* __restrict__ X0,
-                                                 double* __restrict__ X1, const Ctrl* ctrl, int gate_reject) {
+                                                 double* __restrict__ X1, const Ctrl* ctrl, int gate_reject,
+                                                 long long* clk, int clk_stride) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int K = NR / 3;
     const SubTree T = trees[blockIdx.x];
     const int tid = threadIdx.x;
+    long long* ck = clk ? clk + (size_t)blockIdx.x * clk_stride : nullptr;
+    if (ck && tid == 0) ck[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    int ph = 1;
     for (int l = T.nlvl - 1; l >= 0; --l) {
         const SubLevel L = lvls[T.lvl0 + l];
         for (int i = tid; i < L.nbv; i += BLOCK) {          // [y_P ; -x_B] of the level's supernodes
@@ -508,6 +519,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             bwd_row<NR>(nd, r, bnd, Y, X0, X1, lds + K * nd.lds + NR * r);
         }
         __syncthreads();
+        if (ck && tid == 0) ck[ph++] = (long long)__builtin_amdgcn_s_memrealtime();
         for (int i = tid; i < L.nbs; i += BLOCK) {          // segment partials of G^T . v
             const long long it = items2[L.bs0 + i];
             const SubNode nd = nodes[L.n0 + (int)(it >> 40)];
@@ -529,6 +541,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             for (int k = 0; k < NR; ++k) q[k] = a[k];
         }
         __syncthreads();
+        if (ck && tid == 0) ck[ph++] = (long long)__builtin_amdgcn_s_memrealtime();
         for (int i = tid; i < L.nbc; i += BLOCK) {          // columns: sum of their segments
             const int it = items[L.bc0 + i];
             const SubNode nd = nodes[L.n0 + (it >> 16)];
@@ -546,6 +559,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             st_ext<NR>(X0, X1, (size_t)(nd.beg + j), a);
         }
         __syncthreads();
+        if (ck && tid == 0) ck[ph++] = (long long)__builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -694,7 +708,10 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     const char* wr = std::getenv("AA_SOLVE_WAVER");
     wave_p_ = wp ? std::atoi(wp) : wave_p;
     wave_r_ = wr ? std::atoi(wr) : wave_r;
-    const int min_sub = ms ? std::atoi(ms) : 256;
+    // fused subtrees wanted: enough workgroups to fill the chip on one GPU; a partitioned GPU's
+    // share of the tree is P times smaller, and its fused subtrees cost a latency chain per level
+    // whatever their count, so it takes fewer, taller ones (measured)
+    const int min_sub = ms ? std::atoi(ms) : (comm_ ? std::max(32, 256 / comm_->size()) : 256);
     constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
     static_assert(kSubSegRows == 64, "LDS accounting below assumes 64-row segments");
     auto roots_at = [&](int H) {
@@ -1067,6 +1084,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                          top_r0_, top_r1_, top_ft_count_, top_bt_count_);
     }
     if (n_sub_) kernels_ += 2;
+    if (const char* st = std::getenv("AA_SUB_TIMING")) {
+        sub_timing_ = std::atoi(st);
+        if (sub_timing_ > 0 && n_sub_ > 0) { sub_clk_.alloc(2 * 64 * (size_t)n_sub_); sub_clk_.zero(s); }
+        if (cut_height_ + 1 > 21) sub_timing_ = 0;   // 64 clock slots per workgroup
+    }
     bnd_.upload(bnd, s);
     ell_.upload(ell, s);
     Gr_.upload(Gr.get(), (size_t)go, s);
@@ -1133,8 +1155,13 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
                             int gate_reject, hipStream_t s) {
     constexpr int K = NR / 3;
     const Task* T = tasks_.p;
+    // AA_SUB_TIMING: phase clocks of the fused subtrees, printed for the first solves (eager only)
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    AA_HIP(hipStreamIsCapturing(s, &cst));
+    const bool clk_on = sub_timing_ > 0 && cst == hipStreamCaptureStatusNone && n_sub_ > 0;
 #define SUBF(BL) hipLaunchKernelGGL((k_fwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_f_, s, sub_trees_.p, \
-                                    sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
+                                    sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject, \
+                                    clk_on ? sub_clk_.p : nullptr, 64)
     if (n_sub_) switch (sub_block_) { case 1024: SUBF(1024); break; case 512: SUBF(512); break; default: SUBF(256); break; }
 #undef SUBF
     for (auto& L : levels_) {
@@ -1197,10 +1224,37 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     }
 #define SUBB(BL) hipLaunchKernelGGL((k_bwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_b_, s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, \
-                                    ctrl, gate_reject)
+                                    ctrl, gate_reject, clk_on ? sub_clk_.p + 64 * (size_t)n_sub_ : nullptr, 64)
     if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }
 #undef SUBB
     AA_CHECK_LAUNCH();
+    if (clk_on) {
+        --sub_timing_;
+        AA_HIP(hipStreamSynchronize(s));
+        std::vector<long long> h(2 * 64 * (size_t)n_sub_);
+        AA_HIP(hipMemcpy(h.data(), sub_clk_.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+        std::vector<SubTree> tr(n_sub_);
+        AA_HIP(hipMemcpy(tr.data(), sub_trees_.p, tr.size() * sizeof(SubTree), hipMemcpyDeviceToHost));
+        const int nl = tr[0].nlvl;
+        auto show = [&](const char* what, int base, int nph) {   // median / max over workgroups, us (100 MHz)
+            std::fprintf(stderr, "[solve] sub timing NR=%d %s:", NR, what);
+            for (int q = 1; q <= nph; ++q) {
+                std::vector<double> d;
+                for (int b = 0; b < n_sub_; ++b)
+                    if (tr[b].nlvl == nl) d.push_back(0.01 * (double)(h[(base + b) * 64 + q] - h[(base + b) * 64 + q - 1]));
+                if (d.empty()) continue;
+                std::sort(d.begin(), d.end());
+                std::fprintf(stderr, " %.1f/%.1f", d[d.size() / 2], d.back());
+            }
+            std::vector<double> tot;
+            for (int b = 0; b < n_sub_; ++b)
+                if (tr[b].nlvl == nl) tot.push_back(0.01 * (double)(h[(base + b) * 64 + nph] - h[(base + b) * 64]));
+            std::sort(tot.begin(), tot.end());
+            std::fprintf(stderr, " | total %.1f/%.1f us\n", tot[tot.size() / 2], tot.back());
+        };
+        show("fwd (assembly, rows per level, bottom-up)", 0, 2 * nl);
+        show("bwd (vector, segments, columns per level, top-down)", n_sub_, 3 * nl);
+    }
 }
 
 }  // namespace aa

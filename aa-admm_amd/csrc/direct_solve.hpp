@@ -30,6 +30,7 @@ namespace aa {
 class DirectSolver {
 public:
     static constexpr int kTopRows = 2048;    // upper tree levels amalgamated into one dense root
+    static constexpr int kPartTopRows = 4096;   // partitioned: a part's upper levels amalgamated (rows)
     static constexpr int kWaveP = 192;       // forward rows longer than this: wave per row
     static constexpr int kWaveR = 384;       // backward columns longer than this: wave per column
 
@@ -128,6 +129,8 @@ private:
     DevBuf<SubTree> sub_trees_;
     DevBuf<int> sub_items_;   // (local node << 16 | row) per item
     DevBuf<long long> sub_items2_;   // backward segment items (local node << 40 | segment << 20 | column)
+    int sub_timing_ = 0;              // AA_SUB_TIMING: solves left to time phase by phase
+    DevBuf<long long> sub_clk_;       // [2][n_sub_][64] s_memrealtime stamps
 };
 
 }  // namespace aa

@@ -326,8 +326,14 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     // the shared top separators as one dense root split over the ranks (AA_TOP_DENSE=0: one
     // supernode per separator, replicated on every rank -- the round-1 layout)
     const bool top_dense = !(std::getenv("AA_TOP_DENSE") && std::getenv("AA_TOP_DENSE")[0] == '0');
+    // ... and each part's own upper levels amalgamated into one dense supernode of up to this many
+    // rows (AA_PART_TOP_ROWS)
+    const int part_top_rows = std::getenv("AA_PART_TOP_ROWS") ? std::atoi(std::getenv("AA_PART_TOP_ROWS"))
+                                                              : DirectSolver::kPartTopRows;
+    const int nd_leaf = std::getenv("AA_ND_LEAF") ? std::max(1, std::atoi(std::getenv("AA_ND_LEAF"))) : 32;
     stamp("adjacency");
-    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, P > 1 ? P : 0, top_dense);
+    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::kTopRows, P > 1 ? P : 0, top_dense,
+                                     part_top_rows);
     stamp("nested dissection");
     node2int_.assign(n, -1);
     int2node_.assign(n, -1);

@@ -363,6 +363,11 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     // the shared top separators as one dense root split over the ranks (AA_TOP_DENSE=0: one
     // supernode per separator, replicated on every rank -- the round-1 layout)
     const bool top_dense = !(std::getenv("AA_TOP_DENSE") && std::getenv("AA_TOP_DENSE")[0] == '0');
+    // ... and each part's own upper levels amalgamated into one dense supernode of up to this many
+    // rows (AA_PART_TOP_ROWS)
+    const int part_top_rows = std::getenv("AA_PART_TOP_ROWS") ? std::atoi(std::getenv("AA_PART_TOP_ROWS"))
+                                                              : DirectSolver::kPartTopRows;
+    const int nd_leaf = std::getenv("AA_ND_LEAF") ? std::max(1, std::atoi(std::getenv("AA_ND_LEAF"))) : 32;
     if (P > 1) {   // every rank must have been handed the same problem
         double h[4] = {(double)n_, (double)hgroups_.size(), 0, 0};
         for (auto& g : hgroups_) h[2] += (double)g.idx.size();
@@ -373,7 +378,8 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
             if (std::fabs(r[i] - P * h[i]) > 1e-12 * std::fabs(P * h[i]))
                 throw Error(ERR_ARG, "solve_ADMM: the ranks were given different problems");
     }
-    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, 32, P > 1 ? 0 : DirectSolver::kTopRows, P > 1 ? P : 0, top_dense);
+    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::kTopRows, P > 1 ? P : 0, top_dense,
+                                     part_top_rows);
     top_beg_ = P > 1 ? tree.top_beg : n_;
     own_beg_ = P > 1 ? tree.part_beg[rank_] : 0;
     own_end_ = P > 1 ? tree.part_end[rank_] : n_;

@@ -108,7 +108,7 @@ struct NdBuilder {
 }  // namespace
 
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                         int leaf_size, int top_rows, int n_parts, bool merge_top) {
+                         int leaf_size, int top_rows, int n_parts, bool merge_top, int part_top_rows) {
     NdBuilder b(n, xyz, adj_ptr, adj, std::max(1, leaf_size));
     std::vector<int> all(n);
     std::iota(all.begin(), all.end(), 0);
@@ -119,9 +119,51 @@ NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_p
     std::vector<int> part_of = std::move(b.part_of);
     part_of.resize(piv.size(), part_levels > 0 ? -1 : 0);
     if (part_levels > 0) top_rows = 0;   // the partition roots must stay separate supernodes
+    // ---- amalgamate the top levels of the subtree under `root` into one dense supernode (up to
+    // `budget` pivots, whole levels, only while every node of the level is an inner node): upper
+    // levels have few, mid-sized supernodes whose level-by-level solve is pure latency; as one
+    // dense block they are a single wide GEMV per sweep. Returns the new root (or `root`).
+    auto amalgamate = [&](int root, long long budget) -> int {
+        std::vector<std::vector<int>> depth_nodes(1, {root});
+        long long rows = (long long)piv[root].size();
+        int K = 1;
+        for (;;) {
+            std::vector<int> next;
+            for (int s : depth_nodes.back()) next.insert(next.end(), kids[s].begin(), kids[s].end());
+            long long add = 0;
+            for (int s : next) add += (long long)piv[s].size();
+            bool all_inner = !next.empty();
+            for (int s : next) all_inner = all_inner && !kids[s].empty();
+            if (!all_inner || rows + add > budget) break;
+            rows += add;
+            depth_nodes.push_back(next);
+            ++K;
+        }
+        if (K <= 1) return root;
+        std::vector<char> top(piv.size(), 0);
+        for (auto& d : depth_nodes) for (int s : d) top[s] = 1;
+        std::vector<int> merged, below;
+        std::function<void(int)> post = [&](int s) {   // postorder over the merged nodes only
+            for (int c : kids[s]) {
+                if (top[c]) post(c);
+                else below.push_back(c);
+            }
+            merged.insert(merged.end(), piv[s].begin(), piv[s].end());
+        };
+        post(root);
+        const int pr = part_of[root];
+        piv.push_back(merged);
+        kids.push_back(below);
+        part_of.push_back(pr);
+        for (int s = 0; s < (int)top.size(); ++s) if (top[s]) { piv[s].clear(); kids[s].clear(); }
+        return (int)piv.size() - 1;
+    };
+    if (top_rows > 0 && roots.size() == 1) roots = {amalgamate(roots[0], top_rows)};
     // ---- partitioned, merge_top: all shared top separators become ONE dense root supernode
     // (children = the parts' roots). Its two sweeps are then dense GEMVs the GPUs split by rows
-    // (DirectSolver::build) instead of a replicated level-by-level solve.
+    // (DirectSolver::build) instead of a replicated level-by-level solve. Each
+    // part's own top levels are amalgamated too (part_top_rows): a part is a small tree whose
+    // upper levels would otherwise each cost a latency-bound launch per sweep.
     if (part_levels > 0 && merge_top && roots.size() == 1 && part_of[roots[0]] < 0) {
         std::vector<int> merged, below;
         std::function<void(int)> post = [&](int s) {   // postorder over the top separators
@@ -134,47 +176,13 @@ NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_p
             kids[s].clear();
         };
         post(roots[0]);
+        if (part_top_rows > 0)
+            for (int& c : below)
+                if (!kids[c].empty()) c = amalgamate(c, part_top_rows);
         piv.push_back(merged);
         kids.push_back(below);
         part_of.push_back(-1);
         roots = {(int)piv.size() - 1};
-    }
-    // ---- amalgamate the top of the tree into one dense supernode: the upper levels have few,
-    // mid-sized supernodes whose level-by-level solve is pure latency; as one dense block they
-    // are a single wide GEMV per sweep.
-    if (top_rows > 0 && roots.size() == 1) {
-        std::vector<std::vector<int>> depth_nodes(1, {roots[0]});
-        long long rows = (long long)piv[roots[0]].size();
-        int K = 1;
-        for (;;) {
-            std::vector<int> next;
-            for (int s : depth_nodes.back()) next.insert(next.end(), kids[s].begin(), kids[s].end());
-            long long add = 0;
-            for (int s : next) add += (long long)piv[s].size();
-            bool all_inner = !next.empty();
-            for (int s : next) all_inner = all_inner && !kids[s].empty();
-            if (!all_inner || rows + add > top_rows) break;
-            rows += add;
-            depth_nodes.push_back(next);
-            ++K;
-        }
-        if (K > 1) {
-            std::vector<char> top(piv.size(), 0);
-            for (auto& d : depth_nodes) for (int s : d) top[s] = 1;
-            std::vector<int> merged, below;
-            std::function<void(int)> post = [&](int s) {   // postorder over the top nodes only
-                for (int c : kids[s]) {
-                    if (top[c]) post(c);
-                    else below.push_back(c);
-                }
-                merged.insert(merged.end(), piv[s].begin(), piv[s].end());
-            };
-            post(roots[0]);
-            piv.push_back(merged);
-            kids.push_back(below);
-            for (int s = 0; s < (int)top.size(); ++s) if (top[s]) { piv[s].clear(); kids[s].clear(); }
-            roots = {(int)piv.size() - 1};
-        }
     }
     // ---- postorder numbering from the roots (children first). Partitioned: the subtrees of
     // part 0, 1, ... first (each a contiguous pivot range), then the top separators in

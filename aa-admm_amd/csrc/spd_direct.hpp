@@ -40,9 +40,11 @@ struct NdTree {
 // one dense root supernode. n_parts = P > 1: the top bisections are forced until there are P
 // parts (one per GPU of the partitioned solver; any P, uneven counts split by vertex count);
 // their separators form the "top" of the tree (part -1): with merge_top one dense root
-// supernode, else one supernode per separator. No top_rows amalgamation when partitioned.
+// supernode, else one supernode per separator. No top_rows amalgamation when partitioned;
+// part_top_rows > 0 (with merge_top) amalgamates each part's own top levels instead.
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                         int leaf_size, int top_rows = 0, int n_parts = 0, bool merge_top = true);
+                         int leaf_size, int top_rows = 0, int n_parts = 0, bool merge_top = true,
+                         int part_top_rows = 0);
 
 struct SupernodalFactor {
     int n = 0;

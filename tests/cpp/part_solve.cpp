@@ -164,11 +164,13 @@ int main(int argc, char** argv) {
     for (auto& v : b0) v = N01(rng);
 
     int fails = 0;
-    const int cases[][2] = {{1, 0}, {2, 0}, {4, 0}, {8, 0}, {2, 1}, {3, 1}, {4, 1}, {8, 1}};   // (P, dense top)
+    // (P, dense top, rows of each part's amalgamated upper levels)
+    const int cases[][3] = {{1, 0, 0}, {2, 0, 0}, {4, 0, 0}, {8, 0, 0}, {2, 1, 0}, {3, 1, 0}, {4, 1, 0}, {8, 1, 0},
+                            {4, 1, 64}, {8, 1, 40}};
     for (const auto& cs : cases) {
         const int P = cs[0];
         const bool dense = cs[1] != 0;
-        aa::NdTree T = aa::nested_dissection(n, xyz.data(), aptr, aj, 8, 0, P > 1 ? P : 0, dense);
+        aa::NdTree T = aa::nested_dissection(n, xyz.data(), aptr, aj, 8, 0, P > 1 ? P : 0, dense, cs[2]);
         std::vector<int> inv(n);
         for (int q = 0; q < n; ++q) inv[T.perm[q]] = q;
         aa::CsrMatrix A;
@@ -237,6 +239,7 @@ int main(int argc, char** argv) {
         for (int s = 0; s < F.n_nodes; ++s) ntop += T.part[s] == -1 && F.end[s] > F.beg[s];
         const bool ok = rmax <= 1e-10 * bmax && emax <= 1e-10 * xmax && tdiff == 0.0 && (P == 1 || T.top_beg < n) &&
                         (int)T.part_beg.size() == std::max(1, P) && (!dense || ntop == 1);
+        std::printf("part_top_rows=%d ", cs[2]);
         std::printf("parts=%d dense_top=%d n=%d top_rows=%d top_nodes=%d nnzL=%zu |Ax-b|=%.2e |x_part-x|=%.2e top_spread=%.1e %s\n",
                     P, (int)dense, n, n - T.top_beg, ntop, F.nnz_L, rmax / bmax, emax / xmax, tdiff, ok ? "OK" : "FAIL");
         if (!ok) ++fails;

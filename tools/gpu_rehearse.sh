@@ -7,8 +7,8 @@ mkdir -p gpurun_out
 for P in ${PS:-2 4 8}; do
   for TD in ${TDS:-1 0}; do
     for R in ${RANKS:-0}; do
-      AA_TOP_DENSE=$TD timeout -k 10 300 python -u bench.py --config ${CFG:-c4} --rehearse $P --rehearse-rank $R --steps ${STEPS:-3} --warmup 1 > gpurun_out/rehearse_${CFG:-c4}_P${P}_td${TD}_r$R.log 2>&1; rc=$?
-      echo "P=$P top_dense=$TD rank=$R rc=$rc"
+      env AA_TOP_DENSE=$TD ${ENVS//,/ } timeout -k 10 300 python -u bench.py --config ${CFG:-c4} --rehearse $P --rehearse-rank $R --steps ${STEPS:-3} --warmup 1 > gpurun_out/rehearse_${CFG:-c4}_P${P}_td${TD}_r$R.log 2>&1; rc=$?
+      echo "P=$P top_dense=$TD rank=$R [${ENVS}] rc=$rc"
       case $rc in 0) ;; *) tail -5 gpurun_out/rehearse_${CFG:-c4}_P${P}_td${TD}_r$R.log; exit $rc;; esac
       python - gpurun_out/rehearse_${CFG:-c4}_P${P}_td${TD}_r$R.log <<'PY'
 import json, sys
