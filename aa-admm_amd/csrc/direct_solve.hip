@@ -457,6 +457,8 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             const double* f = lds + K * nd.lds;
             const double* G = Gc + nd.goff + r;
             const int cmax = r < p ? r + 1 : p;
+            double fr[NR];   // a boundary row's own front value, gathered before the factor stream
+            if (r >= p) front_row<NR>(nd, r, ell, B0, B1, U, fr);
             double a[NR];
             zero<NR>(a);
 #pragma unroll 8
@@ -470,8 +472,6 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
 #pragma unroll
                 for (int k = 0; k < NR; ++k) y[k] = a[k];
             } else {
-                double fr[NR];
-                front_row<NR>(nd, r, ell, B0, B1, U, fr);
                 double* u = U + K * nd.uoff + NR * (size_t)(r - p);
 #pragma unroll
                 for (int k = 0; k < NR; ++k) u[k] = fr[k] - a[k];
@@ -487,7 +487,10 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
 // column), consecutive threads on consecutive columns of one row -> coalesced), partials in
 // LDS, then one item per column sums its segments in order: short loops instead of one thread
 // walking all R rows of a column.
-constexpr int kSubSegRows = 64;
+#ifndef AA_SUB_SEG
+#define AA_SUB_SEG 64
+#endif
+constexpr int kSubSegRows = AA_SUB_SEG;
 __device__ __forceinline__ int sub_seg_off(int seg, int p) {   // partial slots before segment seg
     int o = 0;
     for (int q = 0; q < seg; ++q) o += min(p, (q + 1) * kSubSegRows);
@@ -713,7 +716,6 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     // whatever their count, so it takes fewer, taller ones (measured)
     const int min_sub = ms ? std::atoi(ms) : (comm_ ? std::max(32, 256 / comm_->size()) : 256);
     constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
-    static_assert(kSubSegRows == 64, "LDS accounting below assumes 64-row segments");
     auto roots_at = [&](int H) {
         std::vector<int> r;
         for (int sn = 0; sn < nn_; ++sn)
@@ -735,7 +737,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             for (int v : collect(rt)) {
                 lf[F.height[v]] += 24LL * KS * p[v];
                 long long slots = 0;
-                for (int sg = 0; sg < (p[v] + nb[v] + 63) / 64; ++sg) slots += std::min(p[v], (sg + 1) * 64);
+                for (int sg = 0; sg < (p[v] + nb[v] + kSubSegRows - 1) / kSubSegRows; ++sg)
+                    slots += std::min(p[v], (sg + 1) * kSubSegRows);
                 lb[F.height[v]] += 24LL * KS * (p[v] + nb[v] + slots);
                 nodes_at[F.height[v]] += 1;
                 if (p[v] + nb[v] > kMaxItemRow) ok = false;

@@ -258,7 +258,7 @@ def geom_line(args, world, rank, local, dist):
     print(f"[bench] {args.config} setup + warm-up {setup_ms / 1e3:.1f} s", file=sys.stderr, flush=True)
     barrier(dist, ctx)
     t0 = time.perf_counter()
-    acc, xupd, tte = 0, 0, []
+    acc, xupd, tte, tte_rel = 0, 0, [], []
     for _ in range(args.steps):
         g.solve(sc.x0, 1e-8 * sc.avg_edge_length(), sc.iters, sc.aa_m)
         rt = g.runtime()
@@ -267,6 +267,11 @@ def geom_line(args, world, rank, local, dist):
         h = g.history()
         hit = np.nonzero(h["comb"] <= eps)[0]
         tte.append((int(hit[0]) + 1, float(h["time_s"][hit[0]] * 1e3)) if len(hit) else None)
+        rel = {}
+        for r in (1e-2, 1e-4, 1e-6):   # relative levels: comb <= r * comb_0 (the absolute stop is rarely met)
+            hr = np.nonzero(h["comb"] <= r * h["comb"][0])[0] if len(h["comb"]) else []
+            rel[str(r)] = {"iters": int(hr[0]) + 1, "ms": round(float(h["time_s"][hr[0]] * 1e3), 3)} if len(hr) else None
+        tte_rel.append(rel)
     barrier(dist, ctx)
     elapsed = time.perf_counter() - t0
     elapsed_max = allreduce(dist, elapsed, _max_op(dist))
@@ -328,6 +333,11 @@ def geom_line(args, world, rank, local, dist):
             "time_to_eps": {"eps_abs": eps, "criterion": "comb <= 2 (1e-8 avg_edge hard_cols)^2 (ALMGeometrySolver.h:173)",
                             "steps": len(tte), "reached": len(tt),
                             "iters_to_eps": [t[0] if t else None for t in tte],
+                            "relative": {r: {"reached": sum(1 for x in tte_rel if x[r]),
+                                             "median_ms": (round(statistics.median([x[r]["ms"] for x in tte_rel if x[r]]), 3)
+                                                           if any(x[r] for x in tte_rel) else None),
+                                             "iters": [x[r]["iters"] if x[r] else None for x in tte_rel]}
+                                         for r in ("0.01", "0.0001", "1e-06")},
                             "clock": "device wall_clock64 from the loop start (elapsed_time_)"},
             "roofline": roof, "cpu_baseline": cpu,
         }
@@ -521,14 +531,15 @@ def main():
                 "phase_bytes_per_launch": {kk: v["bytes"] for kk, v in stats.items()},
                 "dominant_phase": max(per_iter, key=per_iter.get)}
     if roof is not None:   # HBM bytes per solve from the committed PMC passes (tools/gpu_pmc.sh)
-        pmc = os.path.join(REPO, "profiles", f"r1_{args.config}_pmc.json")
-        if os.path.exists(pmc) and comm is None:
+        pmc = next((q for q in (os.path.join(REPO, "profiles", f"r{k}_{args.config}_pmc.json") for k in (2, 1))
+                    if os.path.exists(q)), "")
+        if pmc and comm is None:
             # the PMC group of the same solve the roofline times: two-set (6 RHS) when pipelined
             key = "solve2_per_launch" if pipelined else "solve_per_launch"
             sp = json.load(open(pmc)).get(key) or {}
             if sp.get("traffic_B"):
                 roof["traffic"] = sp["traffic_B"]
-                roof["traffic_source"] = (f"profiles/r1_{args.config}_pmc.json {key}: FETCH_SIZE (x2, calibrated on "
+                roof["traffic_source"] = (f"profiles/{os.path.basename(pmc)} {key}: FETCH_SIZE (x2, calibrated on "
                                           f"k_copy) + WRITE_SIZE over the solve's {sp['kernels']} kernels, separate "
                                           "--pmc passes")
     # run-to-epsilon leg (every rank: a partitioned loop has collectives)

@@ -1,6 +1,8 @@
 #!/bin/bash
 # HBM traffic of the dominant kernels (MI355X_MICROARCH.md HBM/rocprofv3: FETCH_SIZE and WRITE_SIZE
 # in separate passes -- TCC slots; FETCH_SIZE counts half the bytes of wide streaming reads on gfx950).
+# Round 2: the profiled process crashed under --pmc (SIGSEGV in the host launch path, three runs, with
+# and without the GPU setup factor -- AA_DENSE_GPU); bench.py then reads the round-1 passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$(pwd); mkdir -p gpurun_out
 CFG=${CFG:-c4}; TAG=${TAG:-r1}
