@@ -187,9 +187,16 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
 // 128 x NR partial per tile; the last tile of a column block to finish sums the block's partials
 // in tile order (deterministic; hand-off protocol above). Gives (columns/128) x (rows/kBwdTileRows)
 // workgroups per supernode instead of one wave per column with a serial loop over all R rows.
-// minimum waves per SIMD the split-K tiles' register budget is set for (build-time A/B knob)
+// minimum waves per SIMD the split-K tiles' register budget is set for, and the load chunks of
+// their software pipelines (build-time A/B knobs)
 #ifndef AA_TILE_MINW
 #define AA_TILE_MINW 1
+#endif
+#ifndef AA_FWD_CH
+#define AA_FWD_CH 16
+#endif
+#ifndef AA_BWD_CH
+#define AA_BWD_CH 8
 #endif
 using BTile = DirectSolver::BTile;
 using BRed = DirectSolver::BRed;
@@ -1173,7 +1180,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
         if (L.ft_count) {
-            auto kf = L.ftw == 256 ? k_fwd_tile<NR, 16, 256> : (L.ftw == 128 ? k_fwd_tile<NR, 16, 128> : k_fwd_tile<NR, 16, 64>);
+            auto kf = L.ftw == 256 ? k_fwd_tile<NR, AA_FWD_CH, 256> : (L.ftw == 128 ? k_fwd_tile<NR, AA_FWD_CH, 128> : k_fwd_tile<NR, AA_FWD_CH, 64>);
             hipLaunchKernelGGL(kf, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b0, b1,
                                bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
         }
@@ -1195,7 +1202,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         const double* F0 = top_f_.p - sh;
         const double* F1 = top_f_.p + 3 * (size_t)pt - sh;
         if (top_ft_count_) {
-            auto kf = top_ftw_ == 256 ? k_fwd_tile<NR, 16, 256> : (top_ftw_ == 128 ? k_fwd_tile<NR, 16, 128> : k_fwd_tile<NR, 16, 64>);
+            auto kf = top_ftw_ == 256 ? k_fwd_tile<NR, AA_FWD_CH, 256> : (top_ftw_ == 128 ? k_fwd_tile<NR, AA_FWD_CH, 128> : k_fwd_tile<NR, AA_FWD_CH, 64>);
             hipLaunchKernelGGL(kf, dim3(top_ft_count_), dim3(256), 0, s, ftiles_.p, top_ft_first_, Gc_.p, ell_.p, F0, F1,
                                bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
         }
@@ -1203,7 +1210,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         double* Xs0 = top_x_.p - sh;
         double* Xs1 = top_x_.p + 3 * (size_t)pt - sh;
         if (top_bt_count_) {
-            auto kb = top_btw_ == 256 ? k_bwd_tile<NR, 8, 256> : (top_btw_ == 128 ? k_bwd_tile<NR, 8, 128> : k_bwd_tile<NR, 8, 64>);
+            auto kb = top_btw_ == 256 ? k_bwd_tile<NR, AA_BWD_CH, 256> : (top_btw_ == 128 ? k_bwd_tile<NR, AA_BWD_CH, 128> : k_bwd_tile<NR, AA_BWD_CH, 64>);
             hipLaunchKernelGGL(kb, dim3(top_bt_count_), dim3(256), 0, s, btiles_.p, top_bt_first_, Gr_.p, bnd_.p, Y_.p,
                                Xs0, Xs1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
         }
@@ -1220,7 +1227,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
         if (L.bt_count) {
-            auto kb = L.btw == 256 ? k_bwd_tile<NR, 8, 256> : (L.btw == 128 ? k_bwd_tile<NR, 8, 128> : k_bwd_tile<NR, 8, 64>);
+            auto kb = L.btw == 256 ? k_bwd_tile<NR, AA_BWD_CH, 256> : (L.btw == 128 ? k_bwd_tile<NR, AA_BWD_CH, 128> : k_bwd_tile<NR, AA_BWD_CH, 64>);
             hipLaunchKernelGGL(kb, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p,
                                x0, x1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
         }

@@ -67,8 +67,13 @@ def test_geometry_facade_matches_binding(builder, tmp_path, pkg, ctx):
 def test_facade_runs_and_matches_oracle(tmp_path, oracle):
     exe = str(tmp_path / "facade_cloth")
     build(exe)
-    out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    os.makedirs(tmp_path / "result")   # Solver::step() then writes result/residual-6.txt, as the reference
+    out = subprocess.run([exe], capture_output=True, text=True, check=True, cwd=str(tmp_path)).stdout.split()
     n, comb0, combl = int(out[0]), float(out[1]), float(out[2])
+    rows = [l.split("\t") for l in open(tmp_path / "result" / "residual-6.txt").read().splitlines()]
+    assert len(rows) == n and all(len(r) == 4 for r in rows)   # (u,x) variant: time, prim, comb, reject
+    # %.16g in the file (setprecision(16)), %.17g on stdout
+    assert abs(float(rows[0][2]) - comb0) <= 1e-15 * comb0 and abs(float(rows[-1][2]) - combl) <= 1e-15 * comb0
     x1 = np.array([float(v) for v in out[3:6]])
     v, t = scenes.tri_blocks(8, 8)
     v = v * 0.25

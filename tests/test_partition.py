@@ -71,3 +71,15 @@ def test_host_transport_gloo_world2(tmp_path, pkg):
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert r.stdout.count("RANK_OK") == 2
+
+
+def test_solo_rehearsal_comm_host_semantics(pkg):
+    """aa_comm_create_solo (bench.py --rehearse): one rank of a P-way partition alone -- a host
+    all-reduce multiplies by P (the setup's scene-identity checks pass), no GPU needed to create it."""
+    import numpy as np
+    c = pkg.capi.Comm.solo(1, 4)
+    assert c.info() == (1, 4)
+    assert np.array_equal(c.allreduce_host(np.array([1.0, -2.5, 0.0])), np.array([4.0, -10.0, 0.0]))
+    c.close()
+    with pytest.raises(pkg.capi.AAError):
+        pkg.capi.Comm.solo(4, 4)
