@@ -501,6 +501,24 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ dst, const
         dst[i] = src[i];
 }
 
+// Streaming read (16 B per lane, eight loads in flight per thread, one store per thread): the
+// measured HBM read ceiling the bench reports the (read-dominated) roofline kernel against, next
+// to the spec peak (aa_ctx_bench_copy)
+__global__ __launch_bounds__(256) void k_stream_read(const double2* __restrict__ src, long long n, double* __restrict__ out) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    double acc = 0;
+    for (; i + 7 * stride < n; i += 8 * stride) {
+        double2 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = src[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += v[k].x + v[k].y;
+    }
+    for (; i < n; i += stride) acc += src[i].x + src[i].y;
+    out[blockIdx.x * (long long)blockDim.x + threadIdx.x] = acc;
+}
+
 // UX reject test (Solver.cpp:139-146) fused with the restore (Solver.cpp:150-154): every block
 // reduces the prim partials itself (identical order -> identical decision); block 0 records it.
 __global__ __launch_bounds__(kBlock) void k_check_restore_ux(Ctrl* ctrl, const double* __restrict__ red, int nb,
@@ -1212,6 +1230,27 @@ void launch_wind(const int* tris3, const int* tri_ord, const int* lvl_ptr, int n
     if (nlvl <= 0) return;
     hipLaunchKernelGGL(k_wind, dim3(1), dim3(1024), 0, s, tris3, tri_ord, lvl_ptr, nlvl, x, v, dir0, dir1, dir2, dt);
     AA_CHECK_LAUNCH();
+}
+
+double bench_stream_copy(long long bytes, int reps, hipStream_t s) {
+    const long long n = bytes / 16;
+    const int grid = 256 * 8;
+    DevBuf<double2> a((size_t)n);
+    DevBuf<double> out((size_t)grid * 256);
+    AA_HIP(hipMemsetAsync(a.p, 0, (size_t)n * 16, s));
+    hipEvent_t e0, e1;
+    AA_HIP(hipEventCreate(&e0));
+    AA_HIP(hipEventCreate(&e1));
+    hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, s, a.p, n, out.p);   // warm-up
+    AA_HIP(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, s, a.p, n, out.p);
+    AA_HIP(hipEventRecord(e1, s));
+    AA_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    AA_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;   // GB/s read
 }
 
 }  // namespace aa

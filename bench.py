@@ -302,6 +302,13 @@ def geom_line(args, world, rank, local, dist):
                 "phase_us_per_iter": {kk: round(v["avg_ms"] * 1e3, 2) for kk, v in stats.items()},
                 "phase_bytes_per_iter": {kk: v["bytes"] for kk, v in stats.items()},
                 "dominant_phase": max(stats, key=lambda kk: stats[kk]["avg_ms"])}
+        try:
+            cp = ctx.bench_copy(2 << 30)
+            roof["read_peak_measured"] = round(cp, 1)
+            roof["frac_of_read_peak"] = round(achieved / cp, 4) if cp > 0 else None
+        except Exception as e:
+            roof["read_peak_measured"] = None
+            roof["read_peak_error"] = str(e)[:120]
         z = stats["z"]
         ncon = int(rt0.n_constraints)
         roof["projections"] = {"kernel": "k_geo_z (constraint projections + rhs slot rows)",
@@ -530,6 +537,13 @@ def main():
                 "phase_us_per_launch": {kk: round(v["avg_ms"] * 1e3, 2) for kk, v in stats.items()},
                 "phase_bytes_per_launch": {kk: v["bytes"] for kk, v in stats.items()},
                 "dominant_phase": max(per_iter, key=per_iter.get)}
+        try:   # the measured HBM read ceiling (16-B/lane streaming read of 2 GiB) beside the spec
+            cp = ctx.bench_copy(2 << 30)
+            roof["read_peak_measured"] = round(cp, 1)
+            roof["frac_of_read_peak"] = round(achieved / cp, 4) if cp > 0 else None
+        except Exception as e:
+            roof["read_peak_measured"] = None
+            roof["read_peak_error"] = str(e)[:120]
     if roof is not None:   # HBM bytes per solve from the committed PMC passes (tools/gpu_pmc.sh)
         pmc = next((q for q in (os.path.join(REPO, "profiles", f"r{k}_{args.config}_pmc.json") for k in (2, 1))
                     if os.path.exists(q)), "")
