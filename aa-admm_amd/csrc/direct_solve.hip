@@ -318,7 +318,10 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
     constexpr int C = CH < per ? CH : per;
     constexpr int NC = per / C;
     const int i0 = w * per;
-    const int nloc = min(per, t.nc - i0);   // columns of this wave's slice (<= 0: none)
+    int nloc = min(per, t.nc - i0);   // columns of this wave's slice (<= 0: none)
+    // a row block inside L_PP^-1 (all 64 rows < p): its columns past the block's last row are the
+    // zero upper triangle -- not loaded (the skipped terms are exact zeros: same sums)
+    if (t.r0 + 64 <= t.p) nloc = min(nloc, t.r0 + 64 - (t.c0 + i0));
     const bool live = r < t.R && nloc > 0;
     // software pipeline over chunks of C columns, two chunks in flight (see k_bwd_tile); the
     // first two overlap the extend-add gathers that assemble the front slice
