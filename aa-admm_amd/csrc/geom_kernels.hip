@@ -242,6 +242,14 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
     return b > sl ? b : sl;
 }
 
+// (warm distance / warm triangle's first edge)^2 up to which the warm bound is used alone: the
+// greedy root-to-leaf descent (a chain of dependent node loads) only runs for points that slid
+// farther than ~8 edges from their previous triangle (and on cold starts). Measured (round 2):
+// always descending C3 995 / C5 157 it/s, never 1 056 / 154, 64 -> 1 056 / 158; 4 and 16 in between.
+#ifndef AA_WARM_TIGHT
+#define AA_WARM_TIGHT 64.0
+#endif
+
 // exact closest point on the surface. Stackless depth-first traversal over escape links
 // (`skip` = the node after a subtree): no per-lane stack, so no scratch memory. The upper
 // bound comes from `warm` (the previous iteration's triangle: points move little between ALM
@@ -260,11 +268,14 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         const double d2 = (px - qx) * (px - qx) + (py - qy) * (py - qy) + (pz - qz) * (pz - qz);
         if (d2 < best) { best = d2; best_t = t; cx = qx; cy = qy; cz = qz; }
     };
-    if (warm >= 0 && warm < S.n_tris) test_tri(warm);
-    // cold start only: with a warm triangle the greedy descent (a root-to-leaf chain of dependent
-    // loads) is skipped -- measured: C3 +6 %, C5 -2 % (its points slide further between iterations);
-    // a per-lane test of the warm bound did not help (one lane that descends holds the wave)
-    if (best_t < 0)
+    bool tight = false;
+    if (warm >= 0 && warm < S.n_tris) {
+        test_tri(warm);
+        const double* v = S.tris[warm].v;
+        const double e2 = (v[3] - v[0]) * (v[3] - v[0]) + (v[4] - v[1]) * (v[4] - v[1]) + (v[5] - v[2]) * (v[5] - v[2]);
+        tight = best <= AA_WARM_TIGHT * e2;
+    }
+    if (!tight)
     {   // greedy descent to the nearest-box leaf: a tight bound even when the point slid far
         // from its previous triangle (the warm bound alone then lets the traversal open every
         // box within that distance)
