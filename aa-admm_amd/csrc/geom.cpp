@@ -454,13 +454,23 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
         const int cnt = hg.count(), K = hg.K, P = n_params(hg.type), C = cols_of(hg.type, K);
         std::vector<int> idx((size_t)K * cnt);
         std::vector<double> prm((size_t)std::max(P, 1) * cnt, 0.0);
-        for (int e = 0; e < cnt; ++e) {
+        // reference-surface groups run in the nested-dissection order of their points: a wave's
+        // 64 queries then sit in one compact patch and their BVH traversals share most nodes
+        // (in the caller's order a wave spans a long strip of the mesh)
+        std::vector<int> ord(cnt);
+        std::iota(ord.begin(), ord.end(), 0);
+        if ((hg.type == GEO_POINT_TO_REF || hg.type == GEO_REF_SURFACE) && nd_sort_surf_)
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                return user2int_[hg.idx[(size_t)a * K]] < user2int_[hg.idx[(size_t)b * K]];
+            });
+        for (int ee = 0; ee < cnt; ++ee) {
+            const int e = ord[ee];
             for (int a = 0; a < K; ++a) {
                 const int q = user2int_[hg.idx[(size_t)e * K + a]];
-                idx[(size_t)a * cnt + e] = q;
-                pslots[q].push_back((int)(slots_ + (long long)e * K + a));
+                idx[(size_t)a * cnt + ee] = q;
+                pslots[q].push_back((int)(slots_ + (long long)ee * K + a));
             }
-            for (int p = 0; p < P; ++p) prm[(size_t)p * cnt + e] = hg.prm[(size_t)e * P + p];
+            for (int p = 0; p < P; ++p) prm[(size_t)p * cnt + ee] = hg.prm[(size_t)e * P + p];
         }
         dg.idx.upload(idx, s());
         dg.prm.upload(prm, s());

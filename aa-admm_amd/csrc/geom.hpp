@@ -6,6 +6,7 @@
 #include <map>
 #include <string>
 #include <tuple>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/aa_admm.h"
@@ -60,6 +61,9 @@ private:
         SurfDev dev() const { return SurfDev{dnodes.p, dtris.p, (int)nodes.size(), (int)tris.size()}; }
     };
     struct Reg { std::vector<int> idx; std::vector<double> coef; double tgt[3]; };
+    // reference-surface constraints processed in the points' nested-dissection order
+    // (AA_SURF_ND_ORDER=0: the caller's order)
+    bool nd_sort_surf_ = !(std::getenv("AA_SURF_ND_ORDER") && std::getenv("AA_SURF_ND_ORDER")[0] == '0');
 
     Context* ctx_;
     bool plain_ = false;
