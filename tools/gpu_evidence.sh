@@ -20,5 +20,6 @@ echo "bench part2 rc=$rc"; grep -h '^{' gpurun_out/bench_${TAG}_part2.log | cut 
 cd /tmp && export TMPDIR=/tmp
 AA_ADMM_NO_GRAPH=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_${TAG}_c4" -o run -- python3 "$R/bench.py" --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --eps-steps 0 > "$R/gpurun_out/prof_${TAG}_c4.log" 2>&1; rc=$?
 echo "prof c4 rc=$rc"; fatal $rc prof-c4
+[ "${SKIP_PMC:-0}" = 1 ] && exit 0
 cd "$R" && TAG=$TAG CFG=c4 bash tools/gpu_pmc.sh; rc=$?; fatal $rc pmc
 exit 0
