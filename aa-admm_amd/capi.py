@@ -20,7 +20,7 @@ AA_VARIANT_Z, AA_VARIANT_UX = 0, 1
 NOACC, ANDERSON = 0, 1
 
 EXPORTS = [
-    "aa_last_error", "aa_version", "aa_ctx_create", "aa_ctx_destroy", "aa_ctx_synchronize", "aa_ctx_bench_copy", "aa_lame_from_young",
+    "aa_last_error", "aa_version", "aa_ctx_create", "aa_ctx_destroy", "aa_ctx_synchronize", "aa_ctx_bench_read", "aa_lame_from_young",
     "aa_settings_default", "aa_elastic_create", "aa_elastic_destroy", "aa_elastic_add_nodes", "aa_elastic_add_tets",
     "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
     "aa_elastic_add_obstacle", "aa_elastic_set_collisions", "aa_elastic_add_wind", "aa_elastic_set_wind",
@@ -110,10 +110,10 @@ class Context:
         self.h = C.c_void_p()
         _chk(lib().aa_ctx_create(C.c_int(device), C.byref(self.h)))
 
-    def bench_copy(self, nbytes=1 << 30):
-        """GB/s of a 16-B/lane streaming read of nbytes (aa_ctx_bench_copy): the measured HBM ceiling."""
+    def bench_read(self, nbytes=1 << 30):
+        """GB/s of a 16-B/lane streaming read of nbytes (aa_ctx_bench_read): the measured HBM ceiling."""
         g = C.c_double()
-        _chk(lib().aa_ctx_bench_copy(self.h, C.c_longlong(nbytes), C.byref(g)))
+        _chk(lib().aa_ctx_bench_read(self.h, C.c_longlong(nbytes), C.byref(g)))
         return g.value
 
     def synchronize(self):

@@ -70,11 +70,11 @@ int aa_ctx_synchronize(aa_ctx ctx) {
     return guarded([&] { NEED(ctx, "null ctx"); AA_HIP(hipStreamSynchronize(ctx->c.stream)); });
 }
 
-int aa_ctx_bench_copy(aa_ctx ctx, long long bytes, double* gbps) {
+int aa_ctx_bench_read(aa_ctx ctx, long long bytes, double* gbps) {
     return guarded([&] {
-        NEED(ctx && gbps && bytes >= 16, "aa_ctx_bench_copy: bad argument");
+        NEED(ctx && gbps && bytes >= 16, "aa_ctx_bench_read: bad argument");
         AA_HIP(hipSetDevice(ctx->c.device));
-        *gbps = aa::bench_stream_copy(bytes, 10, ctx->c.stream);
+        *gbps = aa::bench_stream_read(bytes, 10, ctx->c.stream);
     });
 }
 

@@ -4,6 +4,7 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -1200,18 +1201,20 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         hipLaunchKernelGGL((k_top_front<NR>), dim3(nb), dim3(256), 0, s, top_task_d_.p, ell_.p, b0, b1, U_.p, top_f_.p,
                            ctrl, gate_reject);
         comm_->allreduce_sum(top_f_.p, top_f_.p, 3 * (size_t)K * pt, s);
-        // the tiles address the front / x by global row beg + q: shift the set-major buffers
-        const size_t sh = 3 * (size_t)top_task_.beg;
-        const double* F0 = top_f_.p - sh;
-        const double* F1 = top_f_.p + 3 * (size_t)pt - sh;
+        // the tiles address the front / x by global row beg + q: shift the set-major buffers (as
+        // addresses: the shifted base lies before the allocation and is only used with index >= sh)
+        const uintptr_t sh = 3 * (uintptr_t)top_task_.beg * sizeof(double);
+        auto shifted = [sh](double* base) { return reinterpret_cast<double*>(reinterpret_cast<uintptr_t>(base) - sh); };
+        const double* F0 = shifted(top_f_.p);
+        const double* F1 = shifted(top_f_.p + 3 * (size_t)pt);
         if (top_ft_count_) {
             auto kf = top_ftw_ == 256 ? k_fwd_tile<NR, AA_FWD_CH, 256> : (top_ftw_ == 128 ? k_fwd_tile<NR, AA_FWD_CH, 128> : k_fwd_tile<NR, AA_FWD_CH, 64>);
             hipLaunchKernelGGL(kf, dim3(top_ft_count_), dim3(256), 0, s, ftiles_.p, top_ft_first_, Gc_.p, ell_.p, F0, F1,
                                bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
         }
         AA_HIP(hipMemsetAsync(top_x_.p, 0, sizeof(double) * 3 * (size_t)K * pt, s));
-        double* Xs0 = top_x_.p - sh;
-        double* Xs1 = top_x_.p + 3 * (size_t)pt - sh;
+        double* Xs0 = shifted(top_x_.p);
+        double* Xs1 = shifted(top_x_.p + 3 * (size_t)pt);
         if (top_bt_count_) {
             auto kb = top_btw_ == 256 ? k_bwd_tile<NR, AA_BWD_CH, 256> : (top_btw_ == 128 ? k_bwd_tile<NR, AA_BWD_CH, 128> : k_bwd_tile<NR, AA_BWD_CH, 64>);
             hipLaunchKernelGGL(kb, dim3(top_bt_count_), dim3(256), 0, s, btiles_.p, top_bt_first_, Gr_.p, bnd_.p, Y_.p,

@@ -503,7 +503,7 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ dst, const
 
 // Streaming read (16 B per lane, eight loads in flight per thread, one store per thread): the
 // measured HBM read ceiling the bench reports the (read-dominated) roofline kernel against, next
-// to the spec peak (aa_ctx_bench_copy)
+// to the spec peak (aa_ctx_bench_read)
 __global__ __launch_bounds__(256) void k_stream_read(const double2* __restrict__ src, long long n, double* __restrict__ out) {
     const long long stride = (long long)gridDim.x * blockDim.x;
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -1232,7 +1232,7 @@ void launch_wind(const int* tris3, const int* tri_ord, const int* lvl_ptr, int n
     AA_CHECK_LAUNCH();
 }
 
-double bench_stream_copy(long long bytes, int reps, hipStream_t s) {
+double bench_stream_read(long long bytes, int reps, hipStream_t s) {
     const long long n = bytes / 16;
     const int grid = 256 * 8;
     DevBuf<double2> a((size_t)n);

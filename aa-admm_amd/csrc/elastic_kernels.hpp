@@ -115,7 +115,7 @@ void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b
 // dst = src (gate: !done, and reject if gate_reject)
 void launch_copy(double* dst, const double* src, long long n, const Ctrl* ctrl, int gate_reject, hipStream_t s);
 // GB/s of a 16-B/lane streaming read of `bytes` (the measured HBM read ceiling; bench.py)
-double bench_stream_copy(long long bytes, int reps, hipStream_t s);
+double bench_stream_read(long long bytes, int reps, hipStream_t s);
 // predictor: v_y += dt g (free); xbar = x + dt v; Mxbar = m xbar; xfull = xbar (free) / xpin (pinned)
 void launch_predict(int n, int nf, double* xstate, double* vstate, const double* mass, double dt, double gravity,
                     double* xbar, double* Mxbar, double* xfull, hipStream_t s);

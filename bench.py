@@ -303,7 +303,7 @@ def geom_line(args, world, rank, local, dist):
                 "phase_bytes_per_iter": {kk: v["bytes"] for kk, v in stats.items()},
                 "dominant_phase": max(stats, key=lambda kk: stats[kk]["avg_ms"])}
         try:
-            cp = ctx.bench_copy(2 << 30)
+            cp = ctx.bench_read(2 << 30)
             roof["read_peak_measured"] = round(cp, 1)
             roof["frac_of_read_peak"] = round(achieved / cp, 4) if cp > 0 else None
         except Exception as e:
@@ -538,7 +538,7 @@ def main():
                 "phase_bytes_per_launch": {kk: v["bytes"] for kk, v in stats.items()},
                 "dominant_phase": max(per_iter, key=per_iter.get)}
         try:   # the measured HBM read ceiling (16-B/lane streaming read of 2 GiB) beside the spec
-            cp = ctx.bench_copy(2 << 30)
+            cp = ctx.bench_read(2 << 30)
             roof["read_peak_measured"] = round(cp, 1)
             roof["frac_of_read_peak"] = round(achieved / cp, 4) if cp > 0 else None
         except Exception as e:

@@ -78,7 +78,7 @@ int aa_ctx_destroy(aa_ctx ctx);
 int aa_ctx_synchronize(aa_ctx ctx);
 /* Measurement hook (no reference counterpart): GB/s of a 16-B-per-lane streaming read of `bytes`
  * on the context's stream -- the measured HBM read ceiling bench.py reports beside the spec. */
-int aa_ctx_bench_copy(aa_ctx ctx, long long bytes, double* gbps);
+int aa_ctx_bench_read(aa_ctx ctx, long long bytes, double* gbps);
 
 /* ---- admm::Solver ------------------------------------------------------------------ */
 int aa_lame_from_young(double youngs, double poisson, aa_lame* out);    /* Lame(k, v)        */
