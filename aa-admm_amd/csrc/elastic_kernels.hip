@@ -322,19 +322,17 @@ __global__ __launch_bounds__(kBlock) void k_u_and_y(GroupDev g, const double* __
     constexpr int NC = ncol_of(NV), D = 3 * NC;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= g.count) return;
+    // the gradient (mode 1) needs only z: it runs before the element's gathers, so its
+    // temporaries and the gathered G / P x never hold registers together
     double F[D], Cp[D], zz[D], uu[D];
-    gather_F<NV>(g, e, xfull, nf, F, Cp);
     const double w = g.w[e];
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-        const size_t o = g.zoff + (size_t)i * g.count + e;
-        zz[i] = z[o];
-        uu[i] = u[o];
-    }
-    if (mode == 0) {
+    for (int i = 0; i < D; ++i) zz[i] = z[g.zoff + (size_t)i * g.count + e];
+    if (mode != 1) {
 #pragma unroll
-        for (int i = 0; i < D; ++i) uu[i] += w * F[i] - w * zz[i];
-    } else if (mode == 1) {
+        for (int i = 0; i < D; ++i) uu[i] = u[g.zoff + (size_t)i * g.count + e];
+    }
+    if (mode == 1) {
         double gr[D];
         if constexpr (NV == 3 || NV == 1) {
             // TriEnergyTerm::get_gradient / Collision::get_gradient throw in the reference
@@ -350,6 +348,11 @@ __global__ __launch_bounds__(kBlock) void k_u_and_y(GroupDev g, const double* __
         }
 #pragma unroll
         for (int i = 0; i < D; ++i) uu[i] = gr[i] / w;
+    }
+    gather_F<NV>(g, e, xfull, nf, F, Cp);
+    if (mode == 0) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) uu[i] += w * F[i] - w * zz[i];
     }
     if (mode != 2) {
 #pragma unroll
