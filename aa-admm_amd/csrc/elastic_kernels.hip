@@ -441,6 +441,40 @@ __global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ 
     b[3 * (size_t)i + 2] = Mxbar[3 * (size_t)i + 2] + pdt2 * s2;
 }
 
+// The same for the vertex-slot layout, one lane per node COMPONENT: lanes 3j, 3j+1, 3j+2 of a
+// wave sum x, y, z of node 21 w + j along its run (lane 63 idles), so a wave's loads cover 21
+// runs in 24-B pieces instead of 64 runs in 8-B pieces; each component is still summed in slot
+// order (the same sums as k_rhs, bit for bit)
+__global__ __launch_bounds__(kBlock) void k_rhs_slots(int nf, const int* __restrict__ ptr, const double* __restrict__ y,
+                                                      const double* __restrict__ Mxbar, double pdt2,
+                                                      double* __restrict__ b, Ctrl* ctrl, int gate_reject,
+                                                      const double* __restrict__ xsrc, double* __restrict__ xlast,
+                                                      const double* __restrict__ red_final, int nb_final) {
+    if (gated(ctrl, gate_reject)) return;
+    if (red_final && blockIdx.x == 0) {   // prim after a reject recompute; prev_prim = prim
+        __shared__ double sm[kBlock / 64];
+        const double a = block_sum_all(red_final, nb_final, sm);
+        if (threadIdx.x == 0) {
+            if (ctrl->reject) ctrl->prim = sqrt(a);
+            ctrl->prev_prim = ctrl->prim;
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    if (lane == 63) return;
+    const long long w = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long i = w * 21 + lane / 3;
+    const int c = lane % 3;
+    if (i >= nf) return;
+    const size_t o = 3 * (size_t)i + c;
+    if (xlast) xlast[o] = xsrc[o];   // last_x = curr_x (Solver.cpp:170)
+    double sum = 0;
+    const int k1 = ptr[i + 1];
+    const double* q = y + 3 * (size_t)ptr[i] + c;
+#pragma unroll 4
+    for (int k = ptr[i]; k < k1; ++k, q += 3) sum += *q;
+    b[o] = Mxbar[o] + pdt2 * sum;
+}
+
 // ------------------------------------------------------------------ control (one block)
 // 1024 threads: the kernel is latency-bound on summing a few thousand block partials
 constexpr int kCtlBlock = 1024;
@@ -1087,8 +1121,12 @@ void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const
                 double pdt2, double* b, Ctrl* ctrl, int gate_reject, hipStream_t s, const double* xsrc,
                 double* xlast, const double* red_final, int nb_final) {
     if (nf == 0) return;
-    hipLaunchKernelGGL(k_rhs, dim3(blocks_for(nf)), dim3(kBlock), 0, s, nf, ptr, row, val, y, Mxbar, pdt2, b, ctrl, gate_reject,
-                       xsrc, xlast, red_final, nb_final);
+    if (!val)
+        hipLaunchKernelGGL(k_rhs_slots, dim3(blocks_for(64 * ((nf + 20) / 21LL))), dim3(kBlock), 0, s, nf, ptr, y, Mxbar,
+                           pdt2, b, ctrl, gate_reject, xsrc, xlast, red_final, nb_final);
+    else
+        hipLaunchKernelGGL(k_rhs, dim3(blocks_for(nf)), dim3(kBlock), 0, s, nf, ptr, row, val, y, Mxbar, pdt2, b, ctrl,
+                           gate_reject, xsrc, xlast, red_final, nb_final);
     AA_CHECK_LAUNCH();
 }
 
