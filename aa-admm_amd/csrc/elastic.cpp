@@ -330,7 +330,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     // rows (AA_PART_TOP_ROWS)
     const int part_top_rows = std::getenv("AA_PART_TOP_ROWS") ? std::atoi(std::getenv("AA_PART_TOP_ROWS"))
                                                               : DirectSolver::kPartTopRows;
-    const int nd_leaf = std::getenv("AA_ND_LEAF") ? std::max(1, std::atoi(std::getenv("AA_ND_LEAF"))) : 32;
+    const int nd_leaf = default_nd_leaf(nf_);
     stamp("adjacency");
     NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::kTopRows, P > 1 ? P : 0, top_dense,
                                      part_top_rows);

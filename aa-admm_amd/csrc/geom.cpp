@@ -367,7 +367,7 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     // rows (AA_PART_TOP_ROWS)
     const int part_top_rows = std::getenv("AA_PART_TOP_ROWS") ? std::atoi(std::getenv("AA_PART_TOP_ROWS"))
                                                               : DirectSolver::kPartTopRows;
-    const int nd_leaf = std::getenv("AA_ND_LEAF") ? std::max(1, std::atoi(std::getenv("AA_ND_LEAF"))) : 32;
+    const int nd_leaf = default_nd_leaf(n_);
     if (P > 1) {   // every rank must have been handed the same problem
         double h[4] = {(double)n_, (double)hgroups_.size(), 0, 0};
         for (auto& g : hgroups_) h[2] += (double)g.idx.size();

@@ -9,6 +9,8 @@
 // so that each triangular solve is a short sequence of fully parallel kernels
 // (sparse row pulls + dense GEMVs) instead of a column-serial substitution.
 #pragma once
+#include <algorithm>
+#include <cstdlib>
 #include <cstddef>
 #include <cstdint>
 #include <functional>
@@ -36,6 +38,16 @@ struct NdTree {
     std::vector<int> part_beg, part_end;
     int top_beg = 0;
 };
+// Dissection leaf size (AA_ND_LEAF overrides): below ~150k unknowns the triangular solves are
+// bound by their per-level latency chains, and leaves of 128 cut levels (C2 cloth 25k nodes
+// 5 940 -> 6 610 it/s, C3 101k points 1 082 -> 1 126); above, leaves of 32 keep the fronts small
+// (C4 211k nodes: 364 it/s at 32, 343 at 64, 336 at 128; C5 501k points: 160 at 32 and 64, 158 at
+// 128). Measured on one MI355X, DESIGN.md §3.2.
+inline int default_nd_leaf(long long n_unknowns) {
+    if (const char* e = std::getenv("AA_ND_LEAF")) return std::max(1, std::atoi(e));
+    return n_unknowns <= 150000 ? 128 : 32;
+}
+
 // top_rows > 0: the upper levels of the tree (up to top_rows pivots) are amalgamated into
 // one dense root supernode. n_parts = P > 1: the top bisections are forced until there are P
 // parts (one per GPU of the partitioned solver; any P, uneven counts split by vertex count);
