@@ -559,18 +559,24 @@ __global__ __launch_bounds__(kBlock) void k_geo_u_plane_dyn(GeoGroupDev g, const
 }
 
 // ------------------------------------------------------------------ rhs gather
+// one lane per point COMPONENT: lanes 3j, 3j+1, 3j+2 of a wave sum x, y, z of point 21 w + j
+// (lane 63 idles), so one load instruction reads 21 slot rows whole instead of 64 rows a third
+// each; every component is summed in slot order, as with a lane per point (bit for bit)
 __global__ __launch_bounds__(kBlock) void k_geo_rhs(int n, const int* __restrict__ ptr, const int* __restrict__ slots,
                                                     const double* __restrict__ y, const double* __restrict__ rf,
                                                     double* __restrict__ b, const Ctrl* ctrl) {
     if (gated(ctrl)) return;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (lane == 63) return;
+    const long long w = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long i = w * 21 + lane / 3;
+    const int c = lane % 3;
     if (i >= n) return;
-    double s0 = rf[3 * (size_t)i], s1 = rf[3 * (size_t)i + 1], s2 = rf[3 * (size_t)i + 2];
-    for (int k = ptr[i]; k < ptr[i + 1]; ++k) {
-        const size_t r = 3 * (size_t)slots[k];
-        s0 += y[r]; s1 += y[r + 1]; s2 += y[r + 2];
-    }
-    b[3 * (size_t)i] = s0; b[3 * (size_t)i + 1] = s1; b[3 * (size_t)i + 2] = s2;
+    const size_t o = 3 * (size_t)i + c;
+    double sum = rf[o];
+    const int k1 = ptr[i + 1];
+    for (int k = ptr[i]; k < k1; ++k) sum += y[3 * (size_t)slots[k] + c];
+    b[o] = sum;
 }
 
 // ------------------------------------------------------------------ control
@@ -758,7 +764,7 @@ void launch_geo_u(const GeoGroupDev& g, const double* xnew, const double* xcur, 
 void launch_geo_rhs(int n, const int* ptr, const int* slots, const double* y, const double* rhs_fixed, double* b,
                     const Ctrl* ctrl, hipStream_t s) {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_geo_rhs, dim3(blocks_for(n)), dim3(kBlock), 0, s, n, ptr, slots, y, rhs_fixed, b, ctrl);
+    hipLaunchKernelGGL(k_geo_rhs, dim3(blocks_for(64 * ((n + 20) / 21LL))), dim3(kBlock), 0, s, n, ptr, slots, y, rhs_fixed, b, ctrl);
     AA_CHECK_LAUNCH();
 }
 
