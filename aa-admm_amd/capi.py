@@ -30,7 +30,7 @@ EXPORTS = [
     "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_create_solo", "aa_comm_destroy", "aa_comm_info",
     "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
     "aa_geom_create", "aa_geom_create_kind", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
-    "aa_geom_add_closeness", "aa_geom_setup", "aa_geom_solve", "aa_geom_get_solution", "aa_geom_get_history",
+    "aa_geom_add_closeness", "aa_geom_setup", "aa_geom_solve", "aa_geom_set_stop", "aa_geom_get_solution", "aa_geom_get_history",
     "aa_geom_runtime_info", "aa_geom_closest_points", "aa_geom_bench_iterations", "aa_geom_kernel_stats",
     "aa_test_prox", "aa_test_cod_solve", "aa_test_geom_project",
 ]
@@ -491,6 +491,11 @@ class GeomSolver:
     def solve(self, init_x, rel_eps, max_iter, m):
         x = np.ascontiguousarray(init_x, np.float64).reshape(-1)
         _chk(lib().aa_geom_solve(self.h, _dp(x), C.c_double(rel_eps), C.c_int(max_iter), C.c_int(m)))
+
+    def set_stop(self, at_eps=False, eps_rel=0.0):
+        """Run-to-epsilon for later solves (aa_geom_set_stop): stop at the reference's
+        commented-out criterion comb < rel_eps^2 hard_cols^2 2 and/or comb <= eps_rel comb_0."""
+        _chk(lib().aa_geom_set_stop(self.h, C.c_int(1 if at_eps else 0), C.c_double(eps_rel)))
 
     def solution(self):
         out = np.zeros(3 * self.n)

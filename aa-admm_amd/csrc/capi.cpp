@@ -382,6 +382,10 @@ int aa_geom_solve(aa_geom h, const double* init_x3, double rel_eps, int max_iter
     });
 }
 
+int aa_geom_set_stop(aa_geom h, int stop_at_eps, double eps_rel) {
+    return guarded([&] { NEED(h, "null handle"); h->s->set_stop(stop_at_eps, eps_rel); });
+}
+
 int aa_geom_get_solution(aa_geom h, double* x3) {
     return guarded([&] { NEED(h && x3, "null argument"); h->s->get_solution(x3); });
 }

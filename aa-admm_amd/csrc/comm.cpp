@@ -82,11 +82,14 @@ public:
         (void)hipFree(d);
         AA_HIP(e);
     }
-    // ncclAllReduce on the solver's stream is recorded into the step's hipGraph (a failed
-    // capture falls back to eager launches on every rank); AA_RCCL_NO_GRAPH=1 forces eager
+    // Eager by default: a partitioned step with RCCL launches its kernels and all-reduces
+    // without a hipGraph (the device-side control still needs no host sync, and at P ranks the
+    // kernels are long enough for the host to stay ahead). AA_RCCL_GRAPH=1 records
+    // ncclAllReduce into the step's graph instead (a failed capture on any rank drops every
+    // rank back to eager launches) -- opt-in until a multi-rank RCCL capture has been verified.
     bool capturable() const override {
-        const char* e = std::getenv("AA_RCCL_NO_GRAPH");
-        return !(e && e[0] == '1');
+        const char* e = std::getenv("AA_RCCL_GRAPH");
+        return e && e[0] == '1';
     }
 
 private:

@@ -80,7 +80,12 @@ struct Grow {   // device buffer that only grows
 
 class RocFrontBackend final : public DenseFrontBackend {
 public:
+    // dev_: the stream's device. factor() runs on OpenMP worker threads whose HIP current device
+    // is 0 unless set, so every entry point selects dev_ first: buffers, the handle and the
+    // stream must all live on the solver's GPU (ranks 1..P-1 of a partitioned run).
     explicit RocFrontBackend(hipStream_t s) : s_(s) {
+        AA_HIP(hipStreamGetDevice(s_, &dev_));
+        AA_HIP(hipSetDevice(dev_));
         rb_check(rocblas_create_handle(&h_), "rocblas_create_handle");
         rb_check(rocblas_set_stream(h_, s_), "rocblas_set_stream");
         info_.alloc(2);
@@ -96,6 +101,7 @@ public:
                 const std::vector<Child>& kids, bool keep_update, std::vector<double>& Linv, std::vector<double>& LBP,
                 std::vector<double>& M, std::vector<double>* U) override {
         std::lock_guard<std::mutex> g(mu_);
+        AA_HIP(hipSetDevice(dev_));
         const auto t0 = std::chrono::steady_clock::now();
         struct Tally {   // time inside the backend (AA_SETUP_TIMES)
             RocFrontBackend* b;
@@ -200,6 +206,7 @@ public:
 
 private:
     hipStream_t s_;
+    int dev_ = 0;
     rocblas_handle h_ = nullptr;
     mutable std::mutex mu_;
     std::map<int, std::unique_ptr<DevBuf<double>>> held_;

@@ -427,8 +427,10 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     SupernodalFactor F;
     try {
         F = factor_on_device(A, tree, s());
+    } catch (const Error&) {
+        throw;   // device / allocation failures keep their own status
     } catch (const std::runtime_error& e) {
-        throw Error(ERR_NUMERIC, e.what());
+        throw Error(ERR_NUMERIC, e.what());   // not positive definite / singular block
     }
     // Z variant with Anderson: the combined-residual solve is batched with the next iteration's
     // solve (enqueue_iteration_z); AA_Z_PIPELINE=0 restores the sequential order
@@ -943,9 +945,16 @@ void ElasticSolver::enqueue_comb_tail_z() {
 }
 
 void ElasticSolver::enqueue_iterations(int iters, bool accel) {
+    // AA_EAGER_SYNC=n (diagnostics, eager launches only): drain the stream every n iterations,
+    // bounding the depth of unsynchronised dispatches (profiler runs)
+    static const int eager_sync = [] { const char* e = std::getenv("AA_EAGER_SYNC"); return e ? std::atoi(e) : 0; }();
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    if (eager_sync > 0) AA_HIP(hipStreamIsCapturing(s(), &cst));
     for (int it = 0; it < iters; ++it) {
         if (st_.variant == AA_VARIANT_UX) enqueue_iteration_ux(accel);
         else enqueue_iteration_z(accel, it);
+        if (eager_sync > 0 && cst == hipStreamCaptureStatusNone && (it + 1) % eager_sync == 0)
+            AA_HIP(hipStreamSynchronize(s()));
     }
     if (st_.variant != AA_VARIANT_UX && accel && pipe_z_ && iters > 0) enqueue_comb_tail_z();
 }

@@ -399,6 +399,8 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     SupernodalFactor F;
     try {
         F = factor_on_device(A, tree, s());
+    } catch (const Error&) {
+        throw;   // device / allocation failures keep their own status
     } catch (const std::runtime_error& e) {
         throw Error(ERR_NUMERIC, std::string("Error: SPD solver initialization failed: ") + e.what());
     }
@@ -580,7 +582,7 @@ void GeomSolver::prepare_m(int m) {
     cur_m_ = m;
 }
 
-void GeomSolver::prologue(const double* init_x3, int max_iter, int m, int cap) {
+void GeomSolver::prologue(const double* init_x3, int max_iter, int m, int cap, double eps_abs, double eps_rel) {
     std::vector<double> x(3 * (size_t)n_);
     for (int q = 0; q < n_; ++q)
         for (int d = 0; d < 3; ++d) x[3 * (size_t)q + d] = init_x3[3 * (size_t)int2user_[q] + d];
@@ -596,6 +598,7 @@ void GeomSolver::prologue(const double* init_x3, int max_iter, int m, int cap) {
         if (g.d.warm) AA_HIP(hipMemsetAsync(g.d.warm, 0xff, (size_t)g.d.count * sizeof(int), s()));
     cap = std::max(1, cap);
     if (cap > hist_cap_) {
+        drop_graph();   // the captured chunk holds the old history pointers
         hist_cap_ = cap;
         hist_comb_.alloc(cap);
         hist_clock_.alloc(cap);
@@ -607,6 +610,8 @@ void GeomSolver::prologue(const double* init_x3, int max_iter, int m, int cap) {
     c.max_iter = max_iter;
     c.aa_m = m;
     c.aa_active = m > 0 ? 1 : 0;
+    c.eps_abs = eps_abs;
+    c.eps_rel = eps_rel;
     AA_HIP(hipMemcpyAsync(ctrl_.p, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s()));
     if (plain_) {
         // GeometrySolver::ADMM_init_variables (GeometrySolver.h:356-382): one z / x / u update
@@ -760,8 +765,23 @@ void GeomSolver::fetch_results() {
 
 // solve_ADMM (ALMGeometrySolver.h:163-283). rel_residual_eps is accepted for API parity: the
 // reference computes its threshold but the stopping test is commented out (:258-263).
+void GeomSolver::set_stop(int at_eps, double eps_rel) {
+    if (!(eps_rel >= 0.0)) throw Error(ERR_ARG, "set_stop: eps_rel must be >= 0");
+    if (plain_ && (at_eps || eps_rel > 0)) throw Error(ERR_ARG, "set_stop: ALMGeometrySolver only");
+    stop_eps_ = at_eps != 0;
+    stop_rel_ = eps_rel;
+}
+
+// z_hard_.cols(): a constraint's columns are its transformed points -- K for the mean-centred
+// kinds, K - 1 for the subtract-first ones (angle, edge; Constraint.h:73-94)
+long long GeomSolver::hard_cols() const {
+    long long n = 0;
+    for (const auto& g : hgroups_)
+        if (g.hard) n += (long long)g.count() * ((g.type == GEO_ANGLE || g.type == GEO_EDGE) ? g.K - 1 : g.K);
+    return n;
+}
+
 void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_iter, int m) {
-    (void)rel_residual_eps;
     if (!setup_done_) throw Error(ERR_STATE, "Error: solver not initialized yet");
     if (!init_x3) throw Error(ERR_ARG, "solve_ADMM: null init_x");
     if (m < 0 || m > kMaxM) throw Error(ERR_ARG, "solve_ADMM: Anderson window must be in [0, 32]");
@@ -770,7 +790,13 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
     if (!factored_) factor_and_upload(init_x3);
     prepare_m(m);
     last_init_.assign(init_x3, init_x3 + 3 * (size_t)n_);
-    prologue(init_x3, max_iter, m, max_iter);
+    double eps_abs = 0.0;
+    if (stop_eps_) {   // residual_eps of ALMGeometrySolver.h:172
+        const double cols = (double)hard_cols();
+        eps_abs = rel_residual_eps * rel_residual_eps * cols * cols * 2.0;
+    }
+    prologue(init_x3, max_iter, m, max_iter, eps_abs, stop_rel_);
+    const bool may_stop = eps_abs > 0.0 || stop_rel_ > 0.0;
     const int target = std::max(1, max_iter);
     const int chunk = std::min(target, 64);
     bool use_graph = !(std::getenv("AA_ADMM_NO_GRAPH") && std::getenv("AA_ADMM_NO_GRAPH")[0] == '1') &&
@@ -796,7 +822,8 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
     };
     // no rejection: exactly ceil(target / chunk) chunks; each rejection adds one x-update
     // (a rejected iteration is always followed by an accepted one, so <= 2 target + 1 passes)
-    const int first = (target + chunk - 1) / chunk;
+    // (with a run-to-epsilon stop: two chunks in flight, then one per done check)
+    const int first = may_stop ? std::min(2, (target + chunk - 1) / chunk) : (target + chunk - 1) / chunk;
     for (int i = 0; i < first; ++i) run_chunk();
     int passes = first * chunk;
     for (;;) {

@@ -29,6 +29,11 @@ public:
     void add_closeness(int idx, double weight, const double* target3);
     void setup(int n_points, double penalty, int spd_solver_type);
     void solve(const double* init_x3, double rel_residual_eps, int max_iter, int anderson_m);
+    // run-to-epsilon (not in the reference's loop, whose test is commented out at
+    // ALMGeometrySolver.h:258-260): at_eps stops after the accepted iteration whose combined
+    // residual falls below rel_residual_eps^2 * hard_cols^2 * 2 (ALMGeometrySolver.h:172);
+    // eps_rel > 0 also stops once comb <= eps_rel * comb of the first accepted iteration
+    void set_stop(int at_eps, double eps_rel);
     void get_solution(double* x3) const;
     int history(double* comb, double* time_s, int cap) const;
     aa_geom_runtime runtime() const { return rt_; }
@@ -85,6 +90,9 @@ private:
     std::vector<std::vector<std::pair<int, double>>> arows_;   // assembled global matrix (user ids)
     std::vector<double> rhs_fixed_user_;
     long long Zh_ = 0, slots_ = 0;
+    bool stop_eps_ = false;
+    double stop_rel_ = 0.0;
+    long long hard_cols() const;
     int red_blocks_ = 0;
 
     // device
@@ -127,7 +135,7 @@ private:
 
     void factor_and_upload(const double* init_x3);
     void prepare_m(int m);
-    void prologue(const double* init_x3, int max_iter, int m, int cap);
+    void prologue(const double* init_x3, int max_iter, int m, int cap, double eps_abs = 0.0, double eps_rel = 0.0);
     void enqueue_iteration(int m);
     void enqueue_iteration_plain(int m);
     void enqueue_u_update(double* red, hipStream_t st);

@@ -601,6 +601,13 @@ __global__ __launch_bounds__(kBlock) void k_geo_control(Ctrl* ctrl, const double
         ctrl->reject = 0;
         ctrl->aa_skip = 0;
         if (ctrl->nrec >= ctrl->max_iter) ctrl->done = 1;
+        // run-to-epsilon (GeomSolver::set_stop): the commented-out test of ALMGeometrySolver.h:258
+        // and / or a level relative to the first accepted iteration's comb
+        const double c0 = k < ctrl->cap ? hist_comb[0] : comb;
+        if ((ctrl->eps_abs > 0.0 && comb < ctrl->eps_abs) || (ctrl->eps_rel > 0.0 && comb <= ctrl->eps_rel * c0)) {
+            ctrl->eps_hit = 1;
+            ctrl->done = 1;
+        }
     } else {
         ctrl->reject = 1;
         ctrl->nrej += 1;

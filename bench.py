@@ -58,10 +58,15 @@ def parse():
                         "GPU per rank; host: host-staged gloo transport, for rehearsals with several ranks on one "
                         "GPU) or run independent replicas (none). auto = rccl when N>1")
     p.add_argument("--same-device", action="store_true", help="all ranks on GPU 0 (rehearsal with --partition host)")
-    p.add_argument("--eps-steps", type=int, default=3,
+    p.add_argument("--eps-steps", type=int, default=-1,
                    help="run-to-epsilon leg: time steps run with the reference's default cap of 500 ADMM iterations "
-                        "(Solver.hpp:62-65) and the stop comb <= 1e-8 comb_0 (0 = skip)")
+                        "(Solver.hpp:62-65) and the stop comb <= 1e-8 comb_0; -1 (default) = the same time steps as "
+                        "the timed region (--steps); 0 = skip")
     p.add_argument("--eps-cap", type=int, default=500)
+    p.add_argument("--geom-eps-cap", type=int, default=2000,
+                   help="geometry run-to-epsilon leg: accepted-iteration cap of the solves that stop at the reference's "
+                        "residual_eps (ALMGeometrySolver.h:172)")
+    p.add_argument("--geom-eps-solves", type=int, default=2, help="geometry run-to-epsilon solves (0 = skip)")
     p.add_argument("--no-secondary", action="store_true",
                    help="c4 only: skip the secondary C3 (planar-quad, configs[2]) object in the same JSON line")
     p.add_argument("--rehearse", type=int, default=0, metavar="P",
@@ -69,13 +74,38 @@ def parse():
                         "collectives replaced by local stand-ins, so the numbers are not a solution) -- the "
                         "per-rank kernel time of a P-GPU run, for the DESIGN.md scaling projection")
     p.add_argument("--rehearse-rank", type=int, default=0)
+    p.add_argument("--launch-check", action="store_true",
+                   help="print the rank layout this invocation runs with (after the --gpus N launch) and exit "
+                        "without touching a GPU -- CPU test of the multi-rank launcher")
     p.add_argument("--lq-stats", action="store_true",
                    help="c4: count the local step's L-BFGS iterations per element and its work-queue trips over "
                         "the timed steps (AA_LQ_STATS=1; atomics in the kernel, so not for the timed number)")
     return p.parse_args()
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`--gpus N` without an outside launcher: start N ranks (one process per GPU) through
+    torch.distributed.run as a CHILD process -- this process has made no HIP call yet and never
+    makes one -- relay its output (rank 0 prints the JSON line) and exit with its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"[bench] --gpus {n}: launching {n} ranks (torch.distributed.run)", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def dist_setup(n_gpus):
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} "
+                         "(the launcher and the flag must agree)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -277,6 +307,7 @@ def geom_line(args, world, rank, local, dist):
     elapsed_max = allreduce(dist, elapsed, _max_op(dist))
     # replicas: independent copies (weak scaling); partitioned: one problem (strong scaling)
     acc_all = float(acc) if comm is not None else allreduce(dist, float(acc), _sum_op(dist))
+    geps = geom_run_to_eps(g, sc, eps, args) if args.geom_eps_solves > 0 else None
     value = acc_all / elapsed_max
     roof, cpu, line = None, None, None
     if comm is not None:
@@ -346,13 +377,54 @@ def geom_line(args, world, rank, local, dist):
                                              "iters": [x[r]["iters"] if x[r] else None for x in tte_rel]}
                                          for r in ("0.01", "0.0001", "1e-06")},
                             "clock": "device wall_clock64 from the loop start (elapsed_time_)"},
+            "run_to_eps": geps,
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if geps is not None and geps["reached"]:   # the headline time-to-eps: the run-to-eps leg
+            line["time_to_eps_ms"] = geps["median_ms"]
     g.close()
     if comm is not None:
         comm.close()
     ctx.close()
     return line
+
+
+def geom_run_to_eps(g, sc, eps, args):
+    """Geometry run-to-epsilon leg: solves with a raised accepted-iteration cap that stop on the
+    device at the reference's residual_eps (ALMGeometrySolver.h:172 -- computed there, its test
+    commented out at :258-260). Relative levels (comb <= r comb_0) are read from the same curve."""
+    rel_eps = 1e-8 * sc.avg_edge_length()
+    g.set_stop(True, 0.0)
+    runs = []
+    try:
+        for _ in range(args.geom_eps_solves):
+            t0 = time.perf_counter()
+            g.solve(sc.x0, rel_eps, args.geom_eps_cap, sc.aa_m)
+            wall = (time.perf_counter() - t0) * 1e3
+            rt = g.runtime()
+            h = g.history()
+            comb, ts = h["comb"], h["time_s"]
+            hit = np.nonzero(comb < eps)[0]
+            run = {"accepted": int(rt.accepted), "x_updates": int(rt.iterations), "solve_wall_ms": round(wall, 1),
+                   "eps_abs": None if not len(hit) else {"iters": int(hit[0]) + 1, "ms": round(float(ts[hit[0]] * 1e3), 3)},
+                   "final_comb": float(comb[-1]) if len(comb) else None,
+                   "min_comb_over_eps": float(comb.min() / eps) if len(comb) else None}
+            for r in (1e-4, 1e-6, 1e-8):
+                hr = np.nonzero(comb <= r * comb[0])[0] if len(comb) else []
+                run[f"rel_{r:g}"] = {"iters": int(hr[0]) + 1, "ms": round(float(ts[hr[0]] * 1e3), 3)} if len(hr) else None
+            runs.append(run)
+    finally:
+        g.set_stop(False, 0.0)
+    hit_ms = [r["eps_abs"]["ms"] for r in runs if r["eps_abs"]]
+    out = {"criterion": "comb < 2 (1e-8 avg_edge hard_cols)^2 (ALMGeometrySolver.h:172; its stop is commented out "
+                        "at :258-260, enabled here by aa_geom_set_stop)", "eps_abs": eps, "cap_accepted": args.geom_eps_cap,
+           "solves": len(runs), "reached": len(hit_ms),
+           "median_ms": round(statistics.median(hit_ms), 3) if hit_ms else None,
+           "clock": "device wall_clock64 from the loop start (elapsed_time_)", "per_solve": runs}
+    if not hit_ms:
+        out["note"] = (f"not reached in {len(runs)}/{len(runs)} solves with cap {args.geom_eps_cap} accepted iterations; "
+                       f"min comb / eps_abs = {min(r['min_comb_over_eps'] for r in runs):.3g}")
+    return out
 
 
 def main_geom(args, world, rank, local, dist):
@@ -431,7 +503,8 @@ def run_to_eps(solver, args, state0):
     solver.set_iterations(args.eps_cap, EPS_ELASTIC)
     solver.set_state(*state0)   # the same time steps as the timed region, from the initial state
     steps = []
-    for _ in range(args.eps_steps):
+    n_eps = args.steps if args.eps_steps < 0 else args.eps_steps
+    for _ in range(n_eps):
         t0 = time.perf_counter()
         solver.step()
         wall = (time.perf_counter() - t0) * 1e3
@@ -444,8 +517,14 @@ def run_to_eps(solver, args, state0):
     solver.set_iterations(args.iters, 0.0)
     key = f"{EPS_ELASTIC:g}"
     hit = [s[key]["ms"] for s in steps if s[key] is not None]
+    its = [s[key]["iters"] for s in steps if s[key] is not None]
     out = {"eps_rel": EPS_ELASTIC, "cap": args.eps_cap, "steps": len(steps), "reached": len(hit),
            "median_ms": round(statistics.median(hit), 3) if hit else None,
+           "p90_ms": round(float(np.percentile(hit, 90)), 3) if hit else None,
+           "iters_to_eps": [s[key]["iters"] if s[key] is not None else None for s in steps],
+           "median_iters": statistics.median(its) if its else None,
+           "not_reached_note": (None if len(hit) == len(steps) else
+                                f"not reached in {len(steps) - len(hit)}/{len(steps)} steps with cap {args.eps_cap}"),
            "clock": "device wall_clock64 from the step's start (prologue included) to the end of the iteration "
                     "reaching comb <= eps_rel * comb_0", "per_step": steps}
     for e in (1e-4, 1e-6):
@@ -458,9 +537,24 @@ def run_to_eps(solver, args, state0):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     if args.rehearse > 1:   # a timing rehearsal is not a bench line: no baselines, no eps leg
-        args.no_cpu_baseline, args.no_secondary, args.eps_steps = True, True, 0
+        args.no_cpu_baseline, args.no_secondary, args.eps_steps, args.geom_eps_solves = True, True, 0, 0
     world, rank, local, dist = dist_setup(args.gpus)
+    if args.launch_check:
+        part = args.partition if args.partition != "auto" else ("rccl" if world > 1 else "none")
+        all_ranks = [None] * world
+        if dist is not None:
+            dist.all_gather_object(all_ranks, {"rank": rank, "local_rank": local})
+        else:
+            all_ranks = [{"rank": 0, "local_rank": 0}]
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": all_ranks,
+                              "parallelism": f"mesh-partitioned{world} ({part})" if part != "none" else f"replicas{world}"}))
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     if args.config in ("c3", "c5"):
         return main_geom(args, world, rank, local, dist)
     pkg = importlib.import_module("aa-admm_amd")
@@ -475,6 +569,9 @@ def main():
     t0 = time.time()
     solver.initialize(capi.settings_from_scene(sc))
     setup_ms = (time.time() - t0) * 1e3
+    if os.environ.get("AA_DUMP_MAPS"):   # diagnostics: library map to resolve a crash's frames
+        with open("/proc/self/maps") as fi, open(os.environ["AA_DUMP_MAPS"], "w") as fo:
+            fo.write(fi.read())
     print(f"[bench] {args.config} setup {setup_ms / 1e3:.1f} s", file=sys.stderr, flush=True)
     for _ in range(args.warmup):
         solver.step()
@@ -545,7 +642,7 @@ def main():
             roof["read_peak_measured"] = None
             roof["read_peak_error"] = str(e)[:120]
     if roof is not None:   # HBM bytes per solve from the committed PMC passes (tools/gpu_pmc.sh)
-        pmc = next((q for q in (os.path.join(REPO, "profiles", f"r{k}_{args.config}_pmc.json") for k in (2, 1))
+        pmc = next((q for q in (os.path.join(REPO, "profiles", f"r{k}_{args.config}_pmc.json") for k in (3, 2, 1))
                     if os.path.exists(q)), "")
         if pmc and comm is None:
             # the PMC group of the same solve the roofline times: two-set (6 RHS) when pipelined
@@ -557,7 +654,7 @@ def main():
                                           f"k_copy) + WRITE_SIZE over the solve's {sp['kernels']} kernels, separate "
                                           "--pmc passes")
     # run-to-epsilon leg (every rank: a partitioned loop has collectives)
-    eps_leg = run_to_eps(solver, args, (x0, v0)) if args.eps_steps > 0 else None
+    eps_leg = run_to_eps(solver, args, (x0, v0)) if args.eps_steps != 0 else None
     rt = solver.runtime()
     solver.close()
     if comm is not None:

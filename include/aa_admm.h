@@ -143,8 +143,9 @@ int aa_elastic_runtime(aa_elastic h, aa_runtime* out);                   /* runt
 /* ---- multi-GPU: mesh partitioned over the GPUs of one node -----------
  * The reference is one OpenMP process (no MPI/NCCL); this is new surface. One process per GPU;
  * every rank builds the SAME scene through the calls above, attaches a communicator, then
- * initialize() partitions the free nodes by nested dissection into `size` parts (a power of
- * two) plus the shared separator rows, and each rank keeps the elements of its part. step()
+ * initialize() partitions the free nodes by nested dissection into `size` parts (any count
+ * >= 1: an odd count is split floor/ceil by vertex count at each forced bisection) plus the
+ * shared separator rows, and each rank keeps the elements of its part. step()
  * runs the identical reference iteration on all ranks (all-reduced residuals, Anderson dot
  * products and separator rows of the global solve); afterwards every rank holds the full
  * x and v. */
@@ -247,6 +248,13 @@ int aa_geom_setup(aa_geom h, int n_points, double penalty, int spd_solver_type);
  * iterations; Anderson_m = 0 runs plain ADMM. */
 int aa_geom_solve(aa_geom h, const double* init_x3, double rel_residual_eps, int max_iter, int anderson_m);
 int aa_geom_get_solution(aa_geom h, double* x3);                               /* get_solution()      */
+/* Run-to-epsilon for later solves (new surface; the reference computes residual_eps at
+ * ALMGeometrySolver.h:172 but its stopping test is commented out at :258-260). stop_at_eps = 1
+ * ends the loop after the first accepted iteration whose combined residual is below
+ * rel_residual_eps^2 * hard_cols^2 * 2; eps_rel > 0 also ends it once comb <= eps_rel * comb of
+ * the first accepted iteration. (0, 0) = the reference loop (max_iter accepted iterations).
+ * ALMGeometrySolver only. */
+int aa_geom_set_stop(aa_geom h, int stop_at_eps, double eps_rel);
 /* function_values_ (combined residual per accepted iteration) and elapsed_time_ (s since the
  * loop started, device clock). Returns the count in *n (<= cap copied). */
 int aa_geom_get_history(aa_geom h, double* comb, double* time_s, int cap, int* n);

@@ -219,6 +219,9 @@ public:
         if (k) check(aa_geom_get_history(h_, function_values_.data(), elapsed_time_.data(), k, &k));
     }
     const Matrix3X& get_solution() const { return x_; }
+    // extension (aa_geom_set_stop): run later solves to the residual_eps the reference computes
+    // (ALMGeometrySolver.h:172) but never tests, and/or to eps_rel * the first comb
+    void set_stop_at_eps(bool stop_at_eps, Scalar eps_rel = 0) { check(aa_geom_set_stop(h_, stop_at_eps ? 1 : 0, eps_rel)); }
 
     // save(Anderson_m) (ALMGeometrySolver.h:343-365, GeometrySolver.h:322-346): "elapsed\tvalue"
     // rows, 16 digits, to ./result/residual-<m>.txt or ./result/residual-no.txt

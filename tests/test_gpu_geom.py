@@ -158,3 +158,39 @@ def test_gpu_geom_error_behaviour(pkg, ctx):
     assert e.value.code == -4
     g.close()
 
+
+
+def test_gpu_geom_run_to_eps_stop(pkg, ctx):
+    """aa_geom_set_stop: the run-to-epsilon mode of the bench's geometry leg. The reference
+    computes residual_eps = rel_eps^2 cols^2 2 (ALMGeometrySolver.h:172) but its test is commented
+    out (:258-260); enabled here it ends the loop after the first accepted iteration below it. The
+    stopped run is a bit-identical prefix of the uncapped run; a raised cap on the same solver
+    (history re-allocated, captured chunk dropped) is the round-3 regression case."""
+    sc = pkg.geom_scenes.pq_heightfield(20, 20, iters=60, aa_m=6, noise=0.3)
+    full, g = pkg.capi.run_geom(ctx, sc)
+    c = full["comb"]
+    assert len(c) == 60
+    cols = g.runtime().hard_cols
+    # relative level: comb <= r comb_0
+    r = c[20] / c[0] * (1 + 1e-9)
+    k = int(np.nonzero(c <= r * c[0])[0][0])
+    g.set_stop(False, r)
+    g.solve(sc.x0, 1e-8, 500, sc.aa_m)
+    h = g.history()["comb"]
+    assert len(h) == k + 1 and np.array_equal(h, c[:k + 1])
+    # the reference's absolute residual_eps
+    thr = c[30] * (1 + 1e-9)
+    j = int(np.nonzero(c < thr)[0][0])
+    g.set_stop(True, 0.0)
+    g.solve(sc.x0, np.sqrt(thr / 2.0) / cols, 500, sc.aa_m)
+    h = g.history()["comb"]
+    assert len(h) == j + 1 and np.array_equal(h, c[:j + 1])
+    assert g.runtime().accepted == j + 1
+    # stop off again: the reference loop, max_iter accepted iterations
+    g.set_stop(False, 0.0)
+    g.solve(sc.x0, 1e-8, 60, sc.aa_m)
+    assert np.array_equal(g.history()["comb"], c)
+    assert np.array_equal(g.solution(), full["x"])
+    with pytest.raises(Exception):
+        g.set_stop(False, -1.0)
+    g.close()

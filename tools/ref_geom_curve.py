@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Reference convergence curve of a geometry config (container only: runs oracle/_ref/ref_geom,
+the reference's ALMGeometrySolver compiled from /root/reference): comb per accepted iteration
+against the reference's residual_eps (ALMGeometrySolver.h:172), to show whether the reference
+itself reaches it. Writes profiles/<tag>.json.
+
+    python tools/ref_geom_curve.py --config c3 --iters 1000 --tag r3_c3_ref_curve
+"""
+import argparse
+import importlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import refio  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c3", choices=["c3", "c5"])
+ap.add_argument("--iters", type=int, default=1000)
+ap.add_argument("--nx", type=int, default=0)
+ap.add_argument("--tag", default="r3_c3_ref_curve")
+a = ap.parse_args()
+gs = importlib.import_module("aa-admm_amd.geom_scenes")
+if a.config == "c3":
+    n = a.nx or 317
+    sc = gs.pq_heightfield(n, n, iters=a.iters, aa_m=10, noise=0.3)
+else:
+    n = a.nx or 707
+    sc = gs.wire_grid(n, n, iters=a.iters, aa_m=20)
+eps = 2.0 * (1e-8 * sc.avg_edge_length() * sc.hard_cols()) ** 2
+with tempfile.TemporaryDirectory() as tmp:
+    refio.write_geom_scene(sc, os.path.join(tmp, "s.bin"))
+    t0 = time.time()
+    r = subprocess.run([os.path.join(REPO, "oracle", "_ref", "ref_geom"), "s.bin", "o.bin"], cwd=tmp,
+                       capture_output=True, text=True)
+    wall = time.time() - t0
+    if r.returncode:
+        sys.exit(r.stderr[-2000:])
+    res = refio.read_geom_result(os.path.join(tmp, "o.bin"), sc.n_points)
+comb = np.asarray(res["comb"])
+idx = sorted(set([0, 1, 2, 4, 9, 19, 49, 99, 199, 299, 499, 699, 999, 1499, 1999, len(comb) - 1]) & set(range(len(comb))))
+out = {"config": a.config, "scene": sc.name, "points": sc.n_points, "hard_cols": sc.hard_cols(), "anderson_m": sc.aa_m,
+       "accepted_iters": int(len(comb)), "eps_abs": eps, "comb0": float(comb[0]),
+       "min_comb": float(comb.min()), "min_comb_over_eps": float(comb.min() / eps),
+       "reached_eps_abs": bool((comb < eps).any()),
+       "first_iter_below": {f"{r:g}": (int(np.nonzero(comb <= r * comb[0])[0][0]) + 1 if (comb <= r * comb[0]).any() else None)
+                            for r in (1e-2, 1e-4, 1e-6, 1e-8)},
+       "curve": {str(i + 1): float(comb[i]) for i in idx},
+       "loop_s": res["loop_s"], "setup_s": res["setup_s"], "wall_s": round(wall, 1),
+       "omp_threads": os.environ.get("OMP_NUM_THREADS", str(os.cpu_count())),
+       "source": "oracle/_ref/ref_geom (reference ALMGeometrySolver compiled from its own sources), this container's CPU"}
+json.dump(out, open(os.path.join(REPO, "profiles", a.tag + ".json"), "w"), indent=1)
+print(json.dumps({k: v for k, v in out.items() if k != "curve"}))
