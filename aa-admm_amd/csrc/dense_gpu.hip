@@ -148,6 +148,7 @@ public:
             AA_CHECK_LAUNCH();
             AA_HIP(hipStreamSynchronize(s_));   // before the staging buffers / held matrix are reused
         }
+        if (reduce_front) reduce_front(F, (size_t)f * f);   // partitioned top: the ranks' partial fronts summed
         // ---- partial factorization
         const double one = 1.0, mone = -1.0;
         rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
@@ -223,12 +224,23 @@ std::unique_ptr<DenseFrontBackend> make_gpu_front_backend(hipStream_t s) {
     return b;
 }
 
-SupernodalFactor factor_on_device(const CsrMatrix& A, const NdTree& tree, hipStream_t s) {
+std::unique_ptr<PartFactor> make_part_factor(Comm* comm, int rank, hipStream_t s) {
+    const char* e = std::getenv("AA_PART_FACTOR");
+    if (!comm || comm->size() < 2 || comm->rehearsal() || (e && e[0] == '0')) return nullptr;
+    auto pf = std::make_unique<PartFactor>();
+    pf->my_part = rank;
+    pf->first = rank == 0;
+    pf->reduce_host = [comm](double* p, size_t n) { comm->allreduce_sum_host(p, n); };
+    pf->reduce_dev = [comm, s](double* p, size_t n) { comm->allreduce_sum(p, p, n, s); };
+    return pf;
+}
+
+SupernodalFactor factor_on_device(const CsrMatrix& A, const NdTree& tree, hipStream_t s, const PartFactor* part) {
     const char* e = std::getenv("AA_DENSE_GPU");
-    if (e && e[0] == '0') return multifrontal_cholesky(A, tree, nullptr);
+    if (e && e[0] == '0') return multifrontal_cholesky(A, tree, nullptr, part);
     auto b = make_gpu_front_backend(s);
     const auto t0 = std::chrono::steady_clock::now();
-    SupernodalFactor F = multifrontal_cholesky(A, tree, b.get());
+    SupernodalFactor F = multifrontal_cholesky(A, tree, b.get(), part);
     if (const char* t = std::getenv("AA_SETUP_TIMES"); t && t[0] == '1') {
         const auto* rb = static_cast<const RocFrontBackend*>(b.get());
         std::fprintf(stderr, "[setup]   factor %.1f ms: %d fronts on the GPU (%.1f ms inside the backend), %.1f GFLOP\n",

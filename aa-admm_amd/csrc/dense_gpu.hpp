@@ -4,6 +4,7 @@
 
 #include <memory>
 
+#include "comm.hpp"
 #include "spd_direct.hpp"
 
 namespace aa {
@@ -13,6 +14,13 @@ namespace aa {
 std::unique_ptr<DenseFrontBackend> make_gpu_front_backend(hipStream_t s);
 
 // multifrontal_cholesky with the GPU backend (or on the host only, AA_DENSE_GPU=0)
-SupernodalFactor factor_on_device(const CsrMatrix& A, const NdTree& tree, hipStream_t s);
+// The partitioned factorization of rank `rank` over `comm` (PartFactor; part r = rank r): host
+// fronts summed by comm's host all-reduce, device fronts by its all-reduce on stream s.
+// Null (every rank factors the whole matrix) for a rehearsal communicator, one rank, or
+// AA_PART_FACTOR=0.
+std::unique_ptr<PartFactor> make_part_factor(Comm* comm, int rank, hipStream_t s);
+
+// part: partitioned (one rank's share, see PartFactor)
+SupernodalFactor factor_on_device(const CsrMatrix& A, const NdTree& tree, hipStream_t s, const PartFactor* part = nullptr);
 
 }  // namespace aa

@@ -77,12 +77,13 @@ __device__ __forceinline__ void zero(double* a) {
 // front row q of a supernode (any record with beg, p, ell_w, ell_off): [b_P ; 0]_q + the
 // children's update entries landing on it (ELL pull list: ell_w offsets into U per row, -1 =
 // none; fixed order -> deterministic)
+// (ext_off: B0 / B1 hold rows from ext_off on -- the partitioned top's summed front)
 template <int NR, class N>
 __device__ __forceinline__ void front_row(const N& t, int q, const long long* __restrict__ ell,
                                           const double* __restrict__ B0, const double* __restrict__ B1,
-                                          const double* __restrict__ U, double* a) {
+                                          const double* __restrict__ U, double* a, int ext_off = 0) {
     zero<NR>(a);
-    if (q < t.p) ld_ext<NR>(B0, B1, (size_t)(t.beg + q), a);
+    if (q < t.p) ld_ext<NR>(B0, B1, (size_t)(t.beg + q - ext_off), a);
     const long long* e = ell + t.ell_off + (size_t)q * t.ell_w;
     for (int k = 0; k < t.ell_w; ++k) {
         const long long o = e[k];
@@ -206,7 +207,8 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_tile(const BTile* __r
                                                   const int* __restrict__ bnd, const double* __restrict__ Y,
                                                   double* __restrict__ X0, double* __restrict__ X1,
                                                   double* __restrict__ part, const BRed* __restrict__ reds,
-                                                  int* __restrict__ cnt, const Ctrl* ctrl, int gate_reject) {
+                                                  int* __restrict__ cnt, const Ctrl* ctrl, int gate_reject,
+                                                  int ext_off) {
     if (solve_gated(ctrl, gate_reject)) return;
     constexpr int W = 2 * NR;   // accumulators per lane: columns c and c + 1
     __shared__ double v[NR * kBwdTileRows];
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_tile(const BTile* __r
         for (int k = 0; k < rd.nt; ++k, q += W * 64)
 #pragma unroll
             for (int m = 0; m < W; ++m) b[m] += q[m];
-        const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane);
+        const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane - ext_off);
         st_ext<NR>(X0, X1, xo, b);
         if (2 * lane + 1 < rd.nc) st_ext<NR>(X0, X1, xo + 1, b + NR);
     }
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
                                                   const double* __restrict__ B1, double* __restrict__ part,
                                                   const FRed* __restrict__ reds, int* __restrict__ cnt,
                                                   double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
-                                                  int gate_reject) {
+                                                  int gate_reject, int ext_off) {
     if (solve_gated(ctrl, gate_reject)) return;
     __shared__ double f[NR * kFwdTileCols];
     __shared__ double red[3][NR * 64];
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
     }
     // this tile's slice of the front f_P = b_P + extend-add of the children's update vectors
     for (int i = tid; i < kFwdTileCols; i += 256) {
-        if (i < t.nc) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i);
+        if (i < t.nc) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i, ext_off);
         else zero<NR>(f + NR * i);   // columns past the tile: finite zeros
     }
     __syncthreads();
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
     if (lane < rd.nr) {
         const int rr = rd.r0 + lane;
         double fr[NR];   // a boundary row's front value: gathered before the partials are summed
-        if (rr >= rd.p) front_row<NR>(rd, rr, ell, B0, B1, U, fr);
+        if (rr >= rd.p) front_row<NR>(rd, rr, ell, B0, B1, U, fr, ext_off);
         double b[NR];
         zero<NR>(b);
         const double* q = part + (NR / 3) * rd.poff + NR * lane;
@@ -398,6 +400,224 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
         }
     }
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Packed split-K tiles (the default): the same tiles, partials and reductions as k_fwd_tile /
+// k_bwd_tile -- so the same sums in the same order, bit-identical -- but the factor entries of a
+// tile come from its own contiguous block of Gt (DirectSolver::build packs them), laid out in the
+// order the tile's waves consume them: each wave streams a sequential run of 1-KB rows (64 lanes
+// x 16 B, two columns or two rows' entries per lane). The column-major / row-major copies put a
+// tile's 64 x 256 entries in 256 pieces of 512 B (or 1 KB) at strides of the supernode's height,
+// spread over several MB: a DRAM-page and TLB pattern a contiguous stream avoids.
+template <int NR, int CH, int kFwdTileCols>
+__global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __restrict__ tiles, int first,
+                                                   const double* __restrict__ Gt, const long long* __restrict__ ell,
+                                                   const double* __restrict__ B0, const double* __restrict__ B1,
+                                                   double* __restrict__ part, const FRed* __restrict__ reds,
+                                                   int* __restrict__ cnt, double* __restrict__ Y, double* __restrict__ U,
+                                                   const Ctrl* ctrl, int gate_reject, int ext_off) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    __shared__ double f[NR * kFwdTileCols];
+    __shared__ double red[3][NR * 64];
+    const FTile t = tiles[first + blockIdx.x];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, w = tid >> 6;
+    constexpr int per = kFwdTileCols / 4;   // columns of a wave's slice (even)
+    constexpr int C = CH < per ? CH : per;   // columns per chunk (even)
+    constexpr int NC = per / C;
+    constexpr int C2 = C / 2;                // 16-B loads per chunk: column pairs
+    const int i0 = w * per;
+    int nloc = min(per, t.nc - i0);
+    if (t.r0 + 64 <= t.p) nloc = min(nloc, t.r0 + 64 - (t.c0 + i0));   // zero upper triangle: not loaded
+    const bool live = nloc > 0;   // wave-uniform: rows past R read the block's zero padding
+    const int qmax = (nloc - 1) >> 1;   // last pair with a live column (later indices re-read it: cache hits)
+    const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * (per / 2) * 64 + lane;
+    double2 ga[C2], gb[C2];
+    auto ld = [&](double2* g, int k) {
+#pragma unroll
+        for (int q = 0; q < C2; ++q) g[q] = G[(size_t)min(k * C2 + q, qmax) * 64];
+    };
+    if (live) {
+        ld(ga, 0);
+        if (NC > 1) ld(gb, 1);
+    }
+    for (int i = tid; i < kFwdTileCols; i += 256) {
+        if (i < t.nc) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i, ext_off);
+        else zero<NR>(f + NR * i);
+    }
+    __syncthreads();
+    double a[NR];
+    zero<NR>(a);
+    if (live) {
+        auto use = [&](const double2* g, int k) {
+#pragma unroll
+            for (int q = 0; q < C2; ++q) {
+                const int i = k * C + 2 * q;
+                const double g0 = i < nloc ? g[q].x : 0.0;
+                const double g1 = i + 1 < nloc ? g[q].y : 0.0;
+#pragma unroll
+                for (int m = 0; m < NR; ++m) a[m] += g0 * f[NR * (i0 + i) + m];
+#pragma unroll
+                for (int m = 0; m < NR; ++m) a[m] += g1 * f[NR * (i0 + i + 1) + m];
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (k & 1) { use(gb, k); if (k + 2 < NC) ld(gb, k + 2); }
+            else       { use(ga, k); if (k + 2 < NC) ld(ga, k + 2); }
+        }
+    }
+    if (w > 0)
+#pragma unroll
+        for (int k = 0; k < NR; ++k) red[w - 1][NR * lane + k] = a[k];
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int k = 0; k < NR; ++k) a[k] += red[q][NR * lane + k];
+    double* o = part + (NR / 3) * t.poff + NR * lane;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) st_sc1(o + k, a[k]);
+    const FRed rd = reds[t.rid];
+    if (!arrive_last(cnt + t.rid, rd.nt, lane)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane < rd.nr) {
+        const int rr = rd.r0 + lane;
+        double fr[NR];
+        if (rr >= rd.p) front_row<NR>(rd, rr, ell, B0, B1, U, fr, ext_off);
+        double b[NR];
+        zero<NR>(b);
+        const double* q = part + (NR / 3) * rd.poff + NR * lane;
+#pragma unroll 8
+        for (int k = 0; k < rd.nt; ++k, q += NR * 64)
+#pragma unroll
+            for (int m = 0; m < NR; ++m) b[m] += q[m];
+        if (rr < rd.p) {
+            double* y = Y + NR * (size_t)(rd.beg + rr);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) y[k] = b[k];
+        } else {
+            double* u = U + (NR / 3) * rd.uoff + NR * (size_t)(rr - rd.p);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) u[k] = fr[k] - b[k];
+        }
+    }
+    if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NR, int CH, int kBwdTileRows>
+__global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __restrict__ tiles, int first,
+                                                   const double* __restrict__ Gt, const int* __restrict__ bnd,
+                                                   const double* __restrict__ Y, double* __restrict__ X0,
+                                                   double* __restrict__ X1, double* __restrict__ part,
+                                                   const BRed* __restrict__ reds, int* __restrict__ cnt, const Ctrl* ctrl,
+                                                   int gate_reject, int ext_off) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    constexpr int W = 2 * NR;
+    __shared__ double v[NR * kBwdTileRows];
+    __shared__ double red[3][W * 64];
+    const BTile t = tiles[first + blockIdx.x];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, w = tid >> 6;
+    constexpr int per = kBwdTileRows / 4;
+    constexpr int C = CH < per ? CH : per;
+    constexpr int NC = per / C;
+    const int i0 = w * per;
+    const int nloc = min(per, t.nr - i0);
+    const bool live = nloc > 0;   // wave-uniform: columns past p read the block's zero padding
+    const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * per * 64 + lane;
+    double2 ga[C], gb[C];
+    auto ld = [&](double2* g, int k) {
+#pragma unroll
+        for (int q = 0; q < C; ++q) g[q] = G[(size_t)min(k * C + q, nloc - 1) * 64];
+    };
+    if (live) {
+        ld(ga, 0);
+        if (NC > 1) ld(gb, 1);
+    }
+    for (int i = tid; i < kBwdTileRows; i += 256) {
+        if (i < t.nr) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
+        else zero<NR>(v + NR * i);
+    }
+    __syncthreads();
+    double a[W];
+    zero<W>(a);
+    if (live) {
+        auto use = [&](const double2* g, int k) {
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                const int i = k * C + q;
+                const double2 gq = i < nloc ? g[q] : make_double2(0.0, 0.0);
+#pragma unroll
+                for (int m = 0; m < NR; ++m) {
+                    const double vk = v[NR * (i0 + i) + m];
+                    a[m] += gq.x * vk;
+                    a[NR + m] += gq.y * vk;
+                }
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (k & 1) { use(gb, k); if (k + 2 < NC) ld(gb, k + 2); }
+            else       { use(ga, k); if (k + 2 < NC) ld(ga, k + 2); }
+        }
+    }
+    if (w > 0)
+#pragma unroll
+        for (int k = 0; k < W; ++k) red[w - 1][W * lane + k] = a[k];
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int k = 0; k < W; ++k) a[k] += red[q][W * lane + k];
+    double* o = part + (NR / 3) * t.poff + W * lane;
+#pragma unroll
+    for (int k = 0; k < W; ++k) st_sc1(o + k, a[k]);
+    const BRed rd = reds[t.rid];
+    if (!arrive_last(cnt + t.rid, rd.nt, lane)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (2 * lane < rd.nc) {
+        double b[W];
+        zero<W>(b);
+        const double* q = part + (NR / 3) * rd.poff + W * lane;
+#pragma unroll 4
+        for (int k = 0; k < rd.nt; ++k, q += W * 64)
+#pragma unroll
+            for (int m = 0; m < W; ++m) b[m] += q[m];
+        const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane - ext_off);
+        st_ext<NR>(X0, X1, xo, b);
+        if (2 * lane + 1 < rd.nc) st_ext<NR>(X0, X1, xo + 1, b + NR);
+    }
+    if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// packing (setup): one workgroup per tile, every entry of its block written (zeros outside the
+// supernode), read from the row-major copy Gr (row stride ldr = p rounded up to even)
+__global__ void k_pack_ftiles(const FTile* __restrict__ tiles, const int* __restrict__ width,
+                              const double* __restrict__ Gr, double* __restrict__ Gt) {
+    const FTile t = tiles[blockIdx.x];
+    const int W = width[blockIdx.x], per2 = W / 8, ldr = t.p + (t.p & 1);
+    const long long n = 64LL * W;
+    for (long long idx = threadIdx.x; idx < n; idx += blockDim.x) {
+        const int j = (int)(idx & 1), r = (int)((idx >> 1) & 63);
+        const long long rest = idx >> 7;
+        const int w = (int)(rest / per2), cp = (int)(rest % per2);
+        const int c = t.c0 + w * (W / 4) + 2 * cp + j, row = t.r0 + r;
+        Gt[t.toff + idx] = (c < t.c0 + t.nc && row < t.R) ? Gr[t.goff + (size_t)row * ldr + c] : 0.0;
+    }
+}
+__global__ void k_pack_btiles(const BTile* __restrict__ tiles, const int* __restrict__ width,
+                              const double* __restrict__ Gr, double* __restrict__ Gt) {
+    const BTile t = tiles[blockIdx.x];
+    const int W = width[blockIdx.x], R = t.p + t.nb;
+    const long long n = 128LL * W;
+    for (long long idx = threadIdx.x; idx < n; idx += blockDim.x) {
+        const int j = (int)(idx & 1), lane = (int)((idx >> 1) & 63), q = (int)(idx >> 7);
+        const int row = t.r0 + q, col = t.c0 + 2 * lane + j;
+        Gt[t.toff + idx] = (q < t.nr && row < R && col < t.p) ? Gr[t.goff + (size_t)row * t.ldr + col] : 0.0;
+    }
 }
 
 // partitioned dense top: this GPU's share of the top front f_T = b_T + its own children's
@@ -885,6 +1105,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     std::vector<BRed> breds;
     std::vector<FTile> ftiles;
     std::vector<FRed> freds;
+    std::vector<int> fwid, bwid;   // tile widths (packing)
     long long poff = 0;
     auto mk = [&](int sn, int r0, int nr) {
         Task t{};
@@ -967,6 +1188,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     ft.rid = (int)freds.size();
                     poff += 3 * 64;
                     ftiles.push_back(ft);
+                    fwid.push_back(ftw);
                     ++rd.nt;
                 }
                 freds.push_back(rd);
@@ -1001,6 +1223,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     bt.rid = (int)breds.size();
                     poff += 6 * 64;
                     btiles.push_back(bt);
+                    bwid.push_back(btw);
                     ++rd.nt;
                 }
                 breds.push_back(rd);
@@ -1060,6 +1283,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 ft.rid = (int)freds.size();
                 poff += 3 * 64;
                 ftiles.push_back(ft);
+                fwid.push_back(top_ftw_);
                 ++rd.nt;
             }
             freds.push_back(rd);
@@ -1080,6 +1304,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 bt.rid = (int)breds.size();
                 poff += 6 * 64;
                 btiles.push_back(bt);
+                bwid.push_back(top_btw_);
                 ++rd.nt;
             }
             breds.push_back(rd);
@@ -1123,6 +1348,38 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             AA_HIP(hipStreamSynchronize(s));
         }
     }
+    // packed tiles: every tile's block in consumption order (see k_fwd_ptile), built on the
+    // device from Gr; AA_SOLVE_PACKED=0 keeps the tiles on the strided copies (A/B)
+    {
+        const char* pk = std::getenv("AA_SOLVE_PACKED");
+        packed_ = !(pk && pk[0] == '0');
+    }
+    if (packed_ && (!ftiles.empty() || !btiles.empty())) {
+        long long to = 0;
+        for (size_t i = 0; i < ftiles.size(); ++i) { ftiles[i].toff = to; to += 64LL * fwid[i]; }
+        for (size_t i = 0; i < btiles.size(); ++i) { btiles[i].toff = to; to += 128LL * bwid[i]; }
+        Gt_.alloc((size_t)to);
+        DevBuf<FTile> dft;
+        DevBuf<BTile> dbt;
+        DevBuf<int> dfw, dbw;
+        if (!ftiles.empty()) {
+            dft.upload(ftiles, s);
+            dfw.upload(fwid, s);
+            hipLaunchKernelGGL(k_pack_ftiles, dim3((unsigned)ftiles.size()), dim3(256), 0, s, dft.p, dfw.p, Gr_.p, Gt_.p);
+            AA_CHECK_LAUNCH();
+        }
+        if (!btiles.empty()) {
+            dbt.upload(btiles, s);
+            dbw.upload(bwid, s);
+            hipLaunchKernelGGL(k_pack_btiles, dim3((unsigned)btiles.size()), dim3(256), 0, s, dbt.p, dbw.p, Gr_.p, Gt_.p);
+            AA_CHECK_LAUNCH();
+        }
+        AA_HIP(hipStreamSynchronize(s));
+        if (stats) std::fprintf(stderr, "[solve] packed tiles: %zu forward, %zu backward, %.1f MB\n", ftiles.size(),
+                                btiles.size(), 8e-6 * (double)to);
+    } else {
+        packed_ = false;
+    }
     tasks_.upload(tasks, s);
     btiles_.upload(btiles, s);
     ftiles_.upload(ftiles, s);
@@ -1164,6 +1421,35 @@ void DirectSolver::solve2(const double* b0, double* x0, const double* b1, double
     solve_nr<6>(b0, x0, b1, x1, ctrl, gate_reject, s);
 }
 
+// one launch of split-K tiles (width w = forward columns / backward rows per tile): packed or on
+// the strided copies
+template <int NR>
+void DirectSolver::launch_ftiles(int w, int count, int first, const double* b0, const double* b1, int ext_off,
+                                 const Ctrl* ctrl, int gate_reject, hipStream_t s) {
+    if (packed_) {
+        auto kf = w == 256 ? k_fwd_ptile<NR, AA_FWD_CH, 256> : (w == 128 ? k_fwd_ptile<NR, AA_FWD_CH, 128> : k_fwd_ptile<NR, AA_FWD_CH, 64>);
+        hipLaunchKernelGGL(kf, dim3(count), dim3(256), 0, s, ftiles_.p, first, Gt_.p, ell_.p, b0, b1, bpart_.p, freds_.p,
+                           fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, ext_off);
+    } else {
+        auto kf = w == 256 ? k_fwd_tile<NR, AA_FWD_CH, 256> : (w == 128 ? k_fwd_tile<NR, AA_FWD_CH, 128> : k_fwd_tile<NR, AA_FWD_CH, 64>);
+        hipLaunchKernelGGL(kf, dim3(count), dim3(256), 0, s, ftiles_.p, first, Gc_.p, ell_.p, b0, b1, bpart_.p, freds_.p,
+                           fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, ext_off);
+    }
+}
+template <int NR>
+void DirectSolver::launch_btiles(int w, int count, int first, double* x0, double* x1, int ext_off, const Ctrl* ctrl,
+                                 int gate_reject, hipStream_t s) {
+    if (packed_) {
+        auto kb = w == 256 ? k_bwd_ptile<NR, AA_BWD_CH, 256> : (w == 128 ? k_bwd_ptile<NR, AA_BWD_CH, 128> : k_bwd_ptile<NR, AA_BWD_CH, 64>);
+        hipLaunchKernelGGL(kb, dim3(count), dim3(256), 0, s, btiles_.p, first, Gt_.p, bnd_.p, Y_.p, x0, x1, bpart_.p,
+                           breds_.p, bcnt_.p, ctrl, gate_reject, ext_off);
+    } else {
+        auto kb = w == 256 ? k_bwd_tile<NR, AA_BWD_CH, 256> : (w == 128 ? k_bwd_tile<NR, AA_BWD_CH, 128> : k_bwd_tile<NR, AA_BWD_CH, 64>);
+        hipLaunchKernelGGL(kb, dim3(count), dim3(256), 0, s, btiles_.p, first, Gr_.p, bnd_.p, Y_.p, x0, x1, bpart_.p,
+                           breds_.p, bcnt_.p, ctrl, gate_reject, ext_off);
+    }
+}
+
 template <int NR>
 void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, double* x1, const Ctrl* ctrl,
                             int gate_reject, hipStream_t s) {
@@ -1183,11 +1469,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
                                    ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
-        if (L.ft_count) {
-            auto kf = L.ftw == 256 ? k_fwd_tile<NR, AA_FWD_CH, 256> : (L.ftw == 128 ? k_fwd_tile<NR, AA_FWD_CH, 128> : k_fwd_tile<NR, AA_FWD_CH, 64>);
-            hipLaunchKernelGGL(kf, dim3(L.ft_count), dim3(256), 0, s, ftiles_.p, L.ft_first, Gc_.p, ell_.p, b0, b1,
-                               bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
-        }
+        if (L.ft_count) launch_ftiles<NR>(L.ftw, L.ft_count, L.ft_first, b0, b1, 0, ctrl, gate_reject, s);
     }
     // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
     // and in the update vectors); their sum over the GPUs is the full forward result. When the
@@ -1201,25 +1483,16 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         hipLaunchKernelGGL((k_top_front<NR>), dim3(nb), dim3(256), 0, s, top_task_d_.p, ell_.p, b0, b1, U_.p, top_f_.p,
                            ctrl, gate_reject);
         comm_->allreduce_sum(top_f_.p, top_f_.p, 3 * (size_t)K * pt, s);
-        // the tiles address the front / x by global row beg + q: shift the set-major buffers (as
-        // addresses: the shifted base lies before the allocation and is only used with index >= sh)
-        const uintptr_t sh = 3 * (uintptr_t)top_task_.beg * sizeof(double);
-        auto shifted = [sh](double* base) { return reinterpret_cast<double*>(reinterpret_cast<uintptr_t>(base) - sh); };
-        const double* F0 = shifted(top_f_.p);
-        const double* F1 = shifted(top_f_.p + 3 * (size_t)pt);
-        if (top_ft_count_) {
-            auto kf = top_ftw_ == 256 ? k_fwd_tile<NR, AA_FWD_CH, 256> : (top_ftw_ == 128 ? k_fwd_tile<NR, AA_FWD_CH, 128> : k_fwd_tile<NR, AA_FWD_CH, 64>);
-            hipLaunchKernelGGL(kf, dim3(top_ft_count_), dim3(256), 0, s, ftiles_.p, top_ft_first_, Gc_.p, ell_.p, F0, F1,
-                               bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject);
-        }
+        // the tiles address the front / x by global row beg + q: the set-major buffers hold rows
+        // from beg on (ext_off)
+        const int eo = top_task_.beg;
+        if (top_ft_count_)
+            launch_ftiles<NR>(top_ftw_, top_ft_count_, top_ft_first_, top_f_.p, top_f_.p + 3 * (size_t)pt, eo, ctrl,
+                              gate_reject, s);
         AA_HIP(hipMemsetAsync(top_x_.p, 0, sizeof(double) * 3 * (size_t)K * pt, s));
-        double* Xs0 = shifted(top_x_.p);
-        double* Xs1 = shifted(top_x_.p + 3 * (size_t)pt);
-        if (top_bt_count_) {
-            auto kb = top_btw_ == 256 ? k_bwd_tile<NR, AA_BWD_CH, 256> : (top_btw_ == 128 ? k_bwd_tile<NR, AA_BWD_CH, 128> : k_bwd_tile<NR, AA_BWD_CH, 64>);
-            hipLaunchKernelGGL(kb, dim3(top_bt_count_), dim3(256), 0, s, btiles_.p, top_bt_first_, Gr_.p, bnd_.p, Y_.p,
-                               Xs0, Xs1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
-        }
+        if (top_bt_count_)
+            launch_btiles<NR>(top_btw_, top_bt_count_, top_bt_first_, top_x_.p, top_x_.p + 3 * (size_t)pt, eo, ctrl,
+                              gate_reject, s);
         comm_->allreduce_sum(top_x_.p, top_x_.p, 3 * (size_t)K * pt, s);
         hipLaunchKernelGGL((k_top_scatter<NR>), dim3(nb), dim3(256), 0, s, top_task_d_.p, top_x_.p, x0, x1, ctrl,
                            gate_reject);
@@ -1232,11 +1505,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
                                    bnd_.p, Y_.p, x0, x1, ctrl, gate_reject)
         if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
-        if (L.bt_count) {
-            auto kb = L.btw == 256 ? k_bwd_tile<NR, AA_BWD_CH, 256> : (L.btw == 128 ? k_bwd_tile<NR, AA_BWD_CH, 128> : k_bwd_tile<NR, AA_BWD_CH, 64>);
-            hipLaunchKernelGGL(kb, dim3(L.bt_count), dim3(256), 0, s, btiles_.p, L.bt_first, Gr_.p, bnd_.p, Y_.p,
-                               x0, x1, bpart_.p, breds_.p, bcnt_.p, ctrl, gate_reject);
-        }
+        if (L.bt_count) launch_btiles<NR>(L.btw, L.bt_count, L.bt_first, x0, x1, 0, ctrl, gate_reject, s);
     }
 #define SUBB(BL) hipLaunchKernelGGL((k_bwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_b_, s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, \

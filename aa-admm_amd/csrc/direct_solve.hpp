@@ -77,11 +77,13 @@ public:
     struct SubTree { int lvl0, nlvl; };
     // split-K backward of large supernodes: a tile (64 columns from c0, nr rows from r0) and the
     // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
-    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid, ldr, pad; long long goff, poff; };
+    // toff: the tile's block in the packed tile stream Gt_ (see build: every tile's factor entries
+    // stored contiguously in the order its waves consume them)
+    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid, ldr, pad; long long goff, poff, toff, pad2; };
     struct BRed { int beg, c0, nc, nt; long long poff; };
     // split-K forward of large supernodes: tile (64 rows from r0, nc columns from c0) and the
     // per-row-block reduction of its nt partials
-    struct FTile { int beg, p, R, c0, r0, nc, rid, ell_w; long long goff, ell_off, poff; };
+    struct FTile { int beg, p, R, c0, r0, nc, rid, ell_w; long long goff, ell_off, poff, toff; };
     struct FRed { int beg, p, r0, nr, nt, ell_w; long long uoff, ell_off, poff; };
 
 private:
@@ -98,11 +100,22 @@ private:
     double bytes_ = 0, bytes2_ = 0;
     int max_sets_ = 1;
     template <int NR>
+    void launch_ftiles(int w, int count, int first, const double* b0, const double* b1, int ext_off, const Ctrl* ctrl,
+                       int gate_reject, hipStream_t s);
+    template <int NR>
+    void launch_btiles(int w, int count, int first, double* x0, double* x1, int ext_off, const Ctrl* ctrl,
+                       int gate_reject, hipStream_t s);
+    template <int NR>
     void solve_nr(const double* b0, double* x0, const double* b1, double* x1, const Ctrl* ctrl, int gate_reject,
                   hipStream_t s);
     DevBuf<int> bnd_;
     DevBuf<long long> ell_;   // per front row, ell_w pull offsets into U (-1 = none)
     DevBuf<double> Gr_, Gc_, Y_, U_;
+    // packed split-K tiles (AA_SOLVE_PACKED, default on): per tile one contiguous block, per wave
+    // a sequential stream of 1-KB rows (64 lanes x 16 B): forward [wave][column pair][row][2],
+    // backward [wave][row][column pair][2]; zero-padded to whole tiles
+    DevBuf<double> Gt_;
+    bool packed_ = true;
     DevBuf<Task> tasks_;
     DevBuf<BTile> btiles_;
     DevBuf<BRed> breds_;

@@ -282,6 +282,174 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     if (fail && ctrl) ctrl->fail = 1;
 }
 
+// k_local_z_hq with a one-element lookahead per lane (the default; AA_LQ_AHEAD=0 keeps
+// k_local_z_hq). A refill of the plain queue is a chain of three dependent round trips -- the
+// returning queue atomic, the element's node ids, then the node positions -- paid while the wave's
+// other lanes wait (28 % of the kernel's cycles at one wave per SIMD). Here each
+// lane holds its NEXT element: the claim atomic is issued at a refill and read on the next trip,
+// the node ids are loaded right then, so the following refill only waits for the positions /
+// coefficient / u loads, all independent (one round trip). The finalize keeps the element's node
+// ids and loads positions only for pinned nodes (the only ones Cp needs). Close to the end of the
+// queue (fewer than `margin` elements left) lookahead stops, so claimed-ahead elements cannot
+// pile up on a few waves. Same arithmetic per element: bit-identical to k_local_z_hq.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_local_z_hqa(GroupDev g, const double* __restrict__ xfull,
+                                                        const double* __restrict__ u, double* __restrict__ z,
+                                                        double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
+                                                        int* __restrict__ queue, int refill, int margin,
+                                                        unsigned long long* __restrict__ stats) {
+    if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
+    unsigned trips = 0, refills = 0;
+    __shared__ unsigned hist[101];
+    if (stats) {
+        for (int i = threadIdx.x; i < 101; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+    }
+    constexpr int D = 3 * (NV - 1), NC = NV - 1;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    dev::HyperLbfgs L;
+    double v[D], x[D];
+    double vol = 0;
+    int e = -1, fail = 0;
+    int nid[NV];                 // node ids of the lane's element
+    int ex = -1, xid[NV];        // lookahead element and its node ids
+    int stage = 0, ab = 0, aleader = 0;   // stage 1: a lookahead claim (atomic) is in flight
+    unsigned long long amask = 0;
+    bool active = false, pending = false, exhausted = false, dry = false;
+#pragma unroll
+    for (int a = 0; a < NV; ++a) { nid[a] = 0; xid[a] = 0; }
+    auto finalize = [&]() {
+#pragma unroll
+        for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * g.count + e] = x[i];
+        if (y) {
+            double Cp[D], uu[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) Cp[i] = 0;
+#pragma unroll
+            for (int a = 0; a < NV; ++a) {   // gather_F's Cp: pinned nodes only, same order
+                const int vv = nid[a];
+                if (vv >= nf) {
+                    const double x0 = xfull[3 * (size_t)vv], x1 = xfull[3 * (size_t)vv + 1], x2 = xfull[3 * (size_t)vv + 2];
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) {
+                        const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
+                        Cp[3 * c + 0] += gc * x0; Cp[3 * c + 1] += gc * x1; Cp[3 * c + 2] += gc * x2;
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < D; ++i) uu[i] = u ? u[g.zoff + (size_t)i * g.count + e] : 0.0;
+            write_slots<NV>(g, e, nf, g.w[e], x, Cp, uu, y);
+        }
+    };
+    auto begin = [&](int ee, const int* ids) {
+        e = ee;
+        double F[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) F[i] = 0;
+#pragma unroll
+        for (int a = 0; a < NV; ++a) {   // gather_F's F, same order
+            nid[a] = ids[a];
+            const double x0 = xfull[3 * (size_t)ids[a]], x1 = xfull[3 * (size_t)ids[a] + 1], x2 = xfull[3 * (size_t)ids[a] + 2];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
+                F[3 * c + 0] += gc * x0; F[3 * c + 1] += gc * x1; F[3 * c + 2] += gc * x2;
+            }
+        }
+        const double w = g.w[e];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            v[i] = F[i] + (u ? u[g.zoff + (size_t)i * g.count + e] : 0.0) / w;
+            x[i] = v[i];
+        }
+        vol = g.vol[e];
+        if (L.start(g.mat, g.mu, g.lambda, g.k, vol, v, x)) {
+            finalize();
+            if (stats) atomicAdd(&hist[0], 1u);
+        } else {
+            active = true;
+        }
+    };
+    for (;;) {
+        const bool need = !active && !exhausted;
+        const unsigned long long mask = __ballot(need);
+        if (!__any(active || need)) break;
+        ++trips;
+        if (stage == 1) {   // the lookahead claim issued at the last refill has returned
+            const int b = __shfl(ab, aleader, 64);
+            if ((amask >> lane) & 1ull) {
+                const int my = b + __popcll(amask & below);
+                if (my < g.count) {
+                    ex = my;
+#pragma unroll
+                    for (int a = 0; a < NV; ++a) xid[a] = g.idx[(size_t)a * g.count + ex];
+                }
+            }
+            if (b + __popcll(amask) >= g.count - margin) dry = true;
+            stage = 0;
+        }
+        if (mask && (__popcll(mask) >= refill || !__any(active))) {
+            ++refills;
+            const bool direct = need && ex < 0;   // no lookahead: claim now (queue start, its tail)
+            const unsigned long long dmask = __ballot(direct);
+            int b = 0, leader = 0;
+            if (dmask) {
+                leader = __ffsll((long long)dmask) - 1;
+                if (lane == leader) b = atomicAdd(queue, __popcll(dmask));
+            }
+            if (pending) {
+                finalize();
+                pending = false;
+            }
+            int ee = -1, ids[NV];
+#pragma unroll
+            for (int a = 0; a < NV; ++a) ids[a] = xid[a];
+            if (need && ex >= 0) { ee = ex; ex = -1; }
+            if (dmask) {
+                b = __shfl(b, leader, 64);
+                if (direct) {
+                    const int my = b + __popcll(dmask & below);
+                    if (my >= g.count) {
+                        exhausted = true;
+                    } else {
+                        ee = my;
+#pragma unroll
+                        for (int a = 0; a < NV; ++a) ids[a] = g.idx[(size_t)a * g.count + ee];
+                    }
+                }
+            }
+            if (ee >= 0) begin(ee, ids);
+            if (!dry) {   // the next lookahead claim, for every lane without one
+                const unsigned long long lm = __ballot(ex < 0 && !exhausted);
+                if (lm) {
+                    amask = lm;
+                    aleader = __ffsll((long long)lm) - 1;
+                    if (lane == aleader) ab = atomicAdd(queue, __popcll(lm));
+                    stage = 1;
+                }
+            }
+        }
+        if (active && L.iterate(g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail)) {
+            active = false;
+            pending = true;
+            if (stats) atomicAdd(&hist[min(L.k_it, 100)], 1u);
+        }
+    }
+    if (stats) {
+        if (lane == 0) {
+            atomicAdd(stats + 101, (unsigned long long)trips);
+            atomicAdd(stats + 102, (unsigned long long)refills);
+            atomicAdd(stats + 103, 1ull);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 101; i += blockDim.x)
+            if (hist[i]) atomicAdd(stats + i, (unsigned long long)hist[i]);
+    }
+    if (fail && ctrl) ctrl->fail = 1;
+}
+
 // r = w(P x - z): prim2 += |r|^2, dual2 += |w P (x - x_last)|^2, u += r
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_resid_u(GroupDev g, const double* __restrict__ xfull,
@@ -1054,7 +1222,12 @@ LocalQueue make_local_queue(int device, int* counter) {
     AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_local_z_hq<4>, kBlock, 0));
     q.resident = std::max(1, cus * std::max(1, per));
     const char* r = std::getenv("AA_LQ_REFILL");
+    const char* ah = std::getenv("AA_LQ_AHEAD");
+    q.ahead = !(ah && ah[0] == '0');
     q.refill = r ? std::atoi(r) : 60;
+    // lookahead stops once fewer elements than this are left (AA_LQ_MARGIN: in resident lanes)
+    const char* mg = std::getenv("AA_LQ_MARGIN");
+    q.margin = (int)(std::max(0.0, mg ? std::atof(mg) : 1.0) * q.resident * kBlock);
     return q;
 }
 
@@ -1065,8 +1238,12 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
     if (g.kind == 0 && g.mat != 0 && !red && queue && queue->counter) {   // hyperelastic, no partials: work queue
         AA_HIP(hipMemsetAsync(queue->counter, 0, sizeof(int), s));
         const int resident = std::max(1, queue->resident), refill = queue->refill;
-        hipLaunchKernelGGL(k_local_z_hq<4>, dim3(std::min(nb, resident)), dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
-                           ctrl, queue->counter, refill, queue->stats);
+        if (queue->ahead)
+            hipLaunchKernelGGL(k_local_z_hqa<4>, dim3(std::min(nb, resident)), dim3(kBlock), 0, s, g, xfull, u, z, y, nf,
+                               mode, ctrl, queue->counter, refill, queue->margin, queue->stats);
+        else
+            hipLaunchKernelGGL(k_local_z_hq<4>, dim3(std::min(nb, resident)), dim3(kBlock), 0, s, g, xfull, u, z, y, nf,
+                               mode, ctrl, queue->counter, refill, queue->stats);
         AA_CHECK_LAUNCH();
         return;
     }

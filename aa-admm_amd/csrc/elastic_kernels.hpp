@@ -74,7 +74,8 @@ enum LocalMode { LZ_NORMAL = 0, LZ_REDO = 1, LZ_INIT = 2 };
 // device and the refill threshold (computed once per solver, make_local_queue)
 struct LocalQueue {
     int* counter = nullptr;
-    int resident = 0, refill = 60;
+    int resident = 0, refill = 60, margin = 0;
+    bool ahead = true;   // k_local_z_hqa (one-element lookahead per lane)
     // optional diagnostics (AA_LQ_STATS=1): [0..100] elements by L-BFGS iterations (0 = the start
     // point passed the gradient test), [101] trips, [102] refills, [103] waves; summed over launches
     unsigned long long* stats = nullptr;

@@ -398,7 +398,8 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     }
     SupernodalFactor F;
     try {
-        F = factor_on_device(A, tree, s());
+        auto pf = make_part_factor(P > 1 ? comm_ : nullptr, rank_, s());   // no rank factors another's part
+        F = factor_on_device(A, tree, s(), pf.get());
     } catch (const Error&) {
         throw;   // device / allocation failures keep their own status
     } catch (const std::runtime_error& e) {

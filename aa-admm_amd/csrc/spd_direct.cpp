@@ -275,6 +275,7 @@ struct FrontCtx {
     std::vector<std::vector<double>>& U;   // host update matrices, freed when consumed
     std::vector<double>& flops;
     DenseFrontBackend* dense;
+    const PartFactor* part;   // partitioned: this rank's share of a top front, summed (see PartFactor)
 };
 
 int front_order(const SupernodalFactor& F, int s) { return F.end[s] - F.beg[s] + (int)F.bnd[s].size(); }
@@ -294,26 +295,44 @@ void factor_front(FrontCtx& C, int s, std::vector<int>& pos, bool inner_parallel
     double fl = 0;
     for (int k = 0; k < p; ++k) fl += (double)(f - k) * (f - k);
     C.flops[s] = fl;
+    // partitioned top front: this rank's terms only (A and top children on the first rank, the
+    // own part's children everywhere), summed over the ranks after assembly
+    const PartFactor* P = (C.part && tree.part[s] == -1) ? C.part : nullptr;
+    const bool add_a = !P || P->first;
+    auto take_child = [&](int c) {
+        if (!C.part) return true;
+        if (tree.part[c] == -1) return P == nullptr || P->first;
+        return tree.part[c] == C.part->my_part;
+    };
     if (C.dense && f >= C.dense->min_front) {
         std::vector<int> ai, aj;
         std::vector<double> av;
-        for (int j = b0; j < e0; ++j)
-            for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) {
-                const int i = A.col[k];
-                if (i < j) continue;
-                ai.push_back(pos[i]); aj.push_back(pos[j]); av.push_back(A.val[k]);
-            }
+        if (add_a)
+            for (int j = b0; j < e0; ++j)
+                for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) {
+                    const int i = A.col[k];
+                    if (i < j) continue;
+                    ai.push_back(pos[i]); aj.push_back(pos[j]); av.push_back(A.val[k]);
+                }
         std::vector<DenseFrontBackend::Child> kids;
         std::vector<std::vector<int>> maps(tree.children[s].size());
         for (size_t q = 0; q < tree.children[s].size(); ++q) {
             const int c = tree.children[s][q];
+            if (!take_child(c)) continue;
             for (int i : F.bnd[c]) maps[q].push_back(pos[i]);
             kids.push_back({c, maps[q].data(), (int)maps[q].size(), C.dense->holds(c) ? nullptr : &C.U[c]});
         }
         const int par = tree.parent[s];
         const bool keep = par >= 0 && front_order(F, par) >= C.dense->min_front;
         std::vector<double> Us;
-        C.dense->factor(s, f, p, ai, aj, av, kids, keep, F.Linv[s], F.LBP[s], F.M[s], keep ? nullptr : &Us);
+        if (P) C.dense->reduce_front = P->reduce_dev;
+        try {
+            C.dense->factor(s, f, p, ai, aj, av, kids, keep, F.Linv[s], F.LBP[s], F.M[s], keep ? nullptr : &Us);
+        } catch (...) {
+            C.dense->reduce_front = nullptr;
+            throw;
+        }
+        C.dense->reduce_front = nullptr;
         for (int c : tree.children[s]) std::vector<double>().swap(C.U[c]);
         if (nb > 0 && !keep) C.U[s] = std::move(Us);
         return;
@@ -321,13 +340,15 @@ void factor_front(FrontCtx& C, int s, std::vector<int>& pos, bool inner_parallel
     // ---- assemble front (lower triangle, column-major f x f: Fc(i,j) at j*f + i)
     std::vector<double> Fc((size_t)f * f, 0.0);
     auto FC = [&](int i, int j) -> double& { return Fc[(size_t)j * f + i]; };
-    for (int j = b0; j < e0; ++j)
-        for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) {
-            int i = A.col[k];
-            if (i < j) continue;
-            FC(pos[i], pos[j]) += A.val[k];
-        }
+    if (add_a)
+        for (int j = b0; j < e0; ++j)
+            for (int k = A.ptr[j]; k < A.ptr[j + 1]; ++k) {
+                int i = A.col[k];
+                if (i < j) continue;
+                FC(pos[i], pos[j]) += A.val[k];
+            }
     for (int c : tree.children[s]) {
+        if (!take_child(c)) { std::vector<double>().swap(C.U[c]); continue; }
         const std::vector<int>& cb = F.bnd[c];
         const int m = (int)cb.size();
         if (C.dense && C.dense->holds(c)) throw std::runtime_error("multifrontal_cholesky: update matrix held by the backend");
@@ -340,6 +361,7 @@ void factor_front(FrontCtx& C, int s, std::vector<int>& pos, bool inner_parallel
             }
         std::vector<double>().swap(C.U[c]);
     }
+    if (P) P->reduce_host(Fc.data(), Fc.size());
     // ---- partial dense Cholesky (right-looking, column-major) of the first p columns
     for (int k = 0; k < p; ++k) {
         double* ck = &Fc[(size_t)k * f];
@@ -388,7 +410,8 @@ void factor_front(FrontCtx& C, int s, std::vector<int>& pos, bool inner_parallel
 
 }  // namespace
 
-SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, DenseFrontBackend* dense) {
+SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, DenseFrontBackend* dense,
+                                       const PartFactor* part) {
     SupernodalFactor F;
     const int n = A.n, nn = (int)tree.beg.size();
     F.n = n; F.n_nodes = nn;
@@ -397,10 +420,13 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
     symbolic(A, tree, F);
     std::vector<std::vector<double>> U(nn);
     std::vector<double> flops(nn, 0.0);
-    FrontCtx C{A, tree, F, U, flops, dense};
+    FrontCtx C{A, tree, F, U, flops, dense, part};
+    if (part && (int)tree.part.size() != nn) throw std::runtime_error("multifrontal_cholesky: partitioned factor needs a partitioned tree");
+    auto mine = [&](int s) { return !part || tree.part[s] == part->my_part; };
     if (!dense) {   // host only: postorder, parallel inside the large fronts
         std::vector<int> pos(n, -1);
-        for (int s = 0; s < nn; ++s) factor_front(C, s, pos, true);
+        for (int s = 0; s < nn; ++s)
+            if (mine(s) || tree.part[s] == -1) factor_front(C, s, pos, true);
     } else {
         // tree-parallel: independent subtrees are OpenMP tasks (a front waits for its children),
         // each host front is factored by one thread; the large fronts near the root go to the
@@ -435,17 +461,28 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
                 if (err.empty()) err = e.what();
             }
         };
+        // partitioned: the own part's subtrees (roots: own supernodes whose parent is not own)
+        // in parallel, then the top fronts one at a time in postorder (collectives)
+        auto is_root = [&](int s) {
+            if (!part) return tree.parent[s] < 0;
+            return mine(s) && (tree.parent[s] < 0 || !mine(tree.parent[s]));
+        };
 #pragma omp parallel
 #pragma omp single
         {
             for (int s = 0; s < nn; ++s)
-                if (tree.parent[s] < 0) {
+                if (is_root(s)) {
 #pragma omp task firstprivate(s) shared(rec)
                     rec(s);
                 }
 #pragma omp taskwait
         }
         if (!err.empty()) throw std::runtime_error(err);
+        if (part) {
+            std::vector<int> pos(n, -1);
+            for (int s = 0; s < nn; ++s)
+                if (tree.part[s] == -1) factor_front(C, s, pos, true);
+        }
     }
     for (int s = 0; s < nn; ++s) {
         const int p = tree.end[s] - tree.beg[s], nb = (int)F.bnd[s].size();

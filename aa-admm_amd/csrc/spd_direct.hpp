@@ -95,13 +95,31 @@ struct DenseFrontBackend {
                         std::vector<double>* U) = 0;
     virtual bool holds(int s) const = 0;   // s's update matrix is held by the backend
     int min_front = 1024;                  // fronts of at least this order go to the backend
+    // set for the partitioned top fronts (PartFactor): called on the assembled device front
+    // (f x f doubles) before it is factored -- the sum of the ranks' partial fronts
+    std::function<void(double*, size_t)> reduce_front;
+};
+
+// Partitioned factorization, one rank of P: only the supernodes of
+// part `my_part` and of the shared top (part -1) are factored here. A top front is assembled from
+// this rank's share only -- A's entries and the update matrices of top children on the `first`
+// rank, the own part's children on every rank -- and summed over the ranks (reduce_host on a
+// host front, reduce_dev on a backend front) before its partial Cholesky, so every rank factors
+// the same top and no rank factors another rank's part. The top fronts are factored after the
+// part, one at a time in postorder (the same collective sequence on every rank).
+struct PartFactor {
+    int my_part = -1;
+    bool first = false;
+    std::function<void(double*, size_t)> reduce_host;
+    std::function<void(double*, size_t)> reduce_dev;
 };
 
 // Factor the matrix A (given in NEW ordering as a full-pattern CSR) along the tree.
 // Throws std::runtime_error if A is not positive definite.
 // dense == nullptr: everything on the host, supernodes in postorder. Otherwise independent
 // subtrees are factored in parallel (OpenMP tasks) and the large fronts by `dense`.
-SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, DenseFrontBackend* dense = nullptr);
+SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, DenseFrontBackend* dense = nullptr,
+                                       const PartFactor* part = nullptr);
 
 // Host reference solve with the factor (used by self-checks): x = A^-1 b, b is n x 3.
 void factor_solve_host(const SupernodalFactor& F, std::vector<double>& b3);

@@ -25,6 +25,7 @@ driver under oracle/ (test infrastructure only).
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -138,6 +139,33 @@ def tet_blocks(cx: int, cy: int, cz: int):
     return verts, tets.astype(np.int32)
 
 
+def tet_voxels(occ):
+    """make_tet_blocks' 5 tets (same table, same corner labels) for every occupied cell of a
+    boolean grid occ[x, y, z]; vertices = the lattice nodes the cells use (lattice units),
+    numbered in lattice order. Cells in x-major, then y, then z order as in tet_blocks."""
+    cx, cy, cz = occ.shape
+    X, Y, Z = (a.astype(np.int64) for a in np.nonzero(occ))   # x-major order
+    node = lambda i, j, k: (i * (cy + 1) + j) * (cz + 1) + k
+    lab = [node(X + 1, Y + 1, Z + 1), node(X, Y + 1, Z + 1), node(X, Y + 1, Z), node(X + 1, Y + 1, Z),
+           node(X + 1, Y, Z + 1), node(X, Y, Z + 1), node(X, Y, Z), node(X + 1, Y, Z)]
+    table = [(0, 5, 7, 4), (5, 7, 2, 0), (5, 0, 2, 1), (7, 2, 0, 3), (5, 2, 7, 6)]
+    tets = np.stack([np.stack([lab[t[0]], lab[t[1]], lab[t[2]], lab[t[3]]], 1) for t in table], 1).reshape(-1, 4)
+    used = np.unique(tets)
+    remap = np.full((cx + 1) * (cy + 1) * (cz + 1), -1, np.int64)
+    remap[used] = np.arange(len(used))
+    i, r = np.divmod(used, (cy + 1) * (cz + 1))
+    j, k = np.divmod(r, cz + 1)
+    verts = np.stack([i, j, k], 1).astype(np.float64)
+    return verts, remap[tets].astype(np.int32)
+
+
+def load_voxels(name):
+    """Occupancy grid committed under aa-admm_amd/data (tools/make_bunny_voxels.py)."""
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", name + ".npz"))
+    dims = tuple(int(a) for a in d["dims"])
+    return np.unpackbits(d["bits"])[:int(np.prod(dims))].reshape(dims).astype(bool)
+
+
 def tri_masses(verts, tris, density=1.0):
     e1 = verts[tris[:, 1]] - verts[tris[:, 0]]
     e2 = verts[tris[:, 2]] - verts[tris[:, 0]]
@@ -211,6 +239,25 @@ def tet_drop(cx=100, cy=40, cz=50, material=NEOHOOKEAN, *, squash=0.9, variant=V
     return Scene(x=x, masses=m, groups=[ElementGroup(TET, material, E, nu, t)], pin_idx=np.zeros(0, np.int32),
                  pin_pts=np.zeros((0, 3)), pin_vel=np.zeros((0, 3)), variant=variant, iters=iters, aa_m=aa_m,
                  n_steps=n_steps, accel=accel, name=f"drop{cx}x{cy}x{cz}", rest=v)
+
+
+def bunny_drop(res=100, material=NEOHOOKEAN, *, cell=1.0 / 40.0, squash=0.9, variant=VARIANT_X, aa_m=6, iters=100,
+               n_steps=1, accel=1, E=1e7, nu=0.399) -> Scene:
+    """C4 on the mesh BASELINE configs[3] names: the reference's closed bunny
+    (deps/mclscene/src/data/bunny_closed.obj) voxelised into `res` cells along its longest side
+    (aa-admm_amd/data/bunny_vox<res>.npz; res 100 = 200 556 cells = 1 002 780 tets), 5
+    make_tet_blocks tets per cell of size `cell` (the C4 block's 1/40 m), then the tet_drop
+    recipe: NeoHookean Lame(1e7, 0.399), density 1522, free fall from the rest shape squashed to
+    `squash` in y, z-AA (X order). An irregular, boundary-heavy mesh beside the regular block."""
+    v, t = tet_voxels(load_voxels(f"bunny_vox{res}"))
+    v = v * cell
+    m = tet_masses(v, t, 1522.0)
+    x = v.copy()
+    c = 0.5 * (v[:, 1].min() + v[:, 1].max())
+    x[:, 1] = c + squash * (v[:, 1] - c)
+    return Scene(x=x, masses=m, groups=[ElementGroup(TET, material, E, nu, t)], pin_idx=np.zeros(0, np.int32),
+                 pin_pts=np.zeros((0, 3)), pin_vel=np.zeros((0, 3)), variant=variant, iters=iters, aa_m=aa_m,
+                 n_steps=n_steps, accel=accel, name=f"bunny{res}", rest=v)
 
 
 def beams(dim=3, *, variant=VARIANT_X, aa_m=6, iters=100, n_steps=1, accel=1, materials=(LINEAR, NEOHOOKEAN, STVK)) -> Scene:

@@ -215,14 +215,40 @@ int main(int argc, char** argv) {
             for (int pp = 0; pp < P; ++pp) for (int c = 0; c < 3; ++c) bp[pp][3 * q + c] = b[3 * q + c] * w[pp] / ws;
         }
         SumBarrier bar(P);
+        // each rank factors only its own part and the top (aa::PartFactor: the top fronts are the
+        // sum of the ranks' partial fronts), then solves with its own factor
+        std::vector<aa::SupernodalFactor> Fr(P);
         std::vector<std::thread> th;
         for (int pp = 0; pp < P; ++pp)
             th.emplace_back([&, pp] {
-                if (dense) solve_dense_top(F, T, pp, P, bp[pp], bar);
-                else aa::factor_solve_host_part(F, P > 1 ? &T : nullptr, P > 1 ? pp : -1, bp[pp],
+                aa::PartFactor pf;
+                pf.my_part = pp;
+                pf.first = pp == 0;
+                pf.reduce_host = [&](double* v, size_t m) { bar.reduce(v, m); };
+                Fr[pp] = P > 1 ? aa::multifrontal_cholesky(A, T, nullptr, &pf) : F;
+                const aa::SupernodalFactor& Fp = Fr[pp];
+                if (dense) solve_dense_top(Fp, T, pp, P, bp[pp], bar);
+                else aa::factor_solve_host_part(Fp, P > 1 ? &T : nullptr, P > 1 ? pp : -1, bp[pp],
                                                 [&](double* v, size_t m) { bar.reduce(v, m); });
             });
         for (auto& t : th) t.join();
+        // own part bit-identical to the whole factorization, other parts not factored, the top
+        // the same on every rank and within rounding of the whole factorization's
+        bool fac_ok = true;
+        double top_rel = 0;
+        for (int pp = 0; P > 1 && pp < P; ++pp)
+            for (int s = 0; s < F.n_nodes; ++s) {
+                if (T.part[s] == pp) fac_ok = fac_ok && Fr[pp].Linv[s] == F.Linv[s] && Fr[pp].LBP[s] == F.LBP[s];
+                else if (T.part[s] >= 0) fac_ok = fac_ok && Fr[pp].Linv[s].empty();
+                else {
+                    fac_ok = fac_ok && Fr[pp].Linv[s] == Fr[0].Linv[s] && Fr[pp].Linv[s].size() == F.Linv[s].size();
+                    double mx = 0;
+                    for (double v : F.Linv[s]) mx = std::max(mx, std::fabs(v));
+                    for (size_t k = 0; k < F.Linv[s].size() && k < Fr[pp].Linv[s].size(); ++k)
+                        top_rel = std::max(top_rel, std::fabs(Fr[pp].Linv[s][k] - F.Linv[s][k]) / mx);
+                }
+            }
+        fac_ok = fac_ok && top_rel <= 1e-11;
         double emax = 0, xmax = 0, tdiff = 0;
         for (int q = 0; q < n; ++q) {
             int owner = -1;
@@ -237,11 +263,12 @@ int main(int argc, char** argv) {
         }
         int ntop = 0;
         for (int s = 0; s < F.n_nodes; ++s) ntop += T.part[s] == -1 && F.end[s] > F.beg[s];
-        const bool ok = rmax <= 1e-10 * bmax && emax <= 1e-10 * xmax && tdiff == 0.0 && (P == 1 || T.top_beg < n) &&
+        const bool ok = fac_ok && rmax <= 1e-10 * bmax && emax <= 1e-10 * xmax && tdiff == 0.0 && (P == 1 || T.top_beg < n) &&
                         (int)T.part_beg.size() == std::max(1, P) && (!dense || ntop == 1);
         std::printf("part_top_rows=%d ", cs[2]);
-        std::printf("parts=%d dense_top=%d n=%d top_rows=%d top_nodes=%d nnzL=%zu |Ax-b|=%.2e |x_part-x|=%.2e top_spread=%.1e %s\n",
-                    P, (int)dense, n, n - T.top_beg, ntop, F.nnz_L, rmax / bmax, emax / xmax, tdiff, ok ? "OK" : "FAIL");
+        std::printf("parts=%d dense_top=%d n=%d top_rows=%d top_nodes=%d nnzL=%zu |Ax-b|=%.2e |x_part-x|=%.2e top_spread=%.1e "
+                    "part_factor_top_rel=%.1e %s\n",
+                    P, (int)dense, n, n - T.top_beg, ntop, F.nnz_L, rmax / bmax, emax / xmax, tdiff, top_rel, ok ? "OK" : "FAIL");
         if (!ok) ++fails;
     }
     return fails ? 1 : 0;

@@ -191,6 +191,25 @@ def full_drop40(tmp):
     print("full_drop40_z_nh_aa6", [len(s["prim"]) for s in steps])
 
 
+def full_bunny40(tmp):
+    """The C4 recipe on the voxelised bunny BASELINE configs[3] names, at the golden size
+    (scenes.bunny_drop(40) = 64 150 NeoHookean tets, 15 724 nodes on an irregular, boundary-heavy
+    mesh; z-AA m=6, 3 time steps x 10 iterations): the reference's per-iteration residuals and
+    positions / velocities on 512 sampled nodes plus their column sums per step."""
+    sc = scenes.bunny_drop(40, iters=10, n_steps=3)
+    steps = run_ref(sc, tmp)
+    rng = np.random.default_rng(5)
+    sample = np.sort(rng.choice(sc.n_nodes, 512, replace=False)).astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "full_bunny40_z_nh_aa6.npz"), digest=scene_digest(sc), sample=sample,
+                        nrec=np.array([len(s["prim"]) for s in steps]),
+                        prim=np.concatenate([s["prim"] for s in steps]), comb=np.concatenate([s["comb"] for s in steps]),
+                        reject=np.concatenate([s["reject"] for s in steps]),
+                        x_sample=np.stack([s["x"][sample] for s in steps]),
+                        v_sample=np.stack([s["v"][sample] for s in steps]),
+                        x_sum=np.stack([s["x"].sum(0) for s in steps]), v_sum=np.stack([s["v"].sum(0) for s in steps]))
+    print("full_bunny40_z_nh_aa6", [len(s["prim"]) for s in steps])
+
+
 def residual_files(tmp):
     """The reference's own Solver::save() output (Solver.hpp:130-155: result/residual-<m>.txt,
     written by every step()) for one (u,x)-variant and one z-variant scene, kept verbatim as data
@@ -216,6 +235,10 @@ def main(only=None):
     if only == ["--full"]:
         with tempfile.TemporaryDirectory() as tmp:
             full_drop40(tmp)
+        return
+    if only == ["--bunny"]:
+        with tempfile.TemporaryDirectory() as tmp:
+            full_bunny40(tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         for name, sc in cases().items():

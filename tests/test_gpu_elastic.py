@@ -125,6 +125,54 @@ def test_gpu_full_size_drop_c4(pkg, ctx):
     assert h["comb"][-1] < 1e-4 * h["comb"][0], (h["comb"][0], h["comb"][-1])
 
 
+def test_gpu_full_size_bunny_c4(pkg, ctx):
+    """configs[3] on the mesh it names: the voxelised bunny at 1 002 780 NeoHookean tets (218 090
+    nodes; scenes.bunny_drop(100)), an irregular, boundary-heavy mesh -- the nested dissection,
+    the split-K solve levels and the work queue beyond a perfect box. The same size-independent
+    checks as the block: momentum (mass-weighted mean velocity = g dt, 1e-9) and the residual
+    falling by orders of magnitude."""
+    sc = scenes.bunny_drop(100, iters=30, n_steps=1)
+    assert sc.n_elements() == 1_002_780 and sc.n_nodes == 218_090
+    got, solver = pkg.capi.run_scene(ctx, sc)
+    h = got[0]
+    assert np.all(np.isfinite(h["comb"])) and np.all(np.isfinite(h["x"]))
+    m = sc.masses
+    vbar = (m[:, None] * h["v"]).sum(0) / m.sum()
+    g_dt = sc.gravity * sc.dt
+    assert abs(vbar[1] - g_dt) <= 1e-9 * abs(g_dt), vbar
+    assert abs(vbar[0]) <= 1e-9 * abs(g_dt) and abs(vbar[2]) <= 1e-9 * abs(g_dt), vbar
+    assert h["comb"][-1] < 1e-4 * h["comb"][0], (h["comb"][0], h["comb"][-1])
+
+
+def test_gpu_full_bunny40_matches_reference(pkg, ctx):
+    """The bunny C4 recipe at the golden size (scenes.bunny_drop(40) = 64 150 tets) against the
+    reference's own run (tests/golden/full_bunny40_z_nh_aa6.npz, make_golden.py --bunny), with
+    the bars of the block's 64k-tet golden."""
+    import os
+    import sys
+    from golden_io import GOLDEN
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import scene_digest
+    ref = np.load(os.path.join(GOLDEN, "full_bunny40_z_nh_aa6.npz"))
+    sc = scenes.bunny_drop(40, iters=10, n_steps=3)
+    assert np.array_equal(scene_digest(sc), ref["digest"]), "regenerated scene differs from the fixture's"
+    got, _ = pkg.capi.run_scene(ctx, sc)
+    o = 0
+    for k, n in enumerate(ref["nrec"]):
+        h = got[k]
+        rc, rp, rr = ref["comb"][o:o + n], ref["prim"][o:o + n], ref["reject"][o:o + n]
+        o += n
+        assert len(h["comb"]) == n
+        assert np.abs(h["comb"] - rc).max() <= 1e-6 * rc[0], (k, np.abs(h["comb"] - rc).max() / rc[0])
+        assert np.abs(h["prim"] - rp).max() <= 1e-5 * rp[0]
+        assert np.array_equal(h["reject"], rr)
+        for key in ("x", "v"):
+            want = ref[key + "_sample"][k]
+            scale = np.abs(want).max()
+            assert np.abs(h[key][ref["sample"]] - want).max() <= 1e-6 * scale, (k, key)
+            assert np.allclose(h[key].sum(0), ref[key + "_sum"][k], rtol=1e-6, atol=1e-6 * scale * len(h[key]))
+
+
 @pytest.mark.parametrize("builder", [
     lambda: scenes.tet_drop(12, 4, 6, iters=40, n_steps=2),                       # no break
     lambda: dataclasses.replace(scenes.tet_drop(4, 2, 2, squash=1.0, iters=30, n_steps=2), gravity=0.0),

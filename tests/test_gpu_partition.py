@@ -49,14 +49,21 @@ def as_steps(d, n_steps):
 # 3 ranks: an uneven part count (proportional bisections); top=0: the round-1 layout with one
 # supernode per shared separator, solved whole on every rank (AA_TOP_DENSE=0) -- the default is
 # one dense top root split over the ranks by rows
-@pytest.mark.parametrize("case,nranks,top", [("cloth_ux", 2, 1), ("cloth_ux", 4, 1), ("cloth_ux", 3, 1), ("cant_ux", 2, 1),
-                                             ("drop_z", 2, 1), ("drop_z", 4, 1), ("drop_z", 3, 1), ("drop_z", 4, 0),
-                                             ("beams_z", 2, 1), ("cant_z_noaa", 2, 1)])
-def test_partitioned_matches_single_gpu(case, nranks, top, tmp_path, pkg, ctx):
+# minfront: AA_DENSE_MIN_FRONT -- 64 sends the top fronts (and the larger part fronts) to the GPU
+# backend, so the partitioned factorization's device all-reduce of a partial top front runs
+# (each rank factors only its own part and the top: aa::PartFactor)
+@pytest.mark.parametrize("case,nranks,top,minfront", [("cloth_ux", 2, 1, 0), ("cloth_ux", 4, 1, 0), ("cloth_ux", 3, 1, 0),
+                                                      ("cant_ux", 2, 1, 0), ("drop_z", 2, 1, 0), ("drop_z", 4, 1, 0),
+                                                      ("drop_z", 3, 1, 0), ("drop_z", 4, 0, 0), ("drop_z", 3, 1, 64),
+                                                      ("drop_z", 4, 0, 64), ("beams_z", 2, 1, 0), ("cant_z_noaa", 2, 1, 0)])
+def test_partitioned_matches_single_gpu(case, nranks, top, minfront, tmp_path, pkg, ctx):
     builder, tol = CASES[case]
     sc = builder()
     want, _ = pkg.capi.run_scene(ctx, sc)
-    ranks = run_ranks(case, nranks, tmp_path, extra_env={"AA_TOP_DENSE": str(top)})
+    env = {"AA_TOP_DENSE": str(top)}
+    if minfront:
+        env["AA_DENSE_MIN_FRONT"] = str(minfront)
+    ranks = run_ranks(case, nranks, tmp_path, extra_env=env)
     # every element is owned by exactly one rank
     assert sum(int(r["n_elements"][0]) for r in ranks) == sc.n_elements()
     # all ranks hold the same bits
@@ -88,13 +95,15 @@ def test_rccl_transport_one_rank_is_identity(pkg, ctx):
     comm.close()
 
 
-@pytest.mark.parametrize("case,nranks", [("pq", 2), ("pq", 4), ("pq", 3), ("wire", 2), ("pq_noaa", 2)])
-def test_partitioned_geometry_matches_single_gpu(case, nranks, tmp_path, pkg, ctx):
+@pytest.mark.parametrize("case,nranks,minfront", [("pq", 2, 0), ("pq", 4, 0), ("pq", 3, 0), ("pq", 3, 64), ("wire", 2, 0),
+                                                  ("pq_noaa", 2, 0)])
+def test_partitioned_geometry_matches_single_gpu(case, nranks, minfront, tmp_path, pkg, ctx):
     sc = GEOM_CASES[case]()
     want, g = pkg.capi.run_geom(ctx, sc)
     n_cons = g.runtime().n_constraints
     g.close()
-    ranks = run_ranks("geom:" + case, nranks, tmp_path)
+    ranks = run_ranks("geom:" + case, nranks, tmp_path,
+                      extra_env={"AA_DENSE_MIN_FRONT": str(minfront)} if minfront else None)
     assert sum(int(r["n_constraints"][0]) for r in ranks) == n_cons   # each constraint on one rank
     for r in ranks[1:]:
         assert np.array_equal(r["comb"], ranks[0]["comb"]) and np.array_equal(r["x"], ranks[0]["x"])
