@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <memory>
 #include <string>
 
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
 // x 16 B, two columns or two rows' entries per lane). The column-major / row-major copies put a
 // tile's 64 x 256 entries in 256 pieces of 512 B (or 1 KB) at strides of the supernode's height,
 // spread over several MB: a DRAM-page and TLB pattern a contiguous stream avoids.
-template <int NR, int CH, int kFwdTileCols>
+template <int NR, int CH, int kFwdTileCols, int DEPTH>
 __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __restrict__ tiles, int first,
                                                    const double* __restrict__ Gt, const long long* __restrict__ ell,
                                                    const double* __restrict__ B0, const double* __restrict__ B1,
@@ -432,14 +433,15 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
     const bool live = nloc > 0;   // wave-uniform: rows past R read the block's zero padding
     const int qmax = (nloc - 1) >> 1;   // last pair with a live column (later indices re-read it: cache hits)
     const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * (per / 2) * 64 + lane;
-    double2 ga[C2], gb[C2];
+    constexpr int DP = DEPTH < NC ? DEPTH : NC;   // chunks in flight
+    double2 gbuf[DP][C2];
     auto ld = [&](double2* g, int k) {
 #pragma unroll
         for (int q = 0; q < C2; ++q) g[q] = G[(size_t)min(k * C2 + q, qmax) * 64];
     };
     if (live) {
-        ld(ga, 0);
-        if (NC > 1) ld(gb, 1);
+#pragma unroll
+        for (int d = 0; d < DP; ++d) ld(gbuf[d], d);
     }
     for (int i = tid; i < kFwdTileCols; i += 256) {
         if (i < t.nc) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i, ext_off);
@@ -463,8 +465,8 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
         };
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
-            if (k & 1) { use(gb, k); if (k + 2 < NC) ld(gb, k + 2); }
-            else       { use(ga, k); if (k + 2 < NC) ld(ga, k + 2); }
+            use(gbuf[k % DP], k);
+            if (k + DP < NC) ld(gbuf[k % DP], k + DP);
         }
     }
     if (w > 0)
@@ -506,7 +508,117 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int NR, int CH, int kBwdTileRows>
+// Forward strips (packed tiles): one workgroup runs the split-K tiles of ONE column slice
+// [c0, c0 + W) of a supernode over several consecutive row blocks. The front slice (b + the
+// children's update vectors, pulled through the ELL lists) is gathered once per strip instead of
+// once per tile -- per tile it was ~1/3 of the tile's own bytes again (profiles/r3_c4_solve_pmc_table.txt)
+// -- and the workgroup streams tile after tile. Each tile keeps its partial slot and its row
+// block's reduction (same sums, same order): bit-identical to the tile kernels.
+template <int NR, int CH, int kFwdTileCols, int DEPTH>
+__global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_pstrip(const FTile* __restrict__ tiles, const int2* __restrict__ strips,
+                                                    const int* __restrict__ sids, int first, const double* __restrict__ Gt,
+                                                    const long long* __restrict__ ell, const double* __restrict__ B0,
+                                                    const double* __restrict__ B1, double* __restrict__ part,
+                                                    const FRed* __restrict__ reds, int* __restrict__ cnt,
+                                                    double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
+                                                    int gate_reject, int ext_off) {
+    if (solve_gated(ctrl, gate_reject)) return;
+    __shared__ double f[NR * kFwdTileCols];
+    __shared__ double red[3][NR * 64];
+    const int2 st = strips[first + blockIdx.x];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, w = tid >> 6;
+    constexpr int per = kFwdTileCols / 4;
+    constexpr int C = CH < per ? CH : per;
+    constexpr int NC = per / C;
+    constexpr int C2 = C / 2;
+    constexpr int DP = DEPTH < NC ? DEPTH : NC;
+    const int i0 = w * per;
+    {   // the strip's front slice, once
+        const FTile t = tiles[sids[st.x]];
+        for (int i = tid; i < kFwdTileCols; i += 256) {
+            if (i < t.nc) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i, ext_off);
+            else zero<NR>(f + NR * i);
+        }
+    }
+    __syncthreads();
+    for (int j = 0; j < st.y; ++j) {
+        const FTile t = tiles[sids[st.x + j]];
+        int nloc = min(per, t.nc - i0);
+        if (t.r0 + 64 <= t.p) nloc = min(nloc, t.r0 + 64 - (t.c0 + i0));
+        const bool live = nloc > 0;
+        const int qmax = (nloc - 1) >> 1;
+        const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * (per / 2) * 64 + lane;
+        double2 gbuf[DP][C2];
+        auto ld = [&](double2* g, int k) {
+#pragma unroll
+            for (int q = 0; q < C2; ++q) g[q] = G[(size_t)min(k * C2 + q, qmax) * 64];
+        };
+        double a[NR];
+        zero<NR>(a);
+        if (live) {
+#pragma unroll
+            for (int d = 0; d < DP; ++d) ld(gbuf[d], d);
+            auto use = [&](const double2* g, int k) {
+#pragma unroll
+                for (int q = 0; q < C2; ++q) {
+                    const int i = k * C + 2 * q;
+                    const double g0 = i < nloc ? g[q].x : 0.0;
+                    const double g1 = i + 1 < nloc ? g[q].y : 0.0;
+#pragma unroll
+                    for (int m = 0; m < NR; ++m) a[m] += g0 * f[NR * (i0 + i) + m];
+#pragma unroll
+                    for (int m = 0; m < NR; ++m) a[m] += g1 * f[NR * (i0 + i + 1) + m];
+                }
+            };
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                use(gbuf[k % DP], k);
+                if (k + DP < NC) ld(gbuf[k % DP], k + DP);
+            }
+        }
+        __syncthreads();   // wave 0 has read the previous tile's red
+        if (w > 0)
+#pragma unroll
+            for (int k = 0; k < NR; ++k) red[w - 1][NR * lane + k] = a[k];
+        __syncthreads();
+        if (w != 0) continue;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int k = 0; k < NR; ++k) a[k] += red[q][NR * lane + k];
+        double* o = part + (NR / 3) * t.poff + NR * lane;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) st_sc1(o + k, a[k]);
+        const FRed rd = reds[t.rid];
+        if (!arrive_last(cnt + t.rid, rd.nt, lane)) continue;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (lane < rd.nr) {
+            const int rr = rd.r0 + lane;
+            double fr[NR];
+            if (rr >= rd.p) front_row<NR>(rd, rr, ell, B0, B1, U, fr, ext_off);
+            double b[NR];
+            zero<NR>(b);
+            const double* q = part + (NR / 3) * rd.poff + NR * lane;
+#pragma unroll 8
+            for (int k = 0; k < rd.nt; ++k, q += NR * 64)
+#pragma unroll
+                for (int m = 0; m < NR; ++m) b[m] += q[m];
+            if (rr < rd.p) {
+                double* y = Y + NR * (size_t)(rd.beg + rr);
+#pragma unroll
+                for (int k = 0; k < NR; ++k) y[k] = b[k];
+            } else {
+                double* u = U + (NR / 3) * rd.uoff + NR * (size_t)(rr - rd.p);
+#pragma unroll
+                for (int k = 0; k < NR; ++k) u[k] = fr[k] - b[k];
+            }
+        }
+        if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int NR, int CH, int kBwdTileRows, int DEPTH>
 __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __restrict__ tiles, int first,
                                                    const double* __restrict__ Gt, const int* __restrict__ bnd,
                                                    const double* __restrict__ Y, double* __restrict__ X0,
@@ -527,14 +639,15 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
     const int nloc = min(per, t.nr - i0);
     const bool live = nloc > 0;   // wave-uniform: columns past p read the block's zero padding
     const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * per * 64 + lane;
-    double2 ga[C], gb[C];
+    constexpr int DP = DEPTH < NC ? DEPTH : NC;   // chunks in flight
+    double2 gbuf[DP][C];
     auto ld = [&](double2* g, int k) {
 #pragma unroll
         for (int q = 0; q < C; ++q) g[q] = G[(size_t)min(k * C + q, nloc - 1) * 64];
     };
     if (live) {
-        ld(ga, 0);
-        if (NC > 1) ld(gb, 1);
+#pragma unroll
+        for (int d = 0; d < DP; ++d) ld(gbuf[d], d);
     }
     for (int i = tid; i < kBwdTileRows; i += 256) {
         if (i < t.nr) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
@@ -559,8 +672,8 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
         };
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
-            if (k & 1) { use(gb, k); if (k + 2 < NC) ld(gb, k + 2); }
-            else       { use(ga, k); if (k + 2 < NC) ld(ga, k + 2); }
+            use(gbuf[k % DP], k);
+            if (k + DP < NC) ld(gbuf[k % DP], k + DP);
         }
     }
     if (w > 0)
@@ -662,20 +775,31 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
                                                  const double* __restrict__ Gc, const long long* __restrict__ ell,
                                                  const double* __restrict__ B0, const double* __restrict__ B1,
                                                  double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
-                                                 int gate_reject, long long* clk, int clk_stride) {
+                                                 int gate_reject, long long* clk, int clk_stride, int node_off) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int K = NR / 3;
     const SubTree T = trees[blockIdx.x];
     const int tid = threadIdx.x;
+    // the subtree's supernode records, staged in LDS once: a row item then needs one (coalesced)
+    // load, its item, before its factor stream, instead of the item and then its record
+    SubNode* sn = reinterpret_cast<SubNode*>(reinterpret_cast<char*>(lds) + node_off);
+    {
+        const long long* src = reinterpret_cast<const long long*>(nodes + T.node0);
+        long long* dst = reinterpret_cast<long long*>(sn);
+        constexpr int W8 = sizeof(SubNode) / 8;
+        for (int i = tid; i < T.nnode * W8; i += BLOCK) dst[i] = src[i];
+    }
+    __syncthreads();
     // optional phase clock (AA_SUB_TIMING): kernel start, then after every barrier
     long long* ck = clk ? clk + (size_t)blockIdx.x * clk_stride : nullptr;
     if (ck && tid == 0) ck[0] = (long long)__builtin_amdgcn_s_memrealtime();
     for (int l = 0; l < T.nlvl; ++l) {
         const SubLevel L = lvls[T.lvl0 + l];
+        const SubNode* ln = sn + (L.n0 - T.node0);
         for (int i = tid; i < L.nfa; i += BLOCK) {          // front vectors f_P of the level's supernodes
             const int it = items[L.fa0 + i];
-            const SubNode nd = nodes[L.n0 + (it >> 16)];
+            const SubNode nd = ln[it >> 16];
             const int c = it & 0xffff;
             front_row<NR>(nd, c, ell, B0, B1, U, lds + K * nd.lds + NR * c);
         }
@@ -683,7 +807,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
         if (ck && tid == 0) ck[1 + 2 * l] = (long long)__builtin_amdgcn_s_memrealtime();
         for (int i = tid; i < L.nfr; i += BLOCK) {          // rows of G . f_P
             const int it = items[L.fr0 + i];
-            const SubNode nd = nodes[L.n0 + (it >> 16)];
+            const SubNode nd = ln[it >> 16];
             const int r = it & 0xffff, p = nd.p, R = p + nd.nb;
             const double* f = lds + K * nd.lds;
             const double* G = Gc + nd.goff + r;
@@ -735,20 +859,29 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
                                                  const double* __restrict__ Gr, const int* __restrict__ bnd,
                                                  const double* __restrict__ Y, double* __restrict__ X0,
                                                  double* __restrict__ X1, const Ctrl* ctrl, int gate_reject,
-                                                 long long* clk, int clk_stride) {
+                                                 long long* clk, int clk_stride, int node_off) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int K = NR / 3;
     const SubTree T = trees[blockIdx.x];
     const int tid = threadIdx.x;
+    SubNode* sn = reinterpret_cast<SubNode*>(reinterpret_cast<char*>(lds) + node_off);   // as k_fwd_sub
+    {
+        const long long* src = reinterpret_cast<const long long*>(nodes + T.node0);
+        long long* dst = reinterpret_cast<long long*>(sn);
+        constexpr int W8 = sizeof(SubNode) / 8;
+        for (int i = tid; i < T.nnode * W8; i += BLOCK) dst[i] = src[i];
+    }
+    __syncthreads();
     long long* ck = clk ? clk + (size_t)blockIdx.x * clk_stride : nullptr;
     if (ck && tid == 0) ck[0] = (long long)__builtin_amdgcn_s_memrealtime();
     int ph = 1;
     for (int l = T.nlvl - 1; l >= 0; --l) {
         const SubLevel L = lvls[T.lvl0 + l];
+        const SubNode* ln = sn + (L.n0 - T.node0);
         for (int i = tid; i < L.nbv; i += BLOCK) {          // [y_P ; -x_B] of the level's supernodes
             const int it = items[L.bv0 + i];
-            const SubNode nd = nodes[L.n0 + (it >> 16)];
+            const SubNode nd = ln[it >> 16];
             const int r = it & 0xffff;
             bwd_row<NR>(nd, r, bnd, Y, X0, X1, lds + K * nd.lds + NR * r);
         }
@@ -756,7 +889,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
         if (ck && tid == 0) ck[ph++] = (long long)__builtin_amdgcn_s_memrealtime();
         for (int i = tid; i < L.nbs; i += BLOCK) {          // segment partials of G^T . v
             const long long it = items2[L.bs0 + i];
-            const SubNode nd = nodes[L.n0 + (int)(it >> 40)];
+            const SubNode nd = ln[(int)(it >> 40)];
             const int seg = (int)((it >> 20) & 0xfffff), j = (int)(it & 0xfffff), p = nd.p, R = p + nd.nb;
             const double* v = lds + K * nd.lds;
             const double* G = Gr + nd.goff + j;
@@ -778,7 +911,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
         if (ck && tid == 0) ck[ph++] = (long long)__builtin_amdgcn_s_memrealtime();
         for (int i = tid; i < L.nbc; i += BLOCK) {          // columns: sum of their segments
             const int it = items[L.bc0 + i];
-            const SubNode nd = nodes[L.n0 + (it >> 16)];
+            const SubNode nd = ln[it >> 16];
             const int j = it & 0xffff, p = nd.p, R = p + nd.nb;
             const int nseg = (R + kSubSegRows - 1) / kSubSegRows, s0 = j / kSubSegRows;
             int off = sub_seg_off(s0, p);
@@ -992,7 +1125,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
             for (int rt : roots_at(cut_height_)) {
                 std::vector<int> all = collect(rt);
                 const int H = F.height[rt];
-                SubTree T{(int)slevels.size(), H + 1};
+                SubTree T{(int)slevels.size(), H + 1, (int)snodes.size(), 0};
                 for (int h = 0; h <= H; ++h) {
                     SubLevel L{};
                     L.n0 = (int)snodes.size();
@@ -1054,6 +1187,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     sub_lds_b_ = std::max(sub_lds_b_, lb);
                     slevels.push_back(L);
                 }
+                T.nnode = (int)snodes.size() - T.node0;
+                sub_nodes_max_ = std::max(sub_nodes_max_, T.nnode);
                 strees.push_back(T);
             }
         }
@@ -1106,6 +1241,14 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     std::vector<FTile> ftiles;
     std::vector<FRed> freds;
     std::vector<int> fwid, bwid;   // tile widths (packing)
+    std::vector<int2> fstrips;
+    std::vector<int> fsids;
+    {
+        const char* sm = std::getenv("AA_STRIP");
+        const char* sn = std::getenv("AA_STRIP_MIN");
+        strip_max_ = sm ? std::max(0, std::atoi(sm)) : 4;
+        strip_min_ = sn ? std::max(1, std::atoi(sn)) : 512;
+    }
     long long poff = 0;
     auto mk = [&](int sn, int r0, int nr) {
         Task t{};
@@ -1196,6 +1339,21 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         }
         L.ft_count = (int)ftiles.size() - L.ft_first;
         L.frd_count = (int)freds.size() - L.fr_first;
+        // forward strips over this level's tiles: the tiles of one (supernode, column slice) in
+        // row order, cut into runs of S (as many as keep >= strip_min_ strips on the level)
+        L.fs_first = (int)fstrips.size();
+        if (strip_max_ > 0 && L.ft_count > 0) {
+            const int S = std::max(1, std::min(strip_max_, L.ft_count / strip_min_));
+            std::map<std::pair<long long, int>, std::vector<int>> by;   // (goff, c0) -> tiles, r0 ascending
+            for (int i = L.ft_first; i < L.ft_first + L.ft_count; ++i) by[{ftiles[i].goff, ftiles[i].c0}].push_back(i);
+            for (auto& kv : by)
+                for (size_t a = 0; a < kv.second.size(); a += S) {
+                    const int n = (int)std::min<size_t>(S, kv.second.size() - a);
+                    fstrips.push_back(make_int2((int)fsids.size(), n));
+                    for (int q = 0; q < n; ++q) fsids.push_back(kv.second[a + q]);
+                }
+        }
+        L.fs_count = (int)fstrips.size() - L.fs_first;
         L.bwd_first = (int)tasks.size();
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
@@ -1353,6 +1511,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     {
         const char* pk = std::getenv("AA_SOLVE_PACKED");
         packed_ = !(pk && pk[0] == '0');
+        // chunks of a packed tile's factor stream in flight per wave (AA_TILE_DEPTH_F / _B: 2..4)
+        const char* df = std::getenv("AA_TILE_DEPTH_F");
+        const char* db = std::getenv("AA_TILE_DEPTH_B");
+        depth_f_ = df ? std::max(2, std::min(4, std::atoi(df))) : 2;
+        depth_b_ = db ? std::max(2, std::min(4, std::atoi(db))) : 2;
     }
     if (packed_ && (!ftiles.empty() || !btiles.empty())) {
         long long to = 0;
@@ -1380,6 +1543,9 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     } else {
         packed_ = false;
     }
+    if (!packed_) { fstrips.clear(); fsids.clear(); for (auto& L : levels_) L.fs_count = 0; }
+    fstrips_.upload(fstrips, s);
+    fsids_.upload(fsids, s);
     tasks_.upload(tasks, s);
     btiles_.upload(btiles, s);
     ftiles_.upload(ftiles, s);
@@ -1390,8 +1556,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     bpart_.alloc(std::max<long long>(KS * poff, 3));
     Y_.alloc(3 * KS * (size_t)n_);
     U_.alloc(std::max<long long>(KS * uo, 3));
-    // (LDS figures above are per 3 columns; a 6-column solve needs twice as much)
-    if (KS * std::max(sub_lds_f_, sub_lds_b_) > 64 * 1024)
+    // (LDS figures above are per 3 columns; a 6-column solve needs twice as much; + the staged nodes)
+    if (std::max(sub_lds_bytes(KS, true), sub_lds_bytes(KS, false)) > 64 * 1024)
         for (const void* k : {(const void*)k_fwd_sub<256, 3>, (const void*)k_fwd_sub<512, 3>, (const void*)k_fwd_sub<1024, 3>,
                               (const void*)k_bwd_sub<256, 3>, (const void*)k_bwd_sub<512, 3>, (const void*)k_bwd_sub<1024, 3>,
                               (const void*)k_fwd_sub<256, 6>, (const void*)k_fwd_sub<512, 6>, (const void*)k_fwd_sub<1024, 6>,
@@ -1411,6 +1577,12 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     AA_HIP(hipStreamSynchronize(s));
 }
 
+// dynamic LDS of a fused-subtree launch: the level vectors (K sets), then the staged node records
+size_t DirectSolver::sub_lds_bytes(int K, bool fwd) const {
+    const size_t v = (size_t)K * (fwd ? sub_lds_f_ : sub_lds_b_);
+    return (v + 15) / 16 * 16 + (size_t)sub_nodes_max_ * sizeof(SubNode);
+}
+
 void DirectSolver::solve(const double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
     solve_nr<3>(b, x, nullptr, nullptr, ctrl, gate_reject, s);
 }
@@ -1427,7 +1599,9 @@ template <int NR>
 void DirectSolver::launch_ftiles(int w, int count, int first, const double* b0, const double* b1, int ext_off,
                                  const Ctrl* ctrl, int gate_reject, hipStream_t s) {
     if (packed_) {
-        auto kf = w == 256 ? k_fwd_ptile<NR, AA_FWD_CH, 256> : (w == 128 ? k_fwd_ptile<NR, AA_FWD_CH, 128> : k_fwd_ptile<NR, AA_FWD_CH, 64>);
+#define FSEL(D) (w == 256 ? k_fwd_ptile<NR, AA_FWD_CH, 256, D> : (w == 128 ? k_fwd_ptile<NR, AA_FWD_CH, 128, D> : k_fwd_ptile<NR, AA_FWD_CH, 64, D>))
+        auto kf = depth_f_ >= 4 ? FSEL(4) : (depth_f_ == 3 ? FSEL(3) : FSEL(2));
+#undef FSEL
         hipLaunchKernelGGL(kf, dim3(count), dim3(256), 0, s, ftiles_.p, first, Gt_.p, ell_.p, b0, b1, bpart_.p, freds_.p,
                            fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, ext_off);
     } else {
@@ -1437,10 +1611,22 @@ void DirectSolver::launch_ftiles(int w, int count, int first, const double* b0, 
     }
 }
 template <int NR>
+void DirectSolver::launch_fstrips(const Level& L, const double* b0, const double* b1, const Ctrl* ctrl, int gate_reject,
+                                  hipStream_t s) {
+#define SSEL(D) (L.ftw == 256 ? k_fwd_pstrip<NR, AA_FWD_CH, 256, D> : (L.ftw == 128 ? k_fwd_pstrip<NR, AA_FWD_CH, 128, D> : k_fwd_pstrip<NR, AA_FWD_CH, 64, D>))
+    auto kf = depth_f_ >= 4 ? SSEL(4) : (depth_f_ == 3 ? SSEL(3) : SSEL(2));
+#undef SSEL
+    hipLaunchKernelGGL(kf, dim3(L.fs_count), dim3(256), 0, s, ftiles_.p, fstrips_.p, fsids_.p, L.fs_first, Gt_.p, ell_.p, b0, b1,
+                       bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, 0);
+}
+
+template <int NR>
 void DirectSolver::launch_btiles(int w, int count, int first, double* x0, double* x1, int ext_off, const Ctrl* ctrl,
                                  int gate_reject, hipStream_t s) {
     if (packed_) {
-        auto kb = w == 256 ? k_bwd_ptile<NR, AA_BWD_CH, 256> : (w == 128 ? k_bwd_ptile<NR, AA_BWD_CH, 128> : k_bwd_ptile<NR, AA_BWD_CH, 64>);
+#define BSEL(D) (w == 256 ? k_bwd_ptile<NR, AA_BWD_CH, 256, D> : (w == 128 ? k_bwd_ptile<NR, AA_BWD_CH, 128, D> : k_bwd_ptile<NR, AA_BWD_CH, 64, D>))
+        auto kb = depth_b_ >= 4 ? BSEL(4) : (depth_b_ == 3 ? BSEL(3) : BSEL(2));
+#undef BSEL
         hipLaunchKernelGGL(kb, dim3(count), dim3(256), 0, s, btiles_.p, first, Gt_.p, bnd_.p, Y_.p, x0, x1, bpart_.p,
                            breds_.p, bcnt_.p, ctrl, gate_reject, ext_off);
     } else {
@@ -1459,9 +1645,10 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
     AA_HIP(hipStreamIsCapturing(s, &cst));
     const bool clk_on = sub_timing_ > 0 && cst == hipStreamCaptureStatusNone && n_sub_ > 0;
-#define SUBF(BL) hipLaunchKernelGGL((k_fwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_f_, s, sub_trees_.p, \
+    const int noff_f = (K * sub_lds_f_ + 15) / 16 * 16, noff_b = (K * sub_lds_b_ + 15) / 16 * 16;
+#define SUBF(BL) hipLaunchKernelGGL((k_fwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, true), s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject, \
-                                    clk_on ? sub_clk_.p : nullptr, 64)
+                                    clk_on ? sub_clk_.p : nullptr, 64, noff_f)
     if (n_sub_) switch (sub_block_) { case 1024: SUBF(1024); break; case 512: SUBF(512); break; default: SUBF(256); break; }
 #undef SUBF
     for (auto& L : levels_) {
@@ -1469,7 +1656,8 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
                                    ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
-        if (L.ft_count) launch_ftiles<NR>(L.ftw, L.ft_count, L.ft_first, b0, b1, 0, ctrl, gate_reject, s);
+        if (L.fs_count) launch_fstrips<NR>(L, b0, b1, ctrl, gate_reject, s);
+        else if (L.ft_count) launch_ftiles<NR>(L.ftw, L.ft_count, L.ft_first, b0, b1, 0, ctrl, gate_reject, s);
     }
     // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
     // and in the update vectors); their sum over the GPUs is the full forward result. When the
@@ -1507,9 +1695,9 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
 #undef BWD
         if (L.bt_count) launch_btiles<NR>(L.btw, L.bt_count, L.bt_first, x0, x1, 0, ctrl, gate_reject, s);
     }
-#define SUBB(BL) hipLaunchKernelGGL((k_bwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), K * sub_lds_b_, s, sub_trees_.p, \
+#define SUBB(BL) hipLaunchKernelGGL((k_bwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, false), s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, \
-                                    ctrl, gate_reject, clk_on ? sub_clk_.p + 64 * (size_t)n_sub_ : nullptr, 64)
+                                    ctrl, gate_reject, clk_on ? sub_clk_.p + 64 * (size_t)n_sub_ : nullptr, 64, noff_b)
     if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }
 #undef SUBB
     AA_CHECK_LAUNCH();

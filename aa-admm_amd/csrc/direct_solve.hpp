@@ -74,7 +74,7 @@ public:
         long long goff, uoff, ell_off;
     };
     struct SubLevel { int n0, fa0, nfa, fr0, nfr, bv0, nbv, bc0, nbc, bs0, nbs, pad; };   // item ranges
-    struct SubTree { int lvl0, nlvl; };
+    struct SubTree { int lvl0, nlvl, node0, nnode; };   // nodes [node0, node0 + nnode) staged in LDS
     // split-K backward of large supernodes: a tile (64 columns from c0, nr rows from r0) and the
     // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
     // toff: the tile's block in the packed tile stream Gt_ (see build: every tile's factor entries
@@ -93,6 +93,7 @@ private:
         int ft_first = 0, ft_count = 0, fr_first = 0, frd_count = 0;  // split-K forward tiles
         int fblock = 256, bblock = 256, lds_fwd = 0, lds_bwd = 0;
         int ftw = 256, btw = 256;   // split-K tile widths (forward columns / backward rows)
+        int fs_first = 0, fs_count = 0;   // forward strips (packed tiles, k_fwd_pstrip)
     };
     int n_ = 0, nn_ = 0, kernels_ = 0, top_beg_ = 0;
     Comm* comm_ = nullptr;
@@ -116,6 +117,15 @@ private:
     // backward [wave][row][column pair][2]; zero-padded to whole tiles
     DevBuf<double> Gt_;
     bool packed_ = true;
+    int depth_f_ = 2, depth_b_ = 2;   // chunks in flight per wave in the packed tiles
+    // forward strips: {first index into fsids_, tile count}; AA_STRIP = most tiles per strip
+    // (0 = no strips), AA_STRIP_MIN = strips a level keeps at least
+    DevBuf<int2> fstrips_;
+    DevBuf<int> fsids_;
+    int strip_max_ = 4, strip_min_ = 512;
+    template <int NR>
+    void launch_fstrips(const Level& L, const double* b0, const double* b1, const Ctrl* ctrl, int gate_reject,
+                        hipStream_t s);
     DevBuf<Task> tasks_;
     DevBuf<BTile> btiles_;
     DevBuf<BRed> breds_;
@@ -135,7 +145,8 @@ private:
     DevBuf<Task> top_task_d_;
     DevBuf<double> top_f_, top_x_;   // [set][3 * top_p_]: summed front, partial then summed x_top
     // fused bottom subtrees
-    int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1, sub_block_ = 256;
+    int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1, sub_block_ = 256, sub_nodes_max_ = 0;
+    size_t sub_lds_bytes(int K, bool fwd) const;
     int wave_p_ = kWaveP, wave_r_ = kWaveR;   // row-task / split-K thresholds (AA_SOLVE_WAVEP / _WAVER)
     DevBuf<SubNode> sub_nodes_;
     DevBuf<SubLevel> sub_levels_;

@@ -488,11 +488,24 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
         d.idx = dg.idx.p;
         d.prm = dg.prm.p;
         d.warm = nullptr;
+        d.order = nullptr;
         d.surf = SurfDev{nullptr, nullptr, 0, 0};
         if (hg.surf >= 0) {
             dg.warm.alloc(cnt);
             d.warm = dg.warm.p;
             d.surf = surfs_[hg.surf].dev();
+            if (sort_period_ > 0 && cnt >= 4096 && !plain_) {   // queries ordered by warm triangle
+                std::vector<int> iota(cnt);
+                for (int e = 0; e < cnt; ++e) iota[e] = e;
+                dg.order.upload(iota, s());
+                dg.skeys.alloc(cnt); dg.skeys2.alloc(cnt); dg.svals.alloc(cnt);
+                int bits = 1;
+                while ((1LL << bits) < (long long)surfs_[hg.surf].tris.size() + 2) ++bits;
+                dg.sort_bits = bits;
+                dg.stemp_bytes = warm_sort_bytes(cnt, bits);
+                dg.stemp.alloc(std::max<size_t>(dg.stemp_bytes, 1));
+                d.order = dg.order.p;
+            }
         }
         if (d.hard) { Zh_ += 3LL * C * cnt; red_blocks_ += geo_u_blocks(cnt); }
         if (!hg.hard) soft_cols += (long long)C * cnt;
@@ -694,6 +707,22 @@ void GeomSolver::enqueue_iteration_plain(int m) {
     ev_mark("aa");
 }
 
+// closest-point groups: re-order the constraints by their warm triangles (GeoGroupDev::order)
+void GeomSolver::enqueue_warm_sorts() {
+    for (auto& g : groups_)
+        if (g.d.order)
+            launch_warm_sort(g.d, g.skeys.p, g.skeys2.p, g.svals.p, g.order.p, g.stemp.p, g.stemp_bytes, g.sort_bits, s());
+}
+
+// one chunk of loop passes; the closest-point queries are re-sorted by warm triangle after the
+// chunk's first pass and then every sort_period_ passes (AA_SURF_SORT)
+void GeomSolver::enqueue_chunk(int chunk, int m) {
+    for (int i = 0; i < chunk; ++i) {
+        if (sort_period_ > 0 && i % sort_period_ == 1) enqueue_warm_sorts();
+        enqueue_iteration(m);
+    }
+}
+
 void GeomSolver::ev_mark(const char* name) {
     if (!instrument_) return;
     hipEvent_t e;
@@ -805,7 +834,7 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
     auto run_chunk = [&]() {
         if (use_graph && (!gexec_ || graph_chunk_ != chunk || graph_m_ != m)) {
             drop_graph();
-            bool ok = capture_graph(s(), [&] { for (int i = 0; i < chunk; ++i) enqueue_iteration(m); }, &graph_, &gexec_);
+            bool ok = capture_graph(s(), [&] { enqueue_chunk(chunk, m); }, &graph_, &gexec_);
             if (comm_) {   // the ranks replay or launch eagerly together
                 double f = ok ? 0.0 : 1.0;
                 comm_->allreduce_sum_host(&f, 1);
@@ -818,7 +847,7 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
         if (use_graph) {
             AA_HIP(hipGraphLaunch(gexec_, s()));
         } else {
-            for (int i = 0; i < chunk; ++i) enqueue_iteration(m);
+            enqueue_chunk(chunk, m);
         }
     };
     // no rejection: exactly ceil(target / chunk) chunks; each rejection adds one x-update
@@ -893,7 +922,7 @@ double GeomSolver::bench_iterations(int iters) {
     hipEvent_t e0, e1;
     AA_HIP(hipEventCreate(&e0)); AA_HIP(hipEventCreate(&e1));
     AA_HIP(hipEventRecord(e0, s()));
-    for (int it = 0; it < iters; ++it) enqueue_iteration(cur_m_);
+    enqueue_chunk(iters, cur_m_);
     AA_HIP(hipEventRecord(e1, s()));
     AA_HIP(hipEventSynchronize(e1));
     instrument_ = false;
