@@ -7,7 +7,6 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
-#include <map>
 #include <memory>
 #include <string>
 
@@ -200,6 +199,11 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
 #endif
 #ifndef AA_BWD_CH
 #define AA_BWD_CH 8
+#endif
+// chunks of a packed tile's factor stream in flight per wave (build-time; 3 and 4 measured
+// slower on C4: 2 waves fewer per SIMD, or no gain at 128 VGPRs -- DESIGN.md §3.2)
+#ifndef AA_TILE_DEPTH
+#define AA_TILE_DEPTH 2
 #endif
 using BTile = DirectSolver::BTile;
 using BRed = DirectSolver::BRed;
@@ -506,116 +510,6 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
         }
     }
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Forward strips (packed tiles): one workgroup runs the split-K tiles of ONE column slice
-// [c0, c0 + W) of a supernode over several consecutive row blocks. The front slice (b + the
-// children's update vectors, pulled through the ELL lists) is gathered once per strip instead of
-// once per tile -- per tile it was ~1/3 of the tile's own bytes again (profiles/r3_c4_solve_pmc_table.txt)
-// -- and the workgroup streams tile after tile. Each tile keeps its partial slot and its row
-// block's reduction (same sums, same order): bit-identical to the tile kernels.
-template <int NR, int CH, int kFwdTileCols, int DEPTH>
-__global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_pstrip(const FTile* __restrict__ tiles, const int2* __restrict__ strips,
-                                                    const int* __restrict__ sids, int first, const double* __restrict__ Gt,
-                                                    const long long* __restrict__ ell, const double* __restrict__ B0,
-                                                    const double* __restrict__ B1, double* __restrict__ part,
-                                                    const FRed* __restrict__ reds, int* __restrict__ cnt,
-                                                    double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
-                                                    int gate_reject, int ext_off) {
-    if (solve_gated(ctrl, gate_reject)) return;
-    __shared__ double f[NR * kFwdTileCols];
-    __shared__ double red[3][NR * 64];
-    const int2 st = strips[first + blockIdx.x];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, w = tid >> 6;
-    constexpr int per = kFwdTileCols / 4;
-    constexpr int C = CH < per ? CH : per;
-    constexpr int NC = per / C;
-    constexpr int C2 = C / 2;
-    constexpr int DP = DEPTH < NC ? DEPTH : NC;
-    const int i0 = w * per;
-    {   // the strip's front slice, once
-        const FTile t = tiles[sids[st.x]];
-        for (int i = tid; i < kFwdTileCols; i += 256) {
-            if (i < t.nc) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i, ext_off);
-            else zero<NR>(f + NR * i);
-        }
-    }
-    __syncthreads();
-    for (int j = 0; j < st.y; ++j) {
-        const FTile t = tiles[sids[st.x + j]];
-        int nloc = min(per, t.nc - i0);
-        if (t.r0 + 64 <= t.p) nloc = min(nloc, t.r0 + 64 - (t.c0 + i0));
-        const bool live = nloc > 0;
-        const int qmax = (nloc - 1) >> 1;
-        const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * (per / 2) * 64 + lane;
-        double2 gbuf[DP][C2];
-        auto ld = [&](double2* g, int k) {
-#pragma unroll
-            for (int q = 0; q < C2; ++q) g[q] = G[(size_t)min(k * C2 + q, qmax) * 64];
-        };
-        double a[NR];
-        zero<NR>(a);
-        if (live) {
-#pragma unroll
-            for (int d = 0; d < DP; ++d) ld(gbuf[d], d);
-            auto use = [&](const double2* g, int k) {
-#pragma unroll
-                for (int q = 0; q < C2; ++q) {
-                    const int i = k * C + 2 * q;
-                    const double g0 = i < nloc ? g[q].x : 0.0;
-                    const double g1 = i + 1 < nloc ? g[q].y : 0.0;
-#pragma unroll
-                    for (int m = 0; m < NR; ++m) a[m] += g0 * f[NR * (i0 + i) + m];
-#pragma unroll
-                    for (int m = 0; m < NR; ++m) a[m] += g1 * f[NR * (i0 + i + 1) + m];
-                }
-            };
-#pragma unroll
-            for (int k = 0; k < NC; ++k) {
-                use(gbuf[k % DP], k);
-                if (k + DP < NC) ld(gbuf[k % DP], k + DP);
-            }
-        }
-        __syncthreads();   // wave 0 has read the previous tile's red
-        if (w > 0)
-#pragma unroll
-            for (int k = 0; k < NR; ++k) red[w - 1][NR * lane + k] = a[k];
-        __syncthreads();
-        if (w != 0) continue;
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-#pragma unroll
-            for (int k = 0; k < NR; ++k) a[k] += red[q][NR * lane + k];
-        double* o = part + (NR / 3) * t.poff + NR * lane;
-#pragma unroll
-        for (int k = 0; k < NR; ++k) st_sc1(o + k, a[k]);
-        const FRed rd = reds[t.rid];
-        if (!arrive_last(cnt + t.rid, rd.nt, lane)) continue;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (lane < rd.nr) {
-            const int rr = rd.r0 + lane;
-            double fr[NR];
-            if (rr >= rd.p) front_row<NR>(rd, rr, ell, B0, B1, U, fr, ext_off);
-            double b[NR];
-            zero<NR>(b);
-            const double* q = part + (NR / 3) * rd.poff + NR * lane;
-#pragma unroll 8
-            for (int k = 0; k < rd.nt; ++k, q += NR * 64)
-#pragma unroll
-                for (int m = 0; m < NR; ++m) b[m] += q[m];
-            if (rr < rd.p) {
-                double* y = Y + NR * (size_t)(rd.beg + rr);
-#pragma unroll
-                for (int k = 0; k < NR; ++k) y[k] = b[k];
-            } else {
-                double* u = U + (NR / 3) * rd.uoff + NR * (size_t)(rr - rd.p);
-#pragma unroll
-                for (int k = 0; k < NR; ++k) u[k] = fr[k] - b[k];
-            }
-        }
-        if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 template <int NR, int CH, int kBwdTileRows, int DEPTH>
@@ -1241,14 +1135,6 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     std::vector<FTile> ftiles;
     std::vector<FRed> freds;
     std::vector<int> fwid, bwid;   // tile widths (packing)
-    std::vector<int2> fstrips;
-    std::vector<int> fsids;
-    {
-        const char* sm = std::getenv("AA_STRIP");
-        const char* sn = std::getenv("AA_STRIP_MIN");
-        strip_max_ = sm ? std::max(0, std::atoi(sm)) : 4;
-        strip_min_ = sn ? std::max(1, std::atoi(sn)) : 512;
-    }
     long long poff = 0;
     auto mk = [&](int sn, int r0, int nr) {
         Task t{};
@@ -1339,21 +1225,6 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         }
         L.ft_count = (int)ftiles.size() - L.ft_first;
         L.frd_count = (int)freds.size() - L.fr_first;
-        // forward strips over this level's tiles: the tiles of one (supernode, column slice) in
-        // row order, cut into runs of S (as many as keep >= strip_min_ strips on the level)
-        L.fs_first = (int)fstrips.size();
-        if (strip_max_ > 0 && L.ft_count > 0) {
-            const int S = std::max(1, std::min(strip_max_, L.ft_count / strip_min_));
-            std::map<std::pair<long long, int>, std::vector<int>> by;   // (goff, c0) -> tiles, r0 ascending
-            for (int i = L.ft_first; i < L.ft_first + L.ft_count; ++i) by[{ftiles[i].goff, ftiles[i].c0}].push_back(i);
-            for (auto& kv : by)
-                for (size_t a = 0; a < kv.second.size(); a += S) {
-                    const int n = (int)std::min<size_t>(S, kv.second.size() - a);
-                    fstrips.push_back(make_int2((int)fsids.size(), n));
-                    for (int q = 0; q < n; ++q) fsids.push_back(kv.second[a + q]);
-                }
-        }
-        L.fs_count = (int)fstrips.size() - L.fs_first;
         L.bwd_first = (int)tasks.size();
         for (int sn : l) {
             const int R = p[sn] + nb[sn];
@@ -1511,11 +1382,6 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     {
         const char* pk = std::getenv("AA_SOLVE_PACKED");
         packed_ = !(pk && pk[0] == '0');
-        // chunks of a packed tile's factor stream in flight per wave (AA_TILE_DEPTH_F / _B: 2..4)
-        const char* df = std::getenv("AA_TILE_DEPTH_F");
-        const char* db = std::getenv("AA_TILE_DEPTH_B");
-        depth_f_ = df ? std::max(2, std::min(4, std::atoi(df))) : 2;
-        depth_b_ = db ? std::max(2, std::min(4, std::atoi(db))) : 2;
     }
     if (packed_ && (!ftiles.empty() || !btiles.empty())) {
         long long to = 0;
@@ -1543,9 +1409,6 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     } else {
         packed_ = false;
     }
-    if (!packed_) { fstrips.clear(); fsids.clear(); for (auto& L : levels_) L.fs_count = 0; }
-    fstrips_.upload(fstrips, s);
-    fsids_.upload(fsids, s);
     tasks_.upload(tasks, s);
     btiles_.upload(btiles, s);
     ftiles_.upload(ftiles, s);
@@ -1599,9 +1462,8 @@ template <int NR>
 void DirectSolver::launch_ftiles(int w, int count, int first, const double* b0, const double* b1, int ext_off,
                                  const Ctrl* ctrl, int gate_reject, hipStream_t s) {
     if (packed_) {
-#define FSEL(D) (w == 256 ? k_fwd_ptile<NR, AA_FWD_CH, 256, D> : (w == 128 ? k_fwd_ptile<NR, AA_FWD_CH, 128, D> : k_fwd_ptile<NR, AA_FWD_CH, 64, D>))
-        auto kf = depth_f_ >= 4 ? FSEL(4) : (depth_f_ == 3 ? FSEL(3) : FSEL(2));
-#undef FSEL
+        auto kf = w == 256 ? k_fwd_ptile<NR, AA_FWD_CH, 256, AA_TILE_DEPTH>
+                           : (w == 128 ? k_fwd_ptile<NR, AA_FWD_CH, 128, AA_TILE_DEPTH> : k_fwd_ptile<NR, AA_FWD_CH, 64, AA_TILE_DEPTH>);
         hipLaunchKernelGGL(kf, dim3(count), dim3(256), 0, s, ftiles_.p, first, Gt_.p, ell_.p, b0, b1, bpart_.p, freds_.p,
                            fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, ext_off);
     } else {
@@ -1611,22 +1473,11 @@ void DirectSolver::launch_ftiles(int w, int count, int first, const double* b0, 
     }
 }
 template <int NR>
-void DirectSolver::launch_fstrips(const Level& L, const double* b0, const double* b1, const Ctrl* ctrl, int gate_reject,
-                                  hipStream_t s) {
-#define SSEL(D) (L.ftw == 256 ? k_fwd_pstrip<NR, AA_FWD_CH, 256, D> : (L.ftw == 128 ? k_fwd_pstrip<NR, AA_FWD_CH, 128, D> : k_fwd_pstrip<NR, AA_FWD_CH, 64, D>))
-    auto kf = depth_f_ >= 4 ? SSEL(4) : (depth_f_ == 3 ? SSEL(3) : SSEL(2));
-#undef SSEL
-    hipLaunchKernelGGL(kf, dim3(L.fs_count), dim3(256), 0, s, ftiles_.p, fstrips_.p, fsids_.p, L.fs_first, Gt_.p, ell_.p, b0, b1,
-                       bpart_.p, freds_.p, fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, 0);
-}
-
-template <int NR>
 void DirectSolver::launch_btiles(int w, int count, int first, double* x0, double* x1, int ext_off, const Ctrl* ctrl,
                                  int gate_reject, hipStream_t s) {
     if (packed_) {
-#define BSEL(D) (w == 256 ? k_bwd_ptile<NR, AA_BWD_CH, 256, D> : (w == 128 ? k_bwd_ptile<NR, AA_BWD_CH, 128, D> : k_bwd_ptile<NR, AA_BWD_CH, 64, D>))
-        auto kb = depth_b_ >= 4 ? BSEL(4) : (depth_b_ == 3 ? BSEL(3) : BSEL(2));
-#undef BSEL
+        auto kb = w == 256 ? k_bwd_ptile<NR, AA_BWD_CH, 256, AA_TILE_DEPTH>
+                           : (w == 128 ? k_bwd_ptile<NR, AA_BWD_CH, 128, AA_TILE_DEPTH> : k_bwd_ptile<NR, AA_BWD_CH, 64, AA_TILE_DEPTH>);
         hipLaunchKernelGGL(kb, dim3(count), dim3(256), 0, s, btiles_.p, first, Gt_.p, bnd_.p, Y_.p, x0, x1, bpart_.p,
                            breds_.p, bcnt_.p, ctrl, gate_reject, ext_off);
     } else {
@@ -1656,8 +1507,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
                                    ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
-        if (L.fs_count) launch_fstrips<NR>(L, b0, b1, ctrl, gate_reject, s);
-        else if (L.ft_count) launch_ftiles<NR>(L.ftw, L.ft_count, L.ft_first, b0, b1, 0, ctrl, gate_reject, s);
+        if (L.ft_count) launch_ftiles<NR>(L.ftw, L.ft_count, L.ft_first, b0, b1, 0, ctrl, gate_reject, s);
     }
     // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
     // and in the update vectors); their sum over the GPUs is the full forward result. When the

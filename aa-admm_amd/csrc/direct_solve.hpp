@@ -93,7 +93,6 @@ private:
         int ft_first = 0, ft_count = 0, fr_first = 0, frd_count = 0;  // split-K forward tiles
         int fblock = 256, bblock = 256, lds_fwd = 0, lds_bwd = 0;
         int ftw = 256, btw = 256;   // split-K tile widths (forward columns / backward rows)
-        int fs_first = 0, fs_count = 0;   // forward strips (packed tiles, k_fwd_pstrip)
     };
     int n_ = 0, nn_ = 0, kernels_ = 0, top_beg_ = 0;
     Comm* comm_ = nullptr;
@@ -117,15 +116,7 @@ private:
     // backward [wave][row][column pair][2]; zero-padded to whole tiles
     DevBuf<double> Gt_;
     bool packed_ = true;
-    int depth_f_ = 2, depth_b_ = 2;   // chunks in flight per wave in the packed tiles
-    // forward strips: {first index into fsids_, tile count}; AA_STRIP = most tiles per strip
-    // (0 = no strips), AA_STRIP_MIN = strips a level keeps at least
-    DevBuf<int2> fstrips_;
-    DevBuf<int> fsids_;
-    int strip_max_ = 4, strip_min_ = 512;
-    template <int NR>
-    void launch_fstrips(const Level& L, const double* b0, const double* b1, const Ctrl* ctrl, int gate_reject,
-                        hipStream_t s);
+
     DevBuf<Task> tasks_;
     DevBuf<BTile> btiles_;
     DevBuf<BRed> breds_;

@@ -488,24 +488,11 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
         d.idx = dg.idx.p;
         d.prm = dg.prm.p;
         d.warm = nullptr;
-        d.order = nullptr;
         d.surf = SurfDev{nullptr, nullptr, 0, 0};
         if (hg.surf >= 0) {
             dg.warm.alloc(cnt);
             d.warm = dg.warm.p;
             d.surf = surfs_[hg.surf].dev();
-            if (sort_period_ > 0 && cnt >= 4096 && !plain_) {   // queries ordered by warm triangle
-                std::vector<int> iota(cnt);
-                for (int e = 0; e < cnt; ++e) iota[e] = e;
-                dg.order.upload(iota, s());
-                dg.skeys.alloc(cnt); dg.skeys2.alloc(cnt); dg.svals.alloc(cnt);
-                int bits = 1;
-                while ((1LL << bits) < (long long)surfs_[hg.surf].tris.size() + 2) ++bits;
-                dg.sort_bits = bits;
-                dg.stemp_bytes = warm_sort_bytes(cnt, bits);
-                dg.stemp.alloc(std::max<size_t>(dg.stemp_bytes, 1));
-                d.order = dg.order.p;
-            }
         }
         if (d.hard) { Zh_ += 3LL * C * cnt; red_blocks_ += geo_u_blocks(cnt); }
         if (!hg.hard) soft_cols += (long long)C * cnt;
@@ -707,20 +694,9 @@ void GeomSolver::enqueue_iteration_plain(int m) {
     ev_mark("aa");
 }
 
-// closest-point groups: re-order the constraints by their warm triangles (GeoGroupDev::order)
-void GeomSolver::enqueue_warm_sorts() {
-    for (auto& g : groups_)
-        if (g.d.order)
-            launch_warm_sort(g.d, g.skeys.p, g.skeys2.p, g.svals.p, g.order.p, g.stemp.p, g.stemp_bytes, g.sort_bits, s());
-}
-
-// one chunk of loop passes; the closest-point queries are re-sorted by warm triangle after the
-// chunk's first pass and then every sort_period_ passes (AA_SURF_SORT)
+// one chunk of loop passes
 void GeomSolver::enqueue_chunk(int chunk, int m) {
-    for (int i = 0; i < chunk; ++i) {
-        if (sort_period_ > 0 && i % sort_period_ == 1) enqueue_warm_sorts();
-        enqueue_iteration(m);
-    }
+    for (int i = 0; i < chunk; ++i) enqueue_iteration(m);
 }
 
 void GeomSolver::ev_mark(const char* name) {

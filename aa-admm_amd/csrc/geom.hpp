@@ -57,14 +57,7 @@ private:
         DevBuf<int> idx, warm;
         DevBuf<double> prm;
         GeoGroupDev d{};
-        // closest-point groups: processing order by warm triangle (launch_warm_sort)
-        DevBuf<int> order, skeys, skeys2, svals;
-        DevBuf<unsigned char> stemp;
-        size_t stemp_bytes = 0;
-        int sort_bits = 0;
     };
-    int sort_period_ = std::getenv("AA_SURF_SORT") ? std::atoi(std::getenv("AA_SURF_SORT")) : 16;   // 0 = never
-    void enqueue_warm_sorts();
     void enqueue_chunk(int chunk, int m);
     struct Surface {
         std::vector<BvhNode> nodes;

@@ -15,8 +15,6 @@
 #include "common.hpp"
 #include "geom_kernels.hpp"
 
-#include <hipcub/hipcub.hpp>
-
 namespace aa {
 
 namespace {
@@ -377,9 +375,8 @@ __global__ __launch_bounds__(kBlock) void k_geo_z(GeoGroupDev g, const double* _
                                                   const double* __restrict__ u, double* __restrict__ z,
                                                   double* __restrict__ y, const Ctrl* ctrl) {
     if (gated(ctrl)) return;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= g.count) return;
-    const int e = g.order ? g.order[i] : i;   // each constraint is independent: order only moves lanes
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= g.count) return;
     (void)geo_z_one<T, K, false>(g, e, x, u, z, y);
 }
 
@@ -738,30 +735,6 @@ void launch_geo_z(const GeoGroupDev& g, const double* x, const double* u, double
         GEO_DISPATCH(k_geo_z, g, x, u, z, y, ctrl)
     }
     AA_CHECK_LAUNCH();
-}
-
-__global__ void k_warm_keys(const int* __restrict__ warm, int n, int* __restrict__ keys, int* __restrict__ vals) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
-    keys[e] = warm[e] + 1;
-    vals[e] = e;
-}
-
-size_t warm_sort_bytes(int count, int key_bits) {
-    size_t b = 0;
-    AA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const int*)nullptr, (int*)nullptr, (const int*)nullptr,
-                                              (int*)nullptr, count, 0, key_bits, (hipStream_t)0));
-    return b;
-}
-
-void launch_warm_sort(const GeoGroupDev& g, int* keys, int* keys_out, int* vals, int* order, void* temp, size_t temp_bytes,
-                      int key_bits, hipStream_t s) {
-    if (g.count == 0 || !g.warm) return;
-    hipLaunchKernelGGL(k_warm_keys, dim3(blocks_for(g.count)), dim3(kBlock), 0, s, g.warm, g.count, keys, vals);
-    AA_CHECK_LAUNCH();
-    size_t b = temp_bytes;
-    AA_HIP(hipcub::DeviceRadixSort::SortPairs(temp, b, (const int*)keys, keys_out, (const int*)vals, order, g.count, 0,
-                                              key_bits, s));
 }
 
 void launch_geo_z_plain(const GeoGroupDev& g, const double* x, const double* u, double* z, double* y, const Ctrl* ctrl,

@@ -50,16 +50,7 @@ struct GeoGroupDev {
     const double* prm;    // [P][count]   EDGE length; ANGLE min, max; else unused
     int* warm;            // [count] last closest triangle (closest-point groups), may be null
     SurfDev surf;
-    const int* order;     // closest-point groups: processing order of the constraints (null = 0..count)
 };
-
-// Processing order of a closest-point group by its constraints' warm triangles (the triangles
-// are stored in BVH leaf order, so neighbouring lanes then traverse neighbouring leaves): a
-// stable radix sort of (warm + 1, e) pairs into `order` (cold -1 sorts first). Scratch from
-// warm_sort_bytes; keys/vals/keys_out: count ints each.
-size_t warm_sort_bytes(int count, int key_bits);
-void launch_warm_sort(const GeoGroupDev& g, int* keys, int* keys_out, int* vals, int* order, void* temp, size_t temp_bytes,
-                      int key_bits, hipStream_t s);
 
 // z-step of one group: Dx = T(x) (+u for hard), z = P(Dx) (x sqrt(w) for soft); writes z
 // (hard) and the rhs slot rows y[slot] = yscale * T^T (z - u)  (hard)  /  w T^T P(Dx)  (soft)
