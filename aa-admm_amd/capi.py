@@ -30,7 +30,7 @@ EXPORTS = [
     "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_create_solo", "aa_comm_destroy", "aa_comm_info",
     "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
     "aa_geom_create", "aa_geom_create_kind", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
-    "aa_geom_add_closeness", "aa_geom_setup", "aa_geom_solve", "aa_geom_set_stop", "aa_geom_get_solution", "aa_geom_get_history",
+    "aa_geom_add_closeness", "aa_geom_add_laplacians", "aa_geom_add_closenesses", "aa_geom_setup", "aa_geom_solve", "aa_geom_set_stop", "aa_geom_get_solution", "aa_geom_get_history",
     "aa_geom_runtime_info", "aa_geom_closest_points", "aa_geom_bench_iterations", "aa_geom_kernel_stats",
     "aa_test_prox", "aa_test_cod_solve", "aa_test_geom_project",
 ]
@@ -479,6 +479,23 @@ class GeomSolver:
         t = np.ascontiguousarray(target, np.float64)
         _chk(lib().aa_geom_add_closeness(self.h, C.c_int(idx), C.c_double(weight), _dp(t)))
 
+    def add_laplacians(self, row_ptr, idx, coefs, weights, relative=None, ref_points=None):
+        """n_rows add_laplacian calls in one (CSR rows; relative[r] != 0: add_relative_laplacian)."""
+        rp = np.ascontiguousarray(row_ptr, np.int32)
+        i = np.ascontiguousarray(idx, np.int32)
+        c = np.ascontiguousarray(coefs, np.float64)
+        w = np.ascontiguousarray(weights, np.float64)
+        rl = None if relative is None else np.ascontiguousarray(relative, np.int32)
+        r = None if ref_points is None else np.ascontiguousarray(ref_points, np.float64).reshape(-1)
+        _chk(lib().aa_geom_add_laplacians(self.h, C.c_int(len(rp) - 1), _ip(rp), _ip(i), _dp(c), _dp(w),
+                                          None if rl is None else _ip(rl), None if r is None else _dp(r)))
+
+    def add_closenesses(self, idx, weights, targets):
+        i = np.ascontiguousarray(idx, np.int32)
+        w = np.ascontiguousarray(weights, np.float64)
+        t = np.ascontiguousarray(targets, np.float64).reshape(-1)
+        _chk(lib().aa_geom_add_closenesses(self.h, C.c_int(len(i)), _ip(i), _dp(w), _dp(t)))
+
     def set_comm(self, comm):
         """Partition over comm's ranks at the first solve (every rank adds the same problem)."""
         self.comm = comm
@@ -549,14 +566,26 @@ def geom_from_scene(ctx: Context, sc, comm=None) -> GeomSolver:
         if grp.type in (AA_CON_POINT_TO_REF, AA_CON_REF_SURFACE):
             prm = np.array([[sids[int(p)]] for p in np.asarray(prm).reshape(grp.count, -1)[:, 0]], np.float64)
         g.add_constraints(grp.hard, grp.type, grp.idx, grp.weight, prm)
-    for i in range(len(sc.reg_kind)):
-        a, b = sc.reg_ptr[i], sc.reg_ptr[i + 1]
-        kind = int(sc.reg_kind[i])
-        if kind == 2:
-            g.add_closeness(int(sc.reg_idx[a]), float(sc.reg_weight[i]), sc.reg_target[i])
+    # regularisation rows in insertion order, one batched call per run of laplacian (kinds 0, 1)
+    # or closeness (kind 2) rows -- the same rows as one add_* call each
+    kind = np.asarray(sc.reg_kind, np.int32)
+    ptr = np.asarray(sc.reg_ptr, np.int64)
+    i = 0
+    while i < len(kind):
+        clo = kind[i] == 2
+        j = i + 1
+        while j < len(kind) and (kind[j] == 2) == clo:
+            j += 1
+        if clo:
+            g.add_closenesses(np.asarray(sc.reg_idx)[ptr[i:j]], np.asarray(sc.reg_weight)[i:j],
+                              np.asarray(sc.reg_target)[i:j])
         else:
-            g.add_laplacian(sc.reg_idx[a:b], sc.reg_coef[a:b], float(sc.reg_weight[i]),
-                            sc.ref_points if kind == 1 else None)
+            a, b = int(ptr[i]), int(ptr[j])
+            rel = kind[i:j] == 1
+            g.add_laplacians(ptr[i:j + 1] - a, np.asarray(sc.reg_idx)[a:b], np.asarray(sc.reg_coef)[a:b],
+                             np.asarray(sc.reg_weight)[i:j], rel.astype(np.int32) if rel.any() else None,
+                             sc.ref_points if rel.any() else None)
+        i = j
     g.setup(sc.n_points, sc.penalty)
     return g
 

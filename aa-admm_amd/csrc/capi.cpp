@@ -370,6 +370,29 @@ int aa_geom_add_closeness(aa_geom h, int idx, double weight, const double* targe
     return guarded([&] { NEED(h, "null handle"); h->s->add_closeness(idx, weight, target3); });
 }
 
+int aa_geom_add_laplacians(aa_geom h, int n_rows, const int* row_ptr, const int* idx, const double* coefs,
+                           const double* weights, const int* relative, const double* ref_points3) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        NEED(n_rows >= 0 && (n_rows == 0 || (row_ptr && idx && coefs && weights)), "bad laplacian rows");
+        for (int r = 0; r < n_rows; ++r) {
+            const int a = row_ptr[r], k = row_ptr[r + 1] - a;
+            NEED(k > 0, "empty laplacian row");
+            const bool rel = relative && relative[r];
+            NEED(!rel || ref_points3, "relative laplacian row without reference points");
+            h->s->add_laplacian(idx + a, coefs + a, k, weights[r], rel ? ref_points3 : nullptr);
+        }
+    });
+}
+
+int aa_geom_add_closenesses(aa_geom h, int n, const int* idx, const double* weights, const double* targets3) {
+    return guarded([&] {
+        NEED(h, "null handle");
+        NEED(n >= 0 && (n == 0 || (idx && weights && targets3)), "bad closeness rows");
+        for (int r = 0; r < n; ++r) h->s->add_closeness(idx[r], weights[r], targets3 + 3 * (size_t)r);
+    });
+}
+
 int aa_geom_setup(aa_geom h, int n_points, double penalty, int spd_solver_type) {
     return guarded([&] { NEED(h, "null handle"); h->s->setup(n_points, penalty, spd_solver_type); });
 }

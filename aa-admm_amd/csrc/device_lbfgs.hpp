@@ -181,6 +181,110 @@ struct HyperLbfgs {
     }
 };
 
+// HyperLbfgs with the y half of the history (and y.s) in LDS: a ring of M slots per lane, 10
+// doubles each (y, y.s), lane-interleaved (entry j of the lane at lds[j * stride], stride = the
+// block's lanes: a wave's 64 lanes read 64 consecutive doubles, conflict-free). The s half stays
+// a register shift register. That takes 120 of the ~400 registers per lane out of the VGPR/AGPR
+// file: the AGPR spill traffic (v_accvgpr_read/write around every use of the history, a VALU
+// instruction each) and the y half of the shift (54 moves per iteration) go away. Slot of pair q
+// (0 = newest) = (head - q) mod M; the same operands in the same order as HyperLbfgs, so the
+// results are bit-identical.
+struct HyperLbfgsLds {
+    static constexpr int M = 6, E = 10;
+    double s[M][9], g[9], drt[9];
+    double fx, fpast, step;
+    int k_it, head;
+    double* yl;   // this lane's ring: entry (slot, i) at yl[(slot * E + i) * stride]
+    int stride;
+
+    __device__ __forceinline__ void bind(double* lane_base, int lanes) { yl = lane_base; stride = lanes; }
+
+    __device__ __forceinline__ bool start(int mat, double mu, double lambda, double k, double vol, const double* v,
+                                          double* x) {
+        fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
+        const double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
+        fpast = fx;
+        k_it = 1;
+        head = M - 1;
+        if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return true;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) drt[i] = -g[i];
+        step = 1.0 / sqrt(d9(drt, drt));
+        return false;
+    }
+
+    __device__ __forceinline__ bool iterate(int mat, double mu, double lambda, double k, double vol, const double* v,
+                                            double* x, int* fail) {
+        double xp[9], gp[9], alpha[M];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { xp[i] = x[i]; gp[i] = g[i]; }
+        {
+            const double fx_init = fx, dg_test = 1e-4 * d9(g, drt);
+            for (int it = 0; it < 2000; ++it) {
+#pragma unroll
+                for (int i = 0; i < 9; ++i) x[i] = xp[i] + step * drt[i];
+                fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
+                if (!(fx > fx_init + step * dg_test)) break;
+                if (step < 1e-20 || step > 1e20) { *fail = 1; return true; }
+                step *= 0.5;
+            }
+        }
+        const double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
+        if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return true;
+        if (fabs(fpast - fx) < 1e-16) return true;
+        fpast = fx;
+        if (k_it >= 100) return true;
+#pragma unroll
+        for (int q = M - 1; q > 0; --q)
+#pragma unroll
+            for (int i = 0; i < 9; ++i) s[q][i] = s[q - 1][i];
+        head = head == M - 1 ? 0 : head + 1;
+        double* yh = yl + (size_t)head * E * stride;
+        double ys = 0, yy = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double si = x[i] - xp[i], yi = g[i] - gp[i];
+            s[0][i] = si; yh[i * stride] = yi;
+            ys += yi * si; yy += yi * yi;
+        }
+        yh[9 * stride] = ys;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) drt[i] = -g[i];
+        const int bound = k_it < M ? k_it : M;
+        int sl = head;
+#pragma unroll
+        for (int q = 0; q < M; ++q) {
+            if (q < bound) {
+                const double* yq = yl + (size_t)sl * E * stride;
+                alpha[q] = d9(s[q], drt) / yq[9 * stride];
+#pragma unroll
+                for (int t = 0; t < 9; ++t) drt[t] -= alpha[q] * yq[t * stride];
+            }
+            sl = sl == 0 ? M - 1 : sl - 1;
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) drt[t] *= ys / yy;
+        // sl is now (head - M) mod M = head: walk back up from the oldest pair
+        sl = head == M - 1 ? 0 : head + 1;
+#pragma unroll
+        for (int q = M - 1; q >= 0; --q) {
+            if (q < bound) {
+                const double* yq = yl + (size_t)sl * E * stride;
+                double yd = 0;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) yd += yq[t * stride] * drt[t];
+                const double beta = yd / yq[9 * stride];
+#pragma unroll
+                for (int t = 0; t < 9; ++t) drt[t] += (alpha[q] - beta) * s[q][t];
+            }
+            sl = sl == M - 1 ? 0 : sl + 1;
+        }
+        step = 1.0;
+        ++k_it;
+        return false;
+    }
+};
+
 // x: in = v (start point), out = prox. Returns iterations; sets *fail on a collapsed line search.
 __device__ __forceinline__ int hyper_prox(int mat, double mu, double lambda, double k, double vol, const double* v,
                                           double* x, int* fail) {

@@ -42,6 +42,27 @@ __device__ __forceinline__ bool arrive_last(int* cnt, int nt, int lane) {
     return (int)prev == nt - 1;
 }
 
+// Factor loads (NT = DirectSolver::nt_): a factor streamed past the Infinity Cache (both sweeps'
+// copies > kNtBytes: C3, C4, C5) is read with non-temporal loads -- each entry is read once per
+// sweep by exactly one workgroup (MI355X_MICROARCH.md, nt-weights): C4 two-set solve 753 -> 741 us,
+// C3 1 138 -> 1 207 it/s. A factor that stays resident (C2, ~120 MB working set) keeps plain
+// loads: nt there costs its MALL hits (6 774 -> 5 801 it/s).
+typedef double dbl2v __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ double ld_f(const double* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ double2 ld_f2(const double2* p) {
+    if constexpr (NT) {
+        const dbl2v v = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(p));
+        return make_double2(v.x, v.y);
+    } else {
+        return *p;
+    }
+}
+
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -97,7 +118,7 @@ __device__ __forceinline__ void front_row(const N& t, int q, const long long* __
 
 // forward sweep of one tree level: y_P = Linv f_P (rows r < p), u = f_B - M f_P (rows r >= p);
 // thread per row, f_P in LDS, column-major G (lanes read consecutive rows)
-template <int BLOCK, int NR>
+template <int BLOCK, int NR, bool NT>
 __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, int first, const double* __restrict__ Gc,
                                                const long long* __restrict__ ell, const double* __restrict__ B0,
                                                const double* __restrict__ B1, double* __restrict__ Y,
@@ -122,7 +143,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
     zero<NR>(a);
 #pragma unroll 8
     for (int c = 0; c < cmax; ++c) {
-        const double v = G[(size_t)c * R];
+        const double v = ld_f<NT>(G + (size_t)c * R);
 #pragma unroll
         for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
     }
@@ -154,7 +175,7 @@ __device__ __forceinline__ void bwd_row(const N& t, int r, const int* __restrict
 
 // backward sweep of one tree level: x_P = Linv^T y_P - M^T x_B (columns j of G); thread per
 // column, [y_P ; -x_B] in LDS, row-major G (lanes read consecutive columns)
-template <int BLOCK, int NR>
+template <int BLOCK, int NR, bool NT>
 __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, int first, const double* __restrict__ Gr,
                                                const int* __restrict__ bnd, const double* __restrict__ Y,
                                                double* __restrict__ X0, double* __restrict__ X1, const Ctrl* ctrl,
@@ -175,7 +196,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
     zero<NR>(a);
 #pragma unroll 8
     for (int r = j; r < R; ++r) {
-        const double g = G[(size_t)r * ld];
+        const double g = ld_f<NT>(G + (size_t)r * ld);
 #pragma unroll
         for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
     }
@@ -414,17 +435,59 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
 // x 16 B, two columns or two rows' entries per lane). The column-major / row-major copies put a
 // tile's 64 x 256 entries in 256 pieces of 512 B (or 1 KB) at strides of the supernode's height,
 // spread over several MB: a DRAM-page and TLB pattern a contiguous stream avoids.
-template <int NR, int CH, int kFwdTileCols, int DEPTH>
+// Streamed levels (DirectSolver::Stream): the workgroup's tile is the next ticket of the launch's
+// queue (level order), not blockIdx -- so every tile a workgroup waits for was taken earlier by a
+// workgroup that is running or done, whatever the dispatch order (no deadlock).
+__device__ __forceinline__ int stream_ticket(const int* __restrict__ order, int first, int* sync, int head) {
+    __shared__ int s_t;
+    if (threadIdx.x == 0)
+        s_t = order[first + (int)__hip_atomic_fetch_add((gu32*)(sync + head), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)];
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(s_t);
+}
+// wait until counter sync[dep] reaches need (one lane polls; write-through producers, so a relaxed
+// agent load sees the adds). No agent acquire follows (AA_STREAM_ACQ=1 builds it in): it exists to
+// drop stale copies of the published lines from this CU's L1, and there are none -- every line a
+// tile waits for (update vectors, Xs rows: each producer's rows on 128-B lines of their own) is
+// written once per launch and read by nobody before its producer has signalled, and a launch
+// starts with clean caches. The acquire cost ~1.7 us per workgroup (x4 at 4 workgroups per CU,
+// MI355X_MICROARCH.md price table) and waits for the wave's factor loads in flight.
+#ifndef AA_STREAM_ACQ
+#define AA_STREAM_ACQ 0
+#endif
+__device__ __forceinline__ void stream_wait(int* sync, int dep, int need, int w, int lane) {
+    if (need <= 0) return;
+    if (w == 0) {
+        if (lane == 0) {
+            const gu32* d = (const gu32*)(sync + dep);
+            while ((int)__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) __builtin_amdgcn_s_sleep(2);
+        }
+#if AA_STREAM_ACQ
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    }
+    __syncthreads();
+}
+// publish: the calling wave's write-through stores drained, then one counter add
+__device__ __forceinline__ void stream_signal(int* sync, int sig, int lane) {
+    if (sig < 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add((gu32*)(sync + sig), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NR, int CH, int kFwdTileCols, int DEPTH, bool STREAM, bool NT>
 __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __restrict__ tiles, int first,
                                                    const double* __restrict__ Gt, const long long* __restrict__ ell,
                                                    const double* __restrict__ B0, const double* __restrict__ B1,
                                                    double* __restrict__ part, const FRed* __restrict__ reds,
                                                    int* __restrict__ cnt, double* __restrict__ Y, double* __restrict__ U,
-                                                   const Ctrl* ctrl, int gate_reject, int ext_off) {
+                                                   const Ctrl* ctrl, int gate_reject, int ext_off,
+                                                   const int* __restrict__ order, int* sync, int head) {
     if (solve_gated(ctrl, gate_reject)) return;
     __shared__ double f[NR * kFwdTileCols];
     __shared__ double red[3][NR * 64];
-    const FTile t = tiles[first + blockIdx.x];
+    const FTile t = tiles[STREAM ? stream_ticket(order, first, sync, head) : first + blockIdx.x];
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     constexpr int per = kFwdTileCols / 4;   // columns of a wave's slice (even)
@@ -441,12 +504,13 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
     double2 gbuf[DP][C2];
     auto ld = [&](double2* g, int k) {
 #pragma unroll
-        for (int q = 0; q < C2; ++q) g[q] = G[(size_t)min(k * C2 + q, qmax) * 64];
+        for (int q = 0; q < C2; ++q) g[q] = ld_f2<NT>(G + (size_t)min(k * C2 + q, qmax) * 64);
     };
     if (live) {
 #pragma unroll
         for (int d = 0; d < DP; ++d) ld(gbuf[d], d);
     }
+    if constexpr (STREAM) stream_wait(sync, t.dep, t.need, w, lane);   // the children's update vectors
     for (int i = tid; i < kFwdTileCols; i += 256) {
         if (i < t.nc) front_row<NR>(t, t.c0 + i, ell, B0, B1, U, f + NR * i, ext_off);
         else zero<NR>(f + NR * i);
@@ -506,24 +570,55 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
         } else {
             double* u = U + (NR / 3) * rd.uoff + NR * (size_t)(rr - rd.p);
 #pragma unroll
-            for (int k = 0; k < NR; ++k) u[k] = fr[k] - b[k];
+            for (int k = 0; k < NR; ++k) {
+                if constexpr (STREAM) st_sc1(u + k, fr[k] - b[k]);   // read by the parent in this launch
+                else u[k] = fr[k] - b[k];
+            }
         }
     }
+    if constexpr (STREAM) stream_signal(sync, rd.sig, lane);
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int NR, int CH, int kBwdTileRows, int DEPTH>
+// [y_P ; -x_B]_r of a streamed supernode: x_B rows of supernodes solved in this launch come
+// from the padded copy Xs (bndx >= 0: its row; each supernode's rows on lines of their own, so no
+// line is read before every row on it is final), the others from x
+template <int NR, class N>
+__device__ __forceinline__ void bwd_row_s(const N& t, int r, const int* __restrict__ bnd, const int* __restrict__ bndx,
+                                          const double* __restrict__ Y, const double* __restrict__ X0,
+                                          const double* __restrict__ X1, const double* __restrict__ Xs, double* v) {
+    if (r < t.p) {
+        const double* y = Y + NR * (size_t)(t.beg + r);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) v[k] = y[k];
+        return;
+    }
+    const int xi = bndx[t.bnd_off + r - t.p];
+    if (xi >= 0) {
+        const double* xs = Xs + NR * (size_t)xi;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) v[k] = -xs[k];
+    } else {
+        ld_ext<NR>(X0, X1, (size_t)bnd[t.bnd_off + r - t.p], v);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) v[k] = -v[k];
+    }
+}
+
+template <int NR, int CH, int kBwdTileRows, int DEPTH, bool STREAM, bool NT>
 __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __restrict__ tiles, int first,
                                                    const double* __restrict__ Gt, const int* __restrict__ bnd,
                                                    const double* __restrict__ Y, double* __restrict__ X0,
                                                    double* __restrict__ X1, double* __restrict__ part,
                                                    const BRed* __restrict__ reds, int* __restrict__ cnt, const Ctrl* ctrl,
-                                                   int gate_reject, int ext_off) {
+                                                   int gate_reject, int ext_off, const int* __restrict__ order,
+                                                   int* sync, int head, const int* __restrict__ bndx,
+                                                   double* __restrict__ Xs) {
     if (solve_gated(ctrl, gate_reject)) return;
     constexpr int W = 2 * NR;
     __shared__ double v[NR * kBwdTileRows];
     __shared__ double red[3][W * 64];
-    const BTile t = tiles[first + blockIdx.x];
+    const BTile t = tiles[STREAM ? stream_ticket(order, first, sync, head) : first + blockIdx.x];
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     constexpr int per = kBwdTileRows / 4;
@@ -537,15 +632,20 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
     double2 gbuf[DP][C];
     auto ld = [&](double2* g, int k) {
 #pragma unroll
-        for (int q = 0; q < C; ++q) g[q] = G[(size_t)min(k * C + q, nloc - 1) * 64];
+        for (int q = 0; q < C; ++q) g[q] = ld_f2<NT>(G + (size_t)min(k * C + q, nloc - 1) * 64);
     };
     if (live) {
 #pragma unroll
         for (int d = 0; d < DP; ++d) ld(gbuf[d], d);
     }
+    if constexpr (STREAM) stream_wait(sync, t.dep, t.need, w, lane);   // the parent's x rows
     for (int i = tid; i < kBwdTileRows; i += 256) {
-        if (i < t.nr) bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
-        else zero<NR>(v + NR * i);
+        if (i < t.nr) {
+            if constexpr (STREAM) bwd_row_s<NR>(t, t.r0 + i, bnd, bndx, Y, X0, X1, Xs, v + NR * i);
+            else bwd_row<NR>(t, t.r0 + i, bnd, Y, X0, X1, v + NR * i);
+        } else {
+            zero<NR>(v + NR * i);
+        }
     }
     __syncthreads();
     double a[W];
@@ -596,7 +696,18 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
         const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane - ext_off);
         st_ext<NR>(X0, X1, xo, b);
         if (2 * lane + 1 < rd.nc) st_ext<NR>(X0, X1, xo + 1, b + NR);
+        if constexpr (STREAM) {
+            if (rd.sig >= 0) {   // the children of this supernode read these rows in this launch
+                double* xs = Xs + NR * (size_t)(rd.xso + rd.c0 + 2 * lane);
+#pragma unroll
+                for (int m = 0; m < NR; ++m) st_sc1(xs + m, b[m]);
+                if (2 * lane + 1 < rd.nc)
+#pragma unroll
+                    for (int m = 0; m < NR; ++m) st_sc1(xs + NR + m, b[NR + m]);
+            }
+        }
     }
+    if constexpr (STREAM) stream_signal(sync, rd.sig, lane);
     if (lane == 0) __hip_atomic_store((gu32*)(cnt + t.rid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -663,7 +774,7 @@ using SubLevel = DirectSolver::SubLevel;
 using SubTree = DirectSolver::SubTree;
 
 // forward sweep of a whole bottom subtree (one workgroup), its levels bottom-up
-template <int BLOCK, int NR>
+template <int BLOCK, int NR, bool NT>
 __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
                                                  const SubNode* __restrict__ nodes, const int* __restrict__ items,
                                                  const double* __restrict__ Gc, const long long* __restrict__ ell,
@@ -712,7 +823,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             zero<NR>(a);
 #pragma unroll 8
             for (int c = 0; c < cmax; ++c) {
-                const double v = G[(size_t)c * R];
+                const double v = ld_f<NT>(G + (size_t)c * R);
 #pragma unroll
                 for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
             }
@@ -746,7 +857,7 @@ __device__ __forceinline__ int sub_seg_off(int seg, int p) {   // partial slots 
     return o;
 }
 
-template <int BLOCK, int NR>
+template <int BLOCK, int NR, bool NT>
 __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ trees, const SubLevel* __restrict__ lvls,
                                                  const SubNode* __restrict__ nodes, const int* __restrict__ items,
                                                  const long long* __restrict__ items2,
@@ -793,7 +904,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             zero<NR>(a);
 #pragma unroll 8
             for (int r = max(j, seg * kSubSegRows); r < r1; ++r) {
-                const double g = G[(size_t)r * ld];
+                const double g = ld_f<NT>(G + (size_t)r * ld);
 #pragma unroll
                 for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
             }
@@ -878,6 +989,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         nnz_L_ += (size_t)ps * (ps + 1) / 2 + (size_t)ps * nbs;
         go += (long long)(ps + nbs) * (ps + (ps & 1));
         uo += 3LL * nbs;
+        uo = (uo + 15) / 16 * 16;   // every update vector on 128-B lines of its own (streamed levels)
         dense += 0.5 * ps * (ps + 1.0);
         offd += (double)ps * nbs;
         piv += ps;
@@ -1135,6 +1247,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     std::vector<FTile> ftiles;
     std::vector<FRed> freds;
     std::vector<int> fwid, bwid;   // tile widths (packing)
+    std::vector<int> ft_sn, fr_sn, bt_sn, br_sn;   // supernode of every tile / reduction (streams)
+    std::vector<int> lev_of(nn_, -1);              // level of every level-scheduled supernode
     long long poff = 0;
     auto mk = [&](int sn, int r0, int nr) {
         Task t{};
@@ -1218,9 +1332,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     poff += 3 * 64;
                     ftiles.push_back(ft);
                     fwid.push_back(ftw);
+                    ft_sn.push_back(sn);
                     ++rd.nt;
                 }
                 freds.push_back(rd);
+                fr_sn.push_back(sn);
             }
         }
         L.ft_count = (int)ftiles.size() - L.ft_first;
@@ -1253,9 +1369,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     poff += 6 * 64;
                     btiles.push_back(bt);
                     bwid.push_back(btw);
+                    bt_sn.push_back(sn);
                     ++rd.nt;
                 }
                 breds.push_back(rd);
+                br_sn.push_back(sn);
             }
         }
         L.bt_count = (int)btiles.size() - L.bt_first;
@@ -1263,6 +1381,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         max_lds = std::max(max_lds, std::max(L.lds_fwd, L.lds_bwd));
         kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.bt_count ? 1 : 0) + (L.ft_count ? 1 : 0);
         levels_.push_back(L);
+        for (int sn : l) lev_of[sn] = (int)levels_.size() - 1;
         if (stats) {
             double by = 0;
             int maxp = 0, maxnb = 0, nw = 0;
@@ -1313,9 +1432,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 poff += 3 * 64;
                 ftiles.push_back(ft);
                 fwid.push_back(top_ftw_);
+                ft_sn.push_back(sn);
                 ++rd.nt;
             }
             freds.push_back(rd);
+            fr_sn.push_back(sn);
         }
         top_ft_count_ = (int)ftiles.size() - top_ft_first_;
         // backward: the products of the own rows only (partial x_top, summed over the GPUs)
@@ -1334,9 +1455,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 poff += 6 * 64;
                 btiles.push_back(bt);
                 bwid.push_back(top_btw_);
+                bt_sn.push_back(sn);
                 ++rd.nt;
             }
             breds.push_back(rd);
+            br_sn.push_back(sn);
         }
         top_bt_count_ = (int)btiles.size() - top_bt_first_;
         kernels_ += 4;
@@ -1409,6 +1532,124 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     } else {
         packed_ = false;
     }
+    // ---- streamed tile levels (see Stream in direct_solve.hpp): maximal runs of >= 2 consecutive
+    // levels with packed split-K tiles only and one tile width. Forward: a tile of supernode s waits
+    // for every update-row reduction of its children in the same run; backward: for every
+    // reduction of its parent in the same run (the parent's rows and, through the parent's own
+    // wait, all its ancestors' rows in the run).
+    {
+        const char* st = std::getenv("AA_SOLVE_STREAM");
+        stream_ = packed_ && st && st[0] == '1';   // measured slower on C4: opt-in
+    }
+    fstreams_.clear();
+    bstreams_.clear();
+    std::vector<int> forder, border, bndx(bnd.size(), -1);
+    long long xs_rows = 0;
+    if (stream_) {
+        const int nL = (int)levels_.size();
+        auto runs = [&](bool fwd) {
+            std::vector<std::pair<int, int>> r;
+            for (int i = 0; i < nL;) {
+                auto ok = [&](int l) {
+                    const Level& L = levels_[l];
+                    return fwd ? (L.fwd_count == 0 && L.ft_count > 0) : (L.bwd_count == 0 && L.bt_count > 0);
+                };
+                auto wid = [&](int l) { return fwd ? levels_[l].ftw : levels_[l].btw; };
+                if (!ok(i)) { ++i; continue; }
+                int j = i + 1;
+                while (j < nL && ok(j) && wid(j) == wid(i)) ++j;
+                if (j - i >= 2) r.push_back({i, j});
+                i = j;
+            }
+            return r;
+        };
+        const auto fr = runs(true), br = runs(false);
+        n_heads_ = (int)(fr.size() + br.size());
+        const int CF = n_heads_, CB = n_heads_ + nn_;   // counter bases in sync_
+        std::vector<int> nfr_b(nn_, 0), nbr(nn_, 0);     // per supernode: update-row / all reductions
+        for (size_t i = 0; i < freds.size(); ++i)
+            if (freds[i].r0 + freds[i].nr > freds[i].p) ++nfr_b[fr_sn[i]];
+        for (size_t i = 0; i < breds.size(); ++i) ++nbr[br_sn[i]];
+        int head = 0;
+        for (const auto& run : fr) {
+            const int l0 = run.first, l1 = run.second;
+            auto in = [&](int sn) { return sn >= 0 && lev_of[sn] >= l0 && lev_of[sn] < l1; };
+            Stream S{l0, l1, (int)forder.size(), 0, head++};
+            for (int l = l0; l < l1; ++l)
+                for (int k = 0; k < levels_[l].ft_count; ++k) forder.push_back(levels_[l].ft_first + k);
+            S.count = (int)forder.size() - S.first;
+            for (int k = S.first; k < S.first + S.count; ++k) {
+                FTile& ft = ftiles[forder[k]];
+                const int sn = ft_sn[forder[k]];
+                int need = 0;
+                for (int c : kids[sn]) if (in(c)) need += nfr_b[c];
+                ft.dep = CF + sn;
+                ft.need = need;
+            }
+            for (size_t i = 0; i < freds.size(); ++i) {
+                const int sn = fr_sn[i];
+                if (!in(sn)) continue;
+                const int par = F.parent[sn];
+                freds[i].sig = (in(par) && freds[i].r0 + freds[i].nr > freds[i].p) ? CF + par : -1;
+            }
+            fstreams_.push_back(S);
+        }
+        std::vector<int> node_sn(n_, -1), xso(nn_, -1);
+        for (int sn = 0; sn < nn_; ++sn)
+            for (int i = F.beg[sn]; i < F.end[sn] && i < n_; ++i) node_sn[i] = sn;
+        for (auto it = br.rbegin(); it != br.rend(); ++it) {   // processing order: top runs first
+            const int l0 = it->first, l1 = it->second;
+            auto in = [&](int sn) { return sn >= 0 && lev_of[sn] >= l0 && lev_of[sn] < l1; };
+            Stream S{l0, l1, (int)border.size(), 0, head++};
+            for (int l = l1 - 1; l >= l0; --l)
+                for (int k = 0; k < levels_[l].bt_count; ++k) border.push_back(levels_[l].bt_first + k);
+            S.count = (int)border.size() - S.first;
+            std::vector<char> has_kid(nn_, 0);
+            for (int l = l0; l < l1; ++l)
+                for (int k = 0; k < levels_[l].bt_count; ++k) {
+                    const int sn = bt_sn[levels_[l].bt_first + k];
+                    if (in(F.parent[sn])) has_kid[F.parent[sn]] = 1;
+                }
+            for (int k = S.first; k < S.first + S.count; ++k) {
+                BTile& bt = btiles[border[k]];
+                const int sn = bt_sn[border[k]], par = F.parent[sn];
+                bt.dep = in(par) ? CB + par : -1;
+                bt.need = in(par) ? nbr[par] : 0;
+                if (has_kid[sn] && xso[sn] < 0) { xso[sn] = (int)xs_rows; xs_rows += (p[sn] + 15) / 16 * 16; }
+            }
+            for (size_t i = 0; i < breds.size(); ++i) {
+                const int sn = br_sn[i];
+                if (!in(sn)) continue;
+                breds[i].sig = has_kid[sn] ? CB + sn : -1;
+                breds[i].xso = xso[sn];
+            }
+            // boundary rows of this run's supernodes owned by supernodes of the run: read from Xs
+            for (int l = l0; l < l1; ++l)
+                for (int k = 0; k < levels_[l].bt_count; ++k) {
+                    const int sn = bt_sn[levels_[l].bt_first + k];
+                    for (int a = 0; a < nb[sn]; ++a) {
+                        const int node = F.bnd[sn][a], ow = node < n_ ? node_sn[node] : -1;
+                        if (ow >= 0 && in(ow) && xso[ow] >= 0) bndx[bnd_off[sn] + a] = xso[ow] + (node - beg[ow]);
+                    }
+                }
+            bstreams_.push_back(S);
+        }
+        if (stats)
+            for (auto& S : fstreams_)
+                std::fprintf(stderr, "[solve] streamed forward levels [%d, %d): %d tiles, one launch\n", S.l0, S.l1, S.count);
+        if (stats)
+            for (auto& S : bstreams_)
+                std::fprintf(stderr, "[solve] streamed backward levels [%d, %d): %d tiles, one launch\n", S.l0, S.l1, S.count);
+        if (fstreams_.empty() && bstreams_.empty()) stream_ = false;
+    }
+    if (stream_) {
+        forder_.upload(forder.empty() ? std::vector<int>{0} : forder, s);
+        border_.upload(border.empty() ? std::vector<int>{0} : border, s);
+        bndx_.upload(bndx.empty() ? std::vector<int>{-1} : bndx, s);
+        sync_.alloc((size_t)n_heads_ + 2 * (size_t)nn_);
+        sync_.zero(s);
+        Xs_.alloc(std::max<long long>(3 * KS * xs_rows, 3));
+    }
     tasks_.upload(tasks, s);
     btiles_.upload(btiles, s);
     ftiles_.upload(ftiles, s);
@@ -1421,21 +1662,33 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     U_.alloc(std::max<long long>(KS * uo, 3));
     // (LDS figures above are per 3 columns; a 6-column solve needs twice as much; + the staged nodes)
     if (std::max(sub_lds_bytes(KS, true), sub_lds_bytes(KS, false)) > 64 * 1024)
-        for (const void* k : {(const void*)k_fwd_sub<256, 3>, (const void*)k_fwd_sub<512, 3>, (const void*)k_fwd_sub<1024, 3>,
-                              (const void*)k_bwd_sub<256, 3>, (const void*)k_bwd_sub<512, 3>, (const void*)k_bwd_sub<1024, 3>,
-                              (const void*)k_fwd_sub<256, 6>, (const void*)k_fwd_sub<512, 6>, (const void*)k_fwd_sub<1024, 6>,
-                              (const void*)k_bwd_sub<256, 6>, (const void*)k_bwd_sub<512, 6>, (const void*)k_bwd_sub<1024, 6>})
+        for (const void* k : {(const void*)k_fwd_sub<256, 3, false>, (const void*)k_fwd_sub<512, 3, false>, (const void*)k_fwd_sub<1024, 3, false>,
+                              (const void*)k_bwd_sub<256, 3, false>, (const void*)k_bwd_sub<512, 3, false>, (const void*)k_bwd_sub<1024, 3, false>,
+                              (const void*)k_fwd_sub<256, 6, false>, (const void*)k_fwd_sub<512, 6, false>, (const void*)k_fwd_sub<1024, 6, false>,
+                              (const void*)k_bwd_sub<256, 6, false>, (const void*)k_bwd_sub<512, 6, false>, (const void*)k_bwd_sub<1024, 6, false>,
+                              (const void*)k_fwd_sub<256, 3, true>, (const void*)k_fwd_sub<512, 3, true>, (const void*)k_fwd_sub<1024, 3, true>,
+                              (const void*)k_bwd_sub<256, 3, true>, (const void*)k_bwd_sub<512, 3, true>, (const void*)k_bwd_sub<1024, 3, true>,
+                              (const void*)k_fwd_sub<256, 6, true>, (const void*)k_fwd_sub<512, 6, true>, (const void*)k_fwd_sub<1024, 6, true>,
+                              (const void*)k_bwd_sub<256, 6, true>, (const void*)k_bwd_sub<512, 6, true>, (const void*)k_bwd_sub<1024, 6, true>})
             AA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (KS * max_lds > 64 * 1024) {   // large fronts: opt in to more than the default 64 KiB of LDS
-        for (const void* k : {(const void*)k_fwd<64, 3>, (const void*)k_fwd<128, 3>, (const void*)k_fwd<256, 3>,
-                              (const void*)k_bwd<64, 3>, (const void*)k_bwd<128, 3>, (const void*)k_bwd<256, 3>,
-                              (const void*)k_fwd<64, 6>, (const void*)k_fwd<128, 6>, (const void*)k_fwd<256, 6>,
-                              (const void*)k_bwd<64, 6>, (const void*)k_bwd<128, 6>, (const void*)k_bwd<256, 6>})
+        for (const void* k : {(const void*)k_fwd<64, 3, false>, (const void*)k_fwd<128, 3, false>, (const void*)k_fwd<256, 3, false>,
+                              (const void*)k_bwd<64, 3, false>, (const void*)k_bwd<128, 3, false>, (const void*)k_bwd<256, 3, false>,
+                              (const void*)k_fwd<64, 6, false>, (const void*)k_fwd<128, 6, false>, (const void*)k_fwd<256, 6, false>,
+                              (const void*)k_bwd<64, 6, false>, (const void*)k_bwd<128, 6, false>, (const void*)k_bwd<256, 6, false>,
+                              (const void*)k_fwd<64, 3, true>, (const void*)k_fwd<128, 3, true>, (const void*)k_fwd<256, 3, true>,
+                              (const void*)k_bwd<64, 3, true>, (const void*)k_bwd<128, 3, true>, (const void*)k_bwd<256, 3, true>,
+                              (const void*)k_fwd<64, 6, true>, (const void*)k_fwd<128, 6, true>, (const void*)k_fwd<256, 6, true>,
+                              (const void*)k_bwd<64, 6, true>, (const void*)k_bwd<128, 6, true>, (const void*)k_bwd<256, 6, true>})
             AA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
     // algorithmic bytes of one solve: the factor once per sweep (dense triangles + boundary
     // blocks, fp64), b/y/x (24 B per node each way) and the update vectors (write + read)
     bytes_ = 2.0 * 8.0 * (dense + offd) + 4.0 * 24.0 * piv + 3.0 * 24.0 * bsum;
+    {   // non-temporal factor loads when a solve's factor stream cannot stay in the Infinity Cache
+        const char* e = std::getenv("AA_FACTOR_NT");
+        nt_ = e ? e[0] == '1' : 2.0 * 8.0 * (dense + offd) > kNtBytes;
+    }
     bytes2_ = 2.0 * 8.0 * (dense + offd) + 2.0 * (4.0 * 24.0 * piv + 3.0 * 24.0 * bsum);
     AA_HIP(hipStreamSynchronize(s));
 }
@@ -1462,10 +1715,11 @@ template <int NR>
 void DirectSolver::launch_ftiles(int w, int count, int first, const double* b0, const double* b1, int ext_off,
                                  const Ctrl* ctrl, int gate_reject, hipStream_t s) {
     if (packed_) {
-        auto kf = w == 256 ? k_fwd_ptile<NR, AA_FWD_CH, 256, AA_TILE_DEPTH>
-                           : (w == 128 ? k_fwd_ptile<NR, AA_FWD_CH, 128, AA_TILE_DEPTH> : k_fwd_ptile<NR, AA_FWD_CH, 64, AA_TILE_DEPTH>);
+        auto kf = w == 256 ? (nt_ ? k_fwd_ptile<NR, AA_FWD_CH, 256, AA_TILE_DEPTH, false, true> : k_fwd_ptile<NR, AA_FWD_CH, 256, AA_TILE_DEPTH, false, false>)
+                  : w == 128 ? (nt_ ? k_fwd_ptile<NR, AA_FWD_CH, 128, AA_TILE_DEPTH, false, true> : k_fwd_ptile<NR, AA_FWD_CH, 128, AA_TILE_DEPTH, false, false>)
+                             : (nt_ ? k_fwd_ptile<NR, AA_FWD_CH, 64, AA_TILE_DEPTH, false, true> : k_fwd_ptile<NR, AA_FWD_CH, 64, AA_TILE_DEPTH, false, false>);
         hipLaunchKernelGGL(kf, dim3(count), dim3(256), 0, s, ftiles_.p, first, Gt_.p, ell_.p, b0, b1, bpart_.p, freds_.p,
-                           fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, ext_off);
+                           fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, ext_off, nullptr, nullptr, 0);
     } else {
         auto kf = w == 256 ? k_fwd_tile<NR, AA_FWD_CH, 256> : (w == 128 ? k_fwd_tile<NR, AA_FWD_CH, 128> : k_fwd_tile<NR, AA_FWD_CH, 64>);
         hipLaunchKernelGGL(kf, dim3(count), dim3(256), 0, s, ftiles_.p, first, Gc_.p, ell_.p, b0, b1, bpart_.p, freds_.p,
@@ -1476,15 +1730,38 @@ template <int NR>
 void DirectSolver::launch_btiles(int w, int count, int first, double* x0, double* x1, int ext_off, const Ctrl* ctrl,
                                  int gate_reject, hipStream_t s) {
     if (packed_) {
-        auto kb = w == 256 ? k_bwd_ptile<NR, AA_BWD_CH, 256, AA_TILE_DEPTH>
-                           : (w == 128 ? k_bwd_ptile<NR, AA_BWD_CH, 128, AA_TILE_DEPTH> : k_bwd_ptile<NR, AA_BWD_CH, 64, AA_TILE_DEPTH>);
+        auto kb = w == 256 ? (nt_ ? k_bwd_ptile<NR, AA_BWD_CH, 256, AA_TILE_DEPTH, false, true> : k_bwd_ptile<NR, AA_BWD_CH, 256, AA_TILE_DEPTH, false, false>)
+                  : w == 128 ? (nt_ ? k_bwd_ptile<NR, AA_BWD_CH, 128, AA_TILE_DEPTH, false, true> : k_bwd_ptile<NR, AA_BWD_CH, 128, AA_TILE_DEPTH, false, false>)
+                             : (nt_ ? k_bwd_ptile<NR, AA_BWD_CH, 64, AA_TILE_DEPTH, false, true> : k_bwd_ptile<NR, AA_BWD_CH, 64, AA_TILE_DEPTH, false, false>);
         hipLaunchKernelGGL(kb, dim3(count), dim3(256), 0, s, btiles_.p, first, Gt_.p, bnd_.p, Y_.p, x0, x1, bpart_.p,
-                           breds_.p, bcnt_.p, ctrl, gate_reject, ext_off);
+                           breds_.p, bcnt_.p, ctrl, gate_reject, ext_off, nullptr, nullptr, 0, nullptr, nullptr);
     } else {
         auto kb = w == 256 ? k_bwd_tile<NR, AA_BWD_CH, 256> : (w == 128 ? k_bwd_tile<NR, AA_BWD_CH, 128> : k_bwd_tile<NR, AA_BWD_CH, 64>);
         hipLaunchKernelGGL(kb, dim3(count), dim3(256), 0, s, btiles_.p, first, Gr_.p, bnd_.p, Y_.p, x0, x1, bpart_.p,
                            breds_.p, bcnt_.p, ctrl, gate_reject, ext_off);
     }
+}
+
+// one launch of a streamed run of levels (packed tiles, one width)
+template <int NR>
+void DirectSolver::launch_fstream(const Stream& S, const double* b0, const double* b1, const Ctrl* ctrl, int gate_reject,
+                                  hipStream_t s) {
+    const int w = levels_[S.l0].ftw;
+    auto kf = w == 256 ? (nt_ ? k_fwd_ptile<NR, AA_FWD_CH, 256, AA_TILE_DEPTH, true, true> : k_fwd_ptile<NR, AA_FWD_CH, 256, AA_TILE_DEPTH, true, false>)
+                  : w == 128 ? (nt_ ? k_fwd_ptile<NR, AA_FWD_CH, 128, AA_TILE_DEPTH, true, true> : k_fwd_ptile<NR, AA_FWD_CH, 128, AA_TILE_DEPTH, true, false>)
+                             : (nt_ ? k_fwd_ptile<NR, AA_FWD_CH, 64, AA_TILE_DEPTH, true, true> : k_fwd_ptile<NR, AA_FWD_CH, 64, AA_TILE_DEPTH, true, false>);
+    hipLaunchKernelGGL(kf, dim3(S.count), dim3(256), 0, s, ftiles_.p, S.first, Gt_.p, ell_.p, b0, b1, bpart_.p, freds_.p,
+                       fcnt_.p, Y_.p, U_.p, ctrl, gate_reject, 0, forder_.p, sync_.p, S.head);
+}
+template <int NR>
+void DirectSolver::launch_bstream(const Stream& S, double* x0, double* x1, const Ctrl* ctrl, int gate_reject,
+                                  hipStream_t s) {
+    const int w = levels_[S.l0].btw;
+    auto kb = w == 256 ? (nt_ ? k_bwd_ptile<NR, AA_BWD_CH, 256, AA_TILE_DEPTH, true, true> : k_bwd_ptile<NR, AA_BWD_CH, 256, AA_TILE_DEPTH, true, false>)
+                  : w == 128 ? (nt_ ? k_bwd_ptile<NR, AA_BWD_CH, 128, AA_TILE_DEPTH, true, true> : k_bwd_ptile<NR, AA_BWD_CH, 128, AA_TILE_DEPTH, true, false>)
+                             : (nt_ ? k_bwd_ptile<NR, AA_BWD_CH, 64, AA_TILE_DEPTH, true, true> : k_bwd_ptile<NR, AA_BWD_CH, 64, AA_TILE_DEPTH, true, false>);
+    hipLaunchKernelGGL(kb, dim3(S.count), dim3(256), 0, s, btiles_.p, S.first, Gt_.p, bnd_.p, Y_.p, x0, x1, bpart_.p,
+                       breds_.p, bcnt_.p, ctrl, gate_reject, 0, border_.p, sync_.p, S.head, bndx_.p, Xs_.p);
 }
 
 template <int NR>
@@ -1497,13 +1774,22 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     AA_HIP(hipStreamIsCapturing(s, &cst));
     const bool clk_on = sub_timing_ > 0 && cst == hipStreamCaptureStatusNone && n_sub_ > 0;
     const int noff_f = (K * sub_lds_f_ + 15) / 16 * 16, noff_b = (K * sub_lds_b_ + 15) / 16 * 16;
-#define SUBF(BL) hipLaunchKernelGGL((k_fwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, true), s, sub_trees_.p, \
+    // queue heads and dependency counters of the streamed runs start from zero every solve
+    if (stream_) AA_HIP(hipMemsetAsync(sync_.p, 0, sizeof(int) * ((size_t)n_heads_ + 2 * (size_t)nn_), s));
+#define SUBF(BL) hipLaunchKernelGGL((nt_ ? k_fwd_sub<BL, NR, true> : k_fwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, true), s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject, \
                                     clk_on ? sub_clk_.p : nullptr, 64, noff_f)
     if (n_sub_) switch (sub_block_) { case 1024: SUBF(1024); break; case 512: SUBF(512); break; default: SUBF(256); break; }
 #undef SUBF
-    for (auto& L : levels_) {
-#define FWD(BL) hipLaunchKernelGGL((k_fwd<BL, NR>), dim3(L.fwd_count), dim3(BL), K * L.lds_fwd, s, T, L.fwd_first, Gc_.p, \
+    size_t fs = 0;
+    for (int li = 0; li < (int)levels_.size(); ++li) {
+        const Level& L = levels_[li];
+        if (fs < fstreams_.size() && fstreams_[fs].l0 == li) {
+            launch_fstream<NR>(fstreams_[fs], b0, b1, ctrl, gate_reject, s);
+            li = fstreams_[fs++].l1 - 1;
+            continue;
+        }
+#define FWD(BL) hipLaunchKernelGGL((nt_ ? k_fwd<BL, NR, true> : k_fwd<BL, NR, false>), dim3(L.fwd_count), dim3(BL), K * L.lds_fwd, s, T, L.fwd_first, Gc_.p, \
                                    ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
@@ -1537,15 +1823,21 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     } else if (comm_ && top_beg_ < n_) {
         comm_->allreduce_sum(Y_.p + NR * (size_t)top_beg_, Y_.p + NR * (size_t)top_beg_, NR * (size_t)(n_ - top_beg_), s);
     }
-    for (auto it = levels_.rbegin(); it != levels_.rend(); ++it) {
-        const Level& L = *it;
-#define BWD(BL) hipLaunchKernelGGL((k_bwd<BL, NR>), dim3(L.bwd_count), dim3(BL), K * L.lds_bwd, s, T, L.bwd_first, Gr_.p, \
+    size_t bs = 0;
+    for (int li = (int)levels_.size() - 1; li >= 0; --li) {
+        const Level& L = levels_[li];
+        if (bs < bstreams_.size() && bstreams_[bs].l1 - 1 == li) {
+            launch_bstream<NR>(bstreams_[bs], x0, x1, ctrl, gate_reject, s);
+            li = bstreams_[bs++].l0;
+            continue;
+        }
+#define BWD(BL) hipLaunchKernelGGL((nt_ ? k_bwd<BL, NR, true> : k_bwd<BL, NR, false>), dim3(L.bwd_count), dim3(BL), K * L.lds_bwd, s, T, L.bwd_first, Gr_.p, \
                                    bnd_.p, Y_.p, x0, x1, ctrl, gate_reject)
         if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
         if (L.bt_count) launch_btiles<NR>(L.btw, L.bt_count, L.bt_first, x0, x1, 0, ctrl, gate_reject, s);
     }
-#define SUBB(BL) hipLaunchKernelGGL((k_bwd_sub<BL, NR>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, false), s, sub_trees_.p, \
+#define SUBB(BL) hipLaunchKernelGGL((nt_ ? k_bwd_sub<BL, NR, true> : k_bwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, false), s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, \
                                     ctrl, gate_reject, clk_on ? sub_clk_.p + 64 * (size_t)n_sub_ : nullptr, 64, noff_b)
     if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }

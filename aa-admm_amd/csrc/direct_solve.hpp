@@ -79,12 +79,17 @@ public:
     // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
     // toff: the tile's block in the packed tile stream Gt_ (see build: every tile's factor entries
     // stored contiguously in the order its waves consume them)
-    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid, ldr, pad; long long goff, poff, toff, pad2; };
-    struct BRed { int beg, c0, nc, nt; long long poff; };
+    // streamed levels (see stream_*): dep = the counter a tile waits on (its parent's, -1 = none)
+    // until it reaches need; a reduction adds 1 to counter sig (its own supernode's) when done;
+    // xso = the supernode's first row in the padded in-launch copy Xs_ of x
+    struct BTile { int beg, p, nb, bnd_off, c0, r0, nr, rid, ldr, dep; long long goff, poff, toff; int need, pad; };
+    struct BRed { int beg, c0, nc, nt; long long poff; int sig, xso; };
     // split-K forward of large supernodes: tile (64 rows from r0, nc columns from c0) and the
     // per-row-block reduction of its nt partials
-    struct FTile { int beg, p, R, c0, r0, nc, rid, ell_w; long long goff, ell_off, poff, toff; };
-    struct FRed { int beg, p, r0, nr, nt, ell_w; long long uoff, ell_off, poff; };
+    // streamed levels: dep / need as for BTile (dep = the tile's own supernode: its children's
+    // update vectors), sig = the parent's counter a reduction writing update rows adds to
+    struct FTile { int beg, p, R, c0, r0, nc, rid, ell_w; long long goff, ell_off, poff, toff; int dep, need, pad0, pad1; };
+    struct FRed { int beg, p, r0, nr, nt, ell_w; long long uoff, ell_off, poff; int sig, pad; };
 
 private:
     struct Level {
@@ -105,6 +110,12 @@ private:
     template <int NR>
     void launch_btiles(int w, int count, int first, double* x0, double* x1, int ext_off, const Ctrl* ctrl,
                        int gate_reject, hipStream_t s);
+    struct Stream;
+    template <int NR>
+    void launch_fstream(const Stream& S, const double* b0, const double* b1, const Ctrl* ctrl, int gate_reject,
+                        hipStream_t s);
+    template <int NR>
+    void launch_bstream(const Stream& S, double* x0, double* x1, const Ctrl* ctrl, int gate_reject, hipStream_t s);
     template <int NR>
     void solve_nr(const double* b0, double* x0, const double* b1, double* x1, const Ctrl* ctrl, int gate_reject,
                   hipStream_t s);
@@ -116,6 +127,10 @@ private:
     // backward [wave][row][column pair][2]; zero-padded to whole tiles
     DevBuf<double> Gt_;
     bool packed_ = true;
+    // non-temporal factor loads (AA_FACTOR_NT=0/1 forces): on when both sweeps' factor bytes
+    // exceed kNtBytes, i.e. the factor streams past the 256 MB Infinity Cache every solve
+    static constexpr double kNtBytes = 192e6;
+    bool nt_ = true;
 
     DevBuf<Task> tasks_;
     DevBuf<BTile> btiles_;
@@ -125,6 +140,21 @@ private:
     DevBuf<int> fcnt_, bcnt_;   // tiles finished per reduction task (reset by the last tile)
     DevBuf<double> bpart_;
     std::vector<Level> levels_;
+    // Streamed tile levels (AA_SOLVE_STREAM=1; measured slower than one launch per level on C4): a run of consecutive levels that have
+    // split-K tiles only is ONE launch. Its workgroups take tiles in level order from a queue
+    // (ticket = atomic add), issue their factor loads, and only then wait for the tile's inputs:
+    // the children's update vectors (forward) or the parent's x rows (backward), published
+    // in-launch by the reductions (write-through stores, drained, then a counter add; the waiting
+    // workgroup polls, takes one agent acquire, then reads -- MI355X_MICROARCH.md "Valid
+    // forms"). A level's factor stream thus overlaps the previous level's tail and reductions
+    // instead of waiting for its kernel boundary. Same tiles, partials and sums: bit-identical.
+    struct Stream { int l0, l1, first, count, head; };   // levels [l0, l1), queue order_[first, +count)
+    std::vector<Stream> fstreams_, bstreams_;
+    bool stream_ = false;
+    DevBuf<int> forder_, border_, bndx_;   // tile queues; per boundary entry its Xs_ row (-1: read x)
+    DevBuf<int> sync_;   // [queue heads | forward counters (nn_) | backward counters (nn_)], zeroed per solve
+    int n_heads_ = 0;
+    DevBuf<double> Xs_;   // backward: x rows of streamed supernodes, each supernode 128-B aligned
     // partitioned with a dense shared top (nested_dissection merge_top): the top root supernode
     // top_sn_ is solved outside the levels -- its front assembled locally and summed over the
     // GPUs, then each GPU runs the forward rows [top_r0_, top_r1_) and the backward products of

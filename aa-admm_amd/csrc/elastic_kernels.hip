@@ -7,6 +7,7 @@
 // comb < eps break) on the device so the whole ADMM loop is enqueued without host syncs.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 #include "device_lbfgs.hpp"
@@ -188,7 +189,9 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
 // the optional rhs slots written) takes the next one from a queue (one atomic per wave and
 // refill, ballot-aggregated) and lanes advance one outer L-BFGS iteration per trip. Each
 // element's arithmetic is unchanged, so the results are bit-identical to k_local_z.
-template <int NV>
+// LH: the L-BFGS history's y half in LDS (dev::HyperLbfgsLds, dynamic LDS kLqLdsBytes), else all
+// of it in registers (dev::HyperLbfgs); bit-identical
+template <int NV, bool LH>
 __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double* __restrict__ xfull,
                                                        const double* __restrict__ u, double* __restrict__ z,
                                                        double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
@@ -203,7 +206,11 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     }
     constexpr int D = 3 * (NV - 1);
     const int lane = threadIdx.x & 63;
-    dev::HyperLbfgs L;
+    typename std::conditional<LH, dev::HyperLbfgsLds, dev::HyperLbfgs>::type L;
+    if constexpr (LH) {
+        extern __shared__ double lq_hist[];
+        L.bind(lq_hist + threadIdx.x, kBlock);
+    }
     double v[D], x[D];
     double vol = 0;
     int e = -1, fail = 0;
@@ -282,8 +289,8 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     if (fail && ctrl) ctrl->fail = 1;
 }
 
-// k_local_z_hq with a one-element lookahead per lane (the default; AA_LQ_AHEAD=0 keeps
-// k_local_z_hq). A refill of the plain queue is a chain of three dependent round trips -- the
+// k_local_z_hq with a one-element lookahead per lane (AA_LQ_AHEAD=1; measured 6 % slower than
+// k_local_z_hq on C4). A refill of the plain queue is a chain of three dependent round trips -- the
 // returning queue atomic, the element's node ids, then the node positions -- paid while the wave's
 // other lanes wait (28 % of the kernel's cycles at one wave per SIMD). Here each
 // lane holds its NEXT element: the claim atomic is issued at a refill and read on the next trip,
@@ -292,7 +299,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
 // ids and loads positions only for pinned nodes (the only ones Cp needs). Close to the end of the
 // queue (fewer than `margin` elements left) lookahead stops, so claimed-ahead elements cannot
 // pile up on a few waves. Same arithmetic per element: bit-identical to k_local_z_hq.
-template <int NV>
+template <int NV, bool LH>
 __global__ __launch_bounds__(kBlock) void k_local_z_hqa(GroupDev g, const double* __restrict__ xfull,
                                                         const double* __restrict__ u, double* __restrict__ z,
                                                         double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
@@ -308,7 +315,11 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hqa(GroupDev g, const double
     constexpr int D = 3 * (NV - 1), NC = NV - 1;
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
-    dev::HyperLbfgs L;
+    typename std::conditional<LH, dev::HyperLbfgsLds, dev::HyperLbfgs>::type L;
+    if constexpr (LH) {
+        extern __shared__ double lq_hist[];
+        L.bind(lq_hist + threadIdx.x, kBlock);
+    }
     double v[D], x[D];
     double vol = 0;
     int e = -1, fail = 0;
@@ -721,6 +732,30 @@ __global__ __launch_bounds__(256) void k_stream_read(const double2* __restrict__
         for (int k = 0; k < 8; ++k) acc += v[k].x + v[k].y;
     }
     for (; i < n; i += stride) acc += src[i].x + src[i].y;
+    out[blockIdx.x * (long long)blockDim.x + threadIdx.x] = acc;
+}
+
+// the same read with a contiguous chunk per workgroup (a wave reads 1 KB per instruction, 8 in
+// flight per lane, consecutive instructions on consecutive KB), plain or non-temporal loads
+typedef double dbl2v_ __attribute__((ext_vector_type(2)));
+template <bool NT>
+__global__ __launch_bounds__(256) void k_stream_read_chunk(const double2* __restrict__ src, long long n,
+                                                           double* __restrict__ out) {
+    const long long per = (n + gridDim.x - 1) / gridDim.x;
+    const long long b0 = blockIdx.x * per, b1 = min(n, b0 + per);
+    double acc = 0;
+    long long i = b0 + threadIdx.x;
+    for (; i + 7 * 256 < b1; i += 8 * 256) {
+        dbl2v_ v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const dbl2v_* q = reinterpret_cast<const dbl2v_*>(src + i + k * 256);
+            v[k] = NT ? __builtin_nontemporal_load(q) : *q;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += v[k].x + v[k].y;
+    }
+    for (; i < b1; i += 256) acc += src[i].x + src[i].y;
     out[blockIdx.x * (long long)blockDim.x + threadIdx.x] = acc;
 }
 
@@ -1219,11 +1254,17 @@ LocalQueue make_local_queue(int device, int* counter) {
     q.counter = counter;
     int cus = 0, per = 0;
     AA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_local_z_hq<4>, kBlock, 0));
-    q.resident = std::max(1, cus * std::max(1, per));
     const char* r = std::getenv("AA_LQ_REFILL");
     const char* ah = std::getenv("AA_LQ_AHEAD");
-    q.ahead = !(ah && ah[0] == '0');
+    const char* lh = std::getenv("AA_LQ_LDS");
+    q.ahead = ah && ah[0] == '1';   // opt-in: measured slower on C4
+    q.lds = lh && lh[0] == '1';     // opt-in: no faster on C4
+    const void* kq = q.lds ? (q.ahead ? (const void*)k_local_z_hqa<4, true> : (const void*)k_local_z_hq<4, true>)
+                           : (q.ahead ? (const void*)k_local_z_hqa<4, false> : (const void*)k_local_z_hq<4, false>);
+    const size_t lds = q.lds ? kLqLdsBytes : 0;
+    if (q.lds) AA_HIP(hipFuncSetAttribute(kq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kq, kBlock, lds));
+    q.resident = std::max(1, cus * std::max(1, per));
     q.refill = r ? std::atoi(r) : 60;
     // lookahead stops once fewer elements than this are left (AA_LQ_MARGIN: in resident lanes)
     const char* mg = std::getenv("AA_LQ_MARGIN");
@@ -1238,12 +1279,19 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
     if (g.kind == 0 && g.mat != 0 && !red && queue && queue->counter) {   // hyperelastic, no partials: work queue
         AA_HIP(hipMemsetAsync(queue->counter, 0, sizeof(int), s));
         const int resident = std::max(1, queue->resident), refill = queue->refill;
-        if (queue->ahead)
-            hipLaunchKernelGGL(k_local_z_hqa<4>, dim3(std::min(nb, resident)), dim3(kBlock), 0, s, g, xfull, u, z, y, nf,
-                               mode, ctrl, queue->counter, refill, queue->margin, queue->stats);
+        const dim3 grid(std::min(nb, resident));
+        if (queue->lds && queue->ahead)
+            hipLaunchKernelGGL((k_local_z_hqa<4, true>), grid, dim3(kBlock), kLqLdsBytes, s, g, xfull, u, z, y, nf, mode,
+                               ctrl, queue->counter, refill, queue->margin, queue->stats);
+        else if (queue->lds)
+            hipLaunchKernelGGL((k_local_z_hq<4, true>), grid, dim3(kBlock), kLqLdsBytes, s, g, xfull, u, z, y, nf, mode,
+                               ctrl, queue->counter, refill, queue->stats);
+        else if (queue->ahead)
+            hipLaunchKernelGGL((k_local_z_hqa<4, false>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode, ctrl,
+                               queue->counter, refill, queue->margin, queue->stats);
         else
-            hipLaunchKernelGGL(k_local_z_hq<4>, dim3(std::min(nb, resident)), dim3(kBlock), 0, s, g, xfull, u, z, y, nf,
-                               mode, ctrl, queue->counter, refill, queue->stats);
+            hipLaunchKernelGGL((k_local_z_hq<4, false>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode, ctrl,
+                               queue->counter, refill, queue->stats);
         AA_CHECK_LAUNCH();
         return;
     }
@@ -1459,16 +1507,27 @@ double bench_stream_read(long long bytes, int reps, hipStream_t s) {
     hipEvent_t e0, e1;
     AA_HIP(hipEventCreate(&e0));
     AA_HIP(hipEventCreate(&e1));
-    hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, s, a.p, n, out.p);   // warm-up
-    AA_HIP(hipEventRecord(e0, s));
-    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, s, a.p, n, out.p);
-    AA_HIP(hipEventRecord(e1, s));
-    AA_HIP(hipEventSynchronize(e1));
-    float ms = 0;
-    AA_HIP(hipEventElapsedTime(&ms, e0, e1));
+    // three forms (grid-stride; contiguous chunk per workgroup, plain and non-temporal loads): the
+    // ceiling reported is the fastest
+    double best = 0;
+    for (int form = 0; form < 3; ++form) {
+        auto run = [&] {
+            if (form == 0) hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, s, a.p, n, out.p);
+            else if (form == 1) hipLaunchKernelGGL(k_stream_read_chunk<false>, dim3(grid), dim3(256), 0, s, a.p, n, out.p);
+            else hipLaunchKernelGGL(k_stream_read_chunk<true>, dim3(grid), dim3(256), 0, s, a.p, n, out.p);
+        };
+        run();   // warm-up
+        AA_HIP(hipEventRecord(e0, s));
+        for (int r = 0; r < reps; ++r) run();
+        AA_HIP(hipEventRecord(e1, s));
+        AA_HIP(hipEventSynchronize(e1));
+        float ms = 0;
+        AA_HIP(hipEventElapsedTime(&ms, e0, e1));
+        best = std::max(best, 16.0 * (double)n * reps / (ms * 1e-3) / 1e9);   // GB/s read
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    return 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;   // GB/s read
+    return best;
 }
 
 }  // namespace aa

@@ -75,12 +75,14 @@ enum LocalMode { LZ_NORMAL = 0, LZ_REDO = 1, LZ_INIT = 2 };
 struct LocalQueue {
     int* counter = nullptr;
     int resident = 0, refill = 60, margin = 0;
-    bool ahead = true;   // k_local_z_hqa (one-element lookahead per lane)
+    bool ahead = false;  // AA_LQ_AHEAD=1: k_local_z_hqa (one-element lookahead per lane)
+    bool lds = false;    // AA_LQ_LDS: the L-BFGS history's y half in LDS (dev::HyperLbfgsLds)
     // optional diagnostics (AA_LQ_STATS=1): [0..100] elements by L-BFGS iterations (0 = the start
     // point passed the gradient test), [101] trips, [102] refills, [103] waves; summed over launches
     unsigned long long* stats = nullptr;
 };
 constexpr int kLqStats = 104;
+constexpr size_t kLqLdsBytes = sizeof(double) * 6 * 10 * kBlock;   // HyperLbfgsLds ring, one block
 LocalQueue make_local_queue(int device, int* counter);
 // z = prox(P x + u/w); prim partials; optional y = w(w z + c - u). gate: !done (and reject for REDO)
 // queue given: hyperelastic groups without partials run as a persistent work queue

@@ -243,6 +243,15 @@ int aa_geom_add_constraints(aa_geom h, int hard, int type, const int* idx, int k
 int aa_geom_add_laplacian(aa_geom h, const int* idx, const double* coefs, int k, double weight,
                           const double* ref_points3);
 int aa_geom_add_closeness(aa_geom h, int idx, double weight, const double* target3);   /* add_closeness */
+/* Batched forms for bindings whose per-call overhead dominates (one call per point is ~10 us from
+ * Python): the same rows in the same order as n_rows aa_geom_add_laplacian calls (row r: indices
+ * idx[row_ptr[r] .. row_ptr[r+1]), coefficients coefs[same range], weight weights[r]; relative[r]
+ * != 0 -- relative may be NULL -- passes ref_points3 as add_relative_laplacian does), and as n
+ * aa_geom_add_closeness calls (targets3: n x 3). Reference: the per-point loops of
+ * Geometry/PlanarityOpt.cpp / WireMeshOpt.cpp over LinearRegularization.h:91-117. */
+int aa_geom_add_laplacians(aa_geom h, int n_rows, const int* row_ptr, const int* idx, const double* coefs,
+                           const double* weights, const int* relative, const double* ref_points3);
+int aa_geom_add_closenesses(aa_geom h, int n, const int* idx, const double* weights, const double* targets3);
 int aa_geom_setup(aa_geom h, int n_points, double penalty, int spd_solver_type);       /* setup_ADMM    */
 /* solve_ADMM(init_x (3 x n), rel_residual_eps, max_iter, Anderson_m): max_iter accepted
  * iterations; Anderson_m = 0 runs plain ADMM. */

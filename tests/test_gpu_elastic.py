@@ -201,6 +201,51 @@ def test_gpu_z_pipelined_comb_bit_identical(builder, pkg, ctx, monkeypatch):
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
 
 
+@pytest.mark.parametrize("knobs", [
+    {},
+    # narrow thresholds and tiles: most supernodes above the fused subtrees become split-K tiled,
+    # so the tree has long runs of tile-only levels (several streamed launches per sweep)
+    {"AA_SOLVE_WAVEP": "16", "AA_SOLVE_WAVER": "32", "AA_SOLVE_TILE": "64", "AA_SOLVE_MIN_SUBTREES": "4096"},
+])
+def test_gpu_streamed_levels_bit_identical(pkg, ctx, monkeypatch, capfd, knobs):
+    """Streamed tile levels (one launch per run of tile-only levels, tiles taken from a queue in
+    level order, each waiting in-launch for its children's update vectors / its parent's x rows)
+    give bit-identical trajectories to one launch per level (AA_SOLVE_STREAM=0): same tiles,
+    partials and sums in the same order; only the scheduling differs."""
+    sc = scenes.tet_drop(40, 16, 20, iters=12, n_steps=2)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("AA_SOLVE_STATS", "1")
+    monkeypatch.setenv("AA_SOLVE_STREAM", "0")
+    lev, _ = pkg.capi.run_scene(ctx, sc)
+    capfd.readouterr()
+    monkeypatch.setenv("AA_SOLVE_STREAM", "1")
+    st, _ = pkg.capi.run_scene(ctx, sc)
+    err = capfd.readouterr().err
+    if knobs:
+        assert "streamed forward levels" in err and "streamed backward levels" in err, err[-2000:]
+    for a, b in zip(lev, st):
+        for k in ("prim", "comb", "reject", "x", "v"):
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
+
+
+@pytest.mark.parametrize("ahead", ["0", "1"])
+def test_gpu_local_queue_lds_history_bit_identical(pkg, ctx, monkeypatch, ahead):
+    """The NeoHookean local step with the L-BFGS history's y half in LDS (dev::HyperLbfgsLds, a
+    ring per lane) against the all-register history (AA_LQ_LDS=0), with and without the lookahead
+    queue: the same operations in the same order (TetEnergyTerm.cpp:151-162 via mcloptlib
+    LBFGS.hpp:205-305), so bit-identical trajectories."""
+    sc = scenes.tet_drop(12, 4, 6, iters=30, n_steps=2)
+    monkeypatch.setenv("AA_LQ_AHEAD", ahead)
+    monkeypatch.setenv("AA_LQ_LDS", "0")
+    reg, _ = pkg.capi.run_scene(ctx, sc)
+    monkeypatch.setenv("AA_LQ_LDS", "1")
+    lds, _ = pkg.capi.run_scene(ctx, sc)
+    for a, b in zip(reg, lds):
+        for k in ("prim", "comb", "reject", "x", "v"):
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+
+
 def test_gpu_element_tables(pkg, ctx):
     """The device prox functions and the Anderson COD solve on the reference's own element
     tables (elements.npz, made by oracle/_ref/ref_element from TetEnergyTerm.cpp:74-96,151-162,
