@@ -555,17 +555,27 @@ class GeomSolver:
         return dict(avg_ms=a.value, bytes=b.value, launches=n.value)
 
 
-def geom_from_scene(ctx: Context, sc, comm=None) -> GeomSolver:
-    """Binds a geom_scenes.GeomScene the way optimize_mesh (PlanarityOpt.cpp / WireMeshOpt.cpp) does."""
+def geom_from_scene(ctx: Context, sc, comm=None, timings=None) -> GeomSolver:
+    """Binds a geom_scenes.GeomScene the way optimize_mesh (PlanarityOpt.cpp / WireMeshOpt.cpp) does.
+    timings (dict, optional) receives the wall ms of each binding phase."""
+    import time
+    t = [time.perf_counter()]
+
+    def lap(name):
+        t.append(time.perf_counter())
+        if timings is not None:
+            timings[name] = round((t[-1] - t[-2]) * 1e3, 1)
     g = GeomSolver(ctx, AA_GEOM_PLAIN if getattr(sc, "solver", "alm") == "plain" else AA_GEOM_ALM)
+    lap("create_ms")
     if comm is not None:
         g.set_comm(comm)
     sids = [g.add_ref_surface(V, F) for V, F in sc.surfaces]
     for grp in sc.groups:
         prm = grp.params
-        if grp.type in (AA_CON_POINT_TO_REF, AA_CON_REF_SURFACE):
-            prm = np.array([[sids[int(p)]] for p in np.asarray(prm).reshape(grp.count, -1)[:, 0]], np.float64)
+        if grp.type in (AA_CON_POINT_TO_REF, AA_CON_REF_SURFACE):   # scene surface ids -> solver ids
+            prm = np.asarray(sids, np.float64)[np.asarray(prm).reshape(grp.count, -1)[:, 0].astype(np.int64)][:, None]
         g.add_constraints(grp.hard, grp.type, grp.idx, grp.weight, prm)
+    lap("surfaces_constraints_ms")
     # regularisation rows in insertion order, one batched call per run of laplacian (kinds 0, 1)
     # or closeness (kind 2) rows -- the same rows as one add_* call each
     kind = np.asarray(sc.reg_kind, np.int32)
@@ -586,7 +596,9 @@ def geom_from_scene(ctx: Context, sc, comm=None) -> GeomSolver:
                              np.asarray(sc.reg_weight)[i:j], rel.astype(np.int32) if rel.any() else None,
                              sc.ref_points if rel.any() else None)
         i = j
+    lap("regularization_ms")
     g.setup(sc.n_points, sc.penalty)
+    lap("setup_admm_ms")
     return g
 
 

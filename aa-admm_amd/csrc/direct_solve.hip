@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <memory>
 #include <string>
 
@@ -60,6 +61,50 @@ __device__ __forceinline__ double2 ld_f2(const double2* p) {
         return make_double2(v.x, v.y);
     } else {
         return *p;
+    }
+}
+
+// Thread-per-row / thread-per-column factor products:
+// a[k] += sum_{i0 <= i < i1} G[i * stride] * V[NR * i + k], i ascending (one fused multiply-add
+// chain per k, the order of a plain loop). dot_rows: `#pragma unroll 8` -- a remainder loop of up to
+// 7 serial load -> use steps follows the unrolled bodies. dot_rows_chunk: chunks of CH whose loads
+// are issued together (indices clamped to i1 - 1, the extra terms adding 0), so a row costs
+// ceil(n / CH) round trips and no serial remainder. Measured per call site (A/B builds, phase
+// clocks): the fused subtrees' one-set forward rows -12 us per sweep with chunks of 8 (C3 solve
+// 240 -> 236 us); the two-set (6 RHS) forward rows, the fused backward segments and the row-task
+// kernels are slower chunked (C4 two-set solve 738 -> 763 us with the fused forward chunked,
+// 734 -> 769 with every loop chunked), so they keep the unrolled loop.
+template <int NR, bool NT>
+__device__ __forceinline__ void dot_rows(const double* __restrict__ G, size_t stride, int i0, int i1,
+                                         const double* __restrict__ V, double* a) {
+#pragma unroll 8
+    for (int i = i0; i < i1; ++i) {
+        const double g = ld_f<NT>(G + (size_t)i * stride);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) a[k] += g * V[NR * i + k];
+    }
+}
+#ifndef AA_ROW_CHUNK
+#define AA_ROW_CHUNK 8
+#endif
+template <int NR, bool NT, int CH = AA_ROW_CHUNK>
+__device__ __forceinline__ void dot_rows_chunk(const double* __restrict__ G, size_t stride, int i0, int i1,
+                                               const double* __restrict__ V, double* a) {
+    for (int c0 = i0; c0 < i1; c0 += CH) {
+        double g[CH];
+#pragma unroll
+        for (int q = 0; q < CH; ++q) g[q] = ld_f<NT>(G + (size_t)min(c0 + q, i1 - 1) * stride);
+        __builtin_amdgcn_sched_barrier(0);   // every load of the chunk issued before the first use
+        // no branch per term (the compiler would sink a skipped term's load into it, after the
+        // other terms' wait): a term past i1 adds 0 * V[i1 - 1] (finite), which leaves a unchanged
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+            const bool in = c0 + q < i1;
+            const double gq = in ? g[q] : 0.0;
+            const int iv = in ? c0 + q : i1 - 1;
+#pragma unroll
+            for (int k = 0; k < NR; ++k) a[k] += gq * V[NR * iv + k];
+        }
     }
 }
 
@@ -141,12 +186,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
     if (r >= p) front_row<NR>(t, r, ell, B0, B1, U, fr);
     double a[NR];
     zero<NR>(a);
-#pragma unroll 8
-    for (int c = 0; c < cmax; ++c) {
-        const double v = ld_f<NT>(G + (size_t)c * R);
-#pragma unroll
-        for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
-    }
+    dot_rows<NR, NT>(G, (size_t)R, 0, cmax, f, a);
     if (r < p) {
         double* y = Y + NR * (size_t)(t.beg + r);
 #pragma unroll
@@ -194,12 +234,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd(const Task* __restrict__ tasks, i
     const int ld = t.ldr;
     double a[NR];
     zero<NR>(a);
-#pragma unroll 8
-    for (int r = j; r < R; ++r) {
-        const double g = ld_f<NT>(G + (size_t)r * ld);
-#pragma unroll
-        for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
-    }
+    dot_rows<NR, NT>(G, (size_t)ld, j, R, v, a);
     st_ext<NR>(X0, X1, (size_t)(t.beg + j), a);
 }
 
@@ -821,12 +856,8 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             if (r >= p) front_row<NR>(nd, r, ell, B0, B1, U, fr);
             double a[NR];
             zero<NR>(a);
-#pragma unroll 8
-            for (int c = 0; c < cmax; ++c) {
-                const double v = ld_f<NT>(G + (size_t)c * R);
-#pragma unroll
-                for (int k = 0; k < NR; ++k) a[k] += v * f[NR * c + k];
-            }
+            if constexpr (NR == 3) dot_rows_chunk<NR, NT>(G, (size_t)R, 0, cmax, f, a);
+            else dot_rows<NR, NT>(G, (size_t)R, 0, cmax, f, a);
             if (r < p) {
                 double* y = Y + NR * (size_t)(nd.beg + r);
 #pragma unroll
@@ -902,12 +933,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             const int r1 = min(R, (seg + 1) * kSubSegRows);
             double a[NR];
             zero<NR>(a);
-#pragma unroll 8
-            for (int r = max(j, seg * kSubSegRows); r < r1; ++r) {
-                const double g = ld_f<NT>(G + (size_t)r * ld);
-#pragma unroll
-                for (int k = 0; k < NR; ++k) a[k] += g * v[NR * r + k];
-            }
+            dot_rows<NR, NT>(G, (size_t)ld, max(j, seg * kSubSegRows), r1, v, a);
             double* q = lds + K * nd.slot + NR * (sub_seg_off(seg, p) + j);
 #pragma unroll
             for (int k = 0; k < NR; ++k) q[k] = a[k];
@@ -1865,7 +1891,24 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
             for (int b = 0; b < n_sub_; ++b)
                 if (tr[b].nlvl == nl) tot.push_back(0.01 * (double)(h[(base + b) * 64 + nph] - h[(base + b) * 64]));
             std::sort(tot.begin(), tot.end());
-            std::fprintf(stderr, " | total %.1f/%.1f us\n", tot[tot.size() / 2], tot.back());
+            std::fprintf(stderr, " | total %.1f/%.1f us", tot[tot.size() / 2], tot.back());
+            // every workgroup (any level count): start and end against the earliest start
+            const int per = nph / nl;
+            long long t0 = h[(size_t)base * 64];
+            for (int b = 0; b < n_sub_; ++b) t0 = std::min(t0, h[(size_t)(base + b) * 64]);
+            std::vector<double> st, en;
+            std::map<int, int> by_lvl;
+            for (int b = 0; b < n_sub_; ++b) {
+                st.push_back(0.01 * (double)(h[(size_t)(base + b) * 64] - t0));
+                en.push_back(0.01 * (double)(h[(size_t)(base + b) * 64 + per * tr[b].nlvl] - t0));
+                ++by_lvl[tr[b].nlvl];
+            }
+            std::sort(st.begin(), st.end());
+            std::sort(en.begin(), en.end());
+            std::fprintf(stderr, " | start med/max %.1f/%.1f end med/max %.1f/%.1f us | subtrees by levels:", st[st.size() / 2],
+                         st.back(), en[en.size() / 2], en.back());
+            for (auto& kv : by_lvl) std::fprintf(stderr, " %d:%d", kv.first, kv.second);
+            std::fprintf(stderr, "\n");
         };
         show("fwd (assembly, rows per level, bottom-up)", 0, 2 * nl);
         show("bwd (vector, segments, columns per level, top-down)", n_sub_, 3 * nl);

@@ -624,6 +624,9 @@ __global__ __launch_bounds__(kBlock) void k_rhs(int nf, const int* __restrict__ 
 // wave sum x, y, z of node 21 w + j along its run (lane 63 idles), so a wave's loads cover 21
 // runs in 24-B pieces instead of 64 runs in 8-B pieces; each component is still summed in slot
 // order (the same sums as k_rhs, bit for bit)
+#ifndef AA_RHS_CHUNK
+#define AA_RHS_CHUNK 1
+#endif
 __global__ __launch_bounds__(kBlock) void k_rhs_slots(int nf, const int* __restrict__ ptr, const double* __restrict__ y,
                                                       const double* __restrict__ Mxbar, double pdt2,
                                                       double* __restrict__ b, Ctrl* ctrl, int gate_reject,
@@ -647,10 +650,23 @@ __global__ __launch_bounds__(kBlock) void k_rhs_slots(int nf, const int* __restr
     const size_t o = 3 * (size_t)i + c;
     if (xlast) xlast[o] = xsrc[o];   // last_x = curr_x (Solver.cpp:170)
     double sum = 0;
-    const int k1 = ptr[i + 1];
-    const double* q = y + 3 * (size_t)ptr[i] + c;
+    const int k0 = ptr[i], k1 = ptr[i + 1];
+    const double* q = y + 3 * (size_t)k0 + c;
+#if AA_RHS_CHUNK
+    // the node's slots in chunks of 8 loads issued together (clamped to the last slot, the extra
+    // terms adding 0): ceil(n / 8) round trips, no serial remainder; the same sum order
+    for (int k = 0; k < k1 - k0; k += 8) {
+        double g[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) g[m] = q[3 * (size_t)min(k + m, k1 - k0 - 1)];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) sum += k + m < k1 - k0 ? g[m] : 0.0;
+    }
+#else
 #pragma unroll 4
-    for (int k = ptr[i]; k < k1; ++k, q += 3) sum += *q;
+    for (int k = k0; k < k1; ++k, q += 3) sum += *q;
+#endif
     b[o] = Mxbar[o] + pdt2 * sum;
 }
 

@@ -562,6 +562,9 @@ __global__ __launch_bounds__(kBlock) void k_geo_u_plane_dyn(GeoGroupDev g, const
 // one lane per point COMPONENT: lanes 3j, 3j+1, 3j+2 of a wave sum x, y, z of point 21 w + j
 // (lane 63 idles), so one load instruction reads 21 slot rows whole instead of 64 rows a third
 // each; every component is summed in slot order, as with a lane per point (bit for bit)
+#ifndef AA_RHS_CHUNK
+#define AA_RHS_CHUNK 1
+#endif
 __global__ __launch_bounds__(kBlock) void k_geo_rhs(int n, const int* __restrict__ ptr, const int* __restrict__ slots,
                                                     const double* __restrict__ y, const double* __restrict__ rf,
                                                     double* __restrict__ b, const Ctrl* ctrl) {
@@ -574,8 +577,26 @@ __global__ __launch_bounds__(kBlock) void k_geo_rhs(int n, const int* __restrict
     if (i >= n) return;
     const size_t o = 3 * (size_t)i + c;
     double sum = rf[o];
-    const int k1 = ptr[i + 1];
-    for (int k = ptr[i]; k < k1; ++k) sum += y[3 * (size_t)slots[k] + c];
+    const int k0 = ptr[i], k1 = ptr[i + 1];
+#if AA_RHS_CHUNK
+    // chunks of 8 slots: the 8 slot ids, then the 8 rows, each group issued together (ids clamped
+    // to the last slot, the extra terms adding 0) -- two round trips per chunk instead of two per
+    // slot; the same sum order
+    for (int k = k0; k < k1; k += 8) {
+        int id[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) id[m] = slots[min(k + m, k1 - 1)];
+        __builtin_amdgcn_sched_barrier(0);
+        double g[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) g[m] = y[3 * (size_t)id[m] + c];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) sum += k + m < k1 ? g[m] : 0.0;
+    }
+#else
+    for (int k = k0; k < k1; ++k) sum += y[3 * (size_t)slots[k] + c];
+#endif
     b[o] = sum;
 }
 

@@ -283,7 +283,8 @@ def geom_line(args, world, rank, local, dist):
     sc, desc = geom_scene(args)
     comm, part = make_comm(pkg, ctx, args, world, rank)
     t0 = time.time()
-    g = capi.geom_from_scene(ctx, sc, comm)   # add_*_constraint + setup_ADMM (rows, weights)
+    bind_phases = {}
+    g = capi.geom_from_scene(ctx, sc, comm, bind_phases)   # add_*_constraint + setup_ADMM (rows, weights)
     bind_ms = (time.time() - t0) * 1e3
     eps = 2.0 * (1e-8 * sc.avg_edge_length() * sc.hard_cols()) ** 2   # ALMGeometrySolver.h:173 (commented stop)
     t1 = time.time()
@@ -298,7 +299,8 @@ def geom_line(args, world, rank, local, dist):
     # ordering, factorization and uploads done at the first solve; the first solve's loop (graph
     # capture, Anderson buffers) and the warm-up solves are reported beside it, not in it
     setup_ms = bind_ms + rt0.factor_ms
-    setup_breakdown = {"bind_and_setup_admm_ms": round(bind_ms, 1), "setup_admm_cpp_ms": round(rt0.setup_ms, 1),
+    setup_breakdown = {"bind_and_setup_admm_ms": round(bind_ms, 1), "bind_phases_ms": bind_phases,
+                       "setup_admm_cpp_ms": round(rt0.setup_ms, 1),
                        "order_factor_upload_ms": round(rt0.factor_ms, 1),
                        "first_solve_loop_ms": round(first_ms - rt0.factor_ms, 1),
                        "warmup_solves_ms": round(warm_ms, 1), "warmup_solves": max(1, args.warmup) - 1}
