@@ -108,6 +108,37 @@ __device__ __forceinline__ void dot_rows_chunk(const double* __restrict__ G, siz
     }
 }
 
+// chunked gathers without serial remainder loops (front rows, split-K reductions); 0 = the plain
+// loops (A/B)
+#ifndef AA_FRONT_CHUNK
+#define AA_FRONT_CHUNK 1
+#endif
+// a split-K block's partial sums: b[m] += q[k * STRIDE + m] over its nt tiles, in tile order, in
+// chunks of CH tiles whose loads are issued together (tile index clamped, the extra terms adding 0)
+// -- no serial remainder loop
+template <int W, int STRIDE, int CH = (W >= 12 ? 2 : (W >= 6 ? 4 : 8))>
+__device__ __forceinline__ void red_tiles(const double* __restrict__ q, int nt, double* b) {
+#if AA_FRONT_CHUNK
+    for (int k0 = 0; k0 < nt; k0 += CH) {
+        double t[CH][W];
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int m = 0; m < W; ++m) t[c][m] = q[(size_t)min(k0 + c, nt - 1) * STRIDE + m];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int m = 0; m < W; ++m) b[m] += k0 + c < nt ? t[c][m] : 0.0;
+    }
+#else
+#pragma unroll 4
+    for (int k = 0; k < nt; ++k, q += STRIDE)
+#pragma unroll
+        for (int m = 0; m < W; ++m) b[m] += q[m];
+#endif
+}
+
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -151,6 +182,32 @@ __device__ __forceinline__ void front_row(const N& t, int q, const long long* __
     zero<NR>(a);
     if (q < t.p) ld_ext<NR>(B0, B1, (size_t)(t.beg + q - ext_off), a);
     const long long* e = ell + t.ell_off + (size_t)q * t.ell_w;
+#if AA_FRONT_CHUNK
+    // the row's pull offsets, then its update entries, each group issued together (chunks of FC,
+    // offsets clamped to the row's last, absent ones reading U[0] and adding 0): two round trips
+    // per chunk instead of two per pull; the same sums in the same order
+    constexpr int FC = NR == 6 ? 2 : 4;   // 6 RHS: fewer rows in flight (registers beside the tile's factor chunks)
+    for (int k0 = 0; k0 < t.ell_w; k0 += FC) {
+        long long o[FC];
+#pragma unroll
+        for (int m = 0; m < FC; ++m) o[m] = e[min(k0 + m, t.ell_w - 1)];
+        __builtin_amdgcn_sched_barrier(0);
+        double u[FC][NR];
+#pragma unroll
+        for (int m = 0; m < FC; ++m) {
+            const bool in = k0 + m < t.ell_w && o[m] >= 0;
+            o[m] = in ? o[m] : -1;
+            const double* up = U + (NR / 3) * (in ? o[m] : 0);
+#pragma unroll
+            for (int j = 0; j < NR; ++j) u[m][j] = up[j];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < FC; ++m)
+#pragma unroll
+            for (int j = 0; j < NR; ++j) a[j] += o[m] >= 0 ? u[m][j] : 0.0;
+    }
+#else
     for (int k = 0; k < t.ell_w; ++k) {
         const long long o = e[k];
         if (o >= 0) {
@@ -159,6 +216,7 @@ __device__ __forceinline__ void front_row(const N& t, int q, const long long* __
             for (int j = 0; j < NR; ++j) a[j] += u[j];
         }
     }
+#endif
 }
 
 // forward sweep of one tree level: y_P = Linv f_P (rows r < p), u = f_B - M f_P (rows r >= p);
@@ -346,10 +404,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_tile(const BTile* __r
         double b[W];
         zero<W>(b);
         const double* q = part + (NR / 3) * rd.poff + W * lane;
-#pragma unroll 4
-        for (int k = 0; k < rd.nt; ++k, q += W * 64)
-#pragma unroll
-            for (int m = 0; m < W; ++m) b[m] += q[m];
+        red_tiles<W, W * 64>(q, rd.nt, b);
         const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane - ext_off);
         st_ext<NR>(X0, X1, xo, b);
         if (2 * lane + 1 < rd.nc) st_ext<NR>(X0, X1, xo + 1, b + NR);
@@ -446,10 +501,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
         double b[NR];
         zero<NR>(b);
         const double* q = part + (NR / 3) * rd.poff + NR * lane;
-#pragma unroll 8
-        for (int k = 0; k < rd.nt; ++k, q += NR * 64)
-#pragma unroll
-            for (int m = 0; m < NR; ++m) b[m] += q[m];
+        red_tiles<NR, NR * 64>(q, rd.nt, b);
         if (rr < rd.p) {
             double* y = Y + NR * (size_t)(rd.beg + rr);
 #pragma unroll
@@ -594,10 +646,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
         double b[NR];
         zero<NR>(b);
         const double* q = part + (NR / 3) * rd.poff + NR * lane;
-#pragma unroll 8
-        for (int k = 0; k < rd.nt; ++k, q += NR * 64)
-#pragma unroll
-            for (int m = 0; m < NR; ++m) b[m] += q[m];
+        red_tiles<NR, NR * 64>(q, rd.nt, b);
         if (rr < rd.p) {
             double* y = Y + NR * (size_t)(rd.beg + rr);
 #pragma unroll
@@ -724,10 +773,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
         double b[W];
         zero<W>(b);
         const double* q = part + (NR / 3) * rd.poff + W * lane;
-#pragma unroll 4
-        for (int k = 0; k < rd.nt; ++k, q += W * 64)
-#pragma unroll
-            for (int m = 0; m < W; ++m) b[m] += q[m];
+        red_tiles<W, W * 64>(q, rd.nt, b);
         const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane - ext_off);
         st_ext<NR>(X0, X1, xo, b);
         if (2 * lane + 1 < rd.nc) st_ext<NR>(X0, X1, xo + 1, b + NR);
