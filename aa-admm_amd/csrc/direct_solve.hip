@@ -175,7 +175,10 @@ __device__ __forceinline__ void zero(double* a) {
 // children's update entries landing on it (ELL pull list: ell_w offsets into U per row, -1 =
 // none; fixed order -> deterministic)
 // (ext_off: B0 / B1 hold rows from ext_off on -- the partitioned top's summed front)
-template <int NR, class N>
+// CHUNK (the default): the pulls in issued-together chunks, for gathers followed by a barrier (the
+// LDS front slices); false: the plain loop, for a boundary row's own front value gathered ahead of
+// its factor stream (chunked, its waits would come before the stream's first loads)
+template <int NR, bool CHUNK = true, class N>
 __device__ __forceinline__ void front_row(const N& t, int q, const long long* __restrict__ ell,
                                           const double* __restrict__ B0, const double* __restrict__ B1,
                                           const double* __restrict__ U, double* a, int ext_off = 0) {
@@ -183,6 +186,7 @@ __device__ __forceinline__ void front_row(const N& t, int q, const long long* __
     if (q < t.p) ld_ext<NR>(B0, B1, (size_t)(t.beg + q - ext_off), a);
     const long long* e = ell + t.ell_off + (size_t)q * t.ell_w;
 #if AA_FRONT_CHUNK
+    if constexpr (CHUNK) {
     // the row's pull offsets, then its update entries, each group issued together (chunks of FC,
     // offsets clamped to the row's last, absent ones reading U[0] and adding 0): two round trips
     // per chunk instead of two per pull; the same sums in the same order
@@ -207,7 +211,9 @@ __device__ __forceinline__ void front_row(const N& t, int q, const long long* __
 #pragma unroll
             for (int j = 0; j < NR; ++j) a[j] += o[m] >= 0 ? u[m][j] : 0.0;
     }
-#else
+    return;
+    }
+#endif
     for (int k = 0; k < t.ell_w; ++k) {
         const long long o = e[k];
         if (o >= 0) {
@@ -216,7 +222,6 @@ __device__ __forceinline__ void front_row(const N& t, int q, const long long* __
             for (int j = 0; j < NR; ++j) a[j] += u[j];
         }
     }
-#endif
 }
 
 // forward sweep of one tree level: y_P = Linv f_P (rows r < p), u = f_B - M f_P (rows r >= p);
@@ -241,7 +246,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd(const Task* __restrict__ tasks, i
     // a boundary row's own front value is gathered first: its two dependent loads overlap the
     // factor stream instead of following it
     double fr[NR];
-    if (r >= p) front_row<NR>(t, r, ell, B0, B1, U, fr);
+    if (r >= p) front_row<NR, false>(t, r, ell, B0, B1, U, fr);
     double a[NR];
     zero<NR>(a);
     dot_rows<NR, NT>(G, (size_t)R, 0, cmax, f, a);
@@ -497,7 +502,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_tile(const FTile* __r
     if (lane < rd.nr) {
         const int rr = rd.r0 + lane;
         double fr[NR];   // a boundary row's front value: gathered before the partials are summed
-        if (rr >= rd.p) front_row<NR>(rd, rr, ell, B0, B1, U, fr, ext_off);
+        if (rr >= rd.p) front_row<NR, false>(rd, rr, ell, B0, B1, U, fr, ext_off);
         double b[NR];
         zero<NR>(b);
         const double* q = part + (NR / 3) * rd.poff + NR * lane;
@@ -642,7 +647,7 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
     if (lane < rd.nr) {
         const int rr = rd.r0 + lane;
         double fr[NR];
-        if (rr >= rd.p) front_row<NR>(rd, rr, ell, B0, B1, U, fr, ext_off);
+        if (rr >= rd.p) front_row<NR, false>(rd, rr, ell, B0, B1, U, fr, ext_off);
         double b[NR];
         zero<NR>(b);
         const double* q = part + (NR / 3) * rd.poff + NR * lane;
@@ -899,7 +904,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             const double* G = Gc + nd.goff + r;
             const int cmax = r < p ? r + 1 : p;
             double fr[NR];   // a boundary row's own front value, gathered before the factor stream
-            if (r >= p) front_row<NR>(nd, r, ell, B0, B1, U, fr);
+            if (r >= p) front_row<NR, false>(nd, r, ell, B0, B1, U, fr);
             double a[NR];
             zero<NR>(a);
             if constexpr (NR == 3) dot_rows_chunk<NR, NT>(G, (size_t)R, 0, cmax, f, a);
@@ -1760,6 +1765,14 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     {   // non-temporal factor loads when a solve's factor stream cannot stay in the Infinity Cache
         const char* e = std::getenv("AA_FACTOR_NT");
         nt_ = e ? e[0] == '1' : 2.0 * 8.0 * (dense + offd) > kNtBytes;
+        // the thread-per-row kernels (fused subtrees, row tasks) separately (AA_FACTOR_NT_ROWS):
+        // their 8-B-per-lane loads cover partial lines that a neighbouring wave re-reads, which nt
+        // drops from L2 (PMC, C4: fused backward 1.41 -> 1.81x its factor bytes read). Measured
+        // (same-box A/B): nt on the rows costs C4 (2 GB both sweeps) 33 us and C5 (0.69 GB) 44 us
+        // per solve, and saves C3 (0.28 GB) 12 us -- on only where the factor is within ~2x the
+        // Infinity Cache
+        const char* er = std::getenv("AA_FACTOR_NT_ROWS");
+        nt_rows_ = er ? er[0] == '1' : (nt_ && 2.0 * 8.0 * (dense + offd) < kNtRowsMaxBytes);
     }
     bytes2_ = 2.0 * 8.0 * (dense + offd) + 2.0 * (4.0 * 24.0 * piv + 3.0 * 24.0 * bsum);
     AA_HIP(hipStreamSynchronize(s));
@@ -1848,7 +1861,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     const int noff_f = (K * sub_lds_f_ + 15) / 16 * 16, noff_b = (K * sub_lds_b_ + 15) / 16 * 16;
     // queue heads and dependency counters of the streamed runs start from zero every solve
     if (stream_) AA_HIP(hipMemsetAsync(sync_.p, 0, sizeof(int) * ((size_t)n_heads_ + 2 * (size_t)nn_), s));
-#define SUBF(BL) hipLaunchKernelGGL((nt_ ? k_fwd_sub<BL, NR, true> : k_fwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, true), s, sub_trees_.p, \
+#define SUBF(BL) hipLaunchKernelGGL((nt_rows_ ? k_fwd_sub<BL, NR, true> : k_fwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, true), s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject, \
                                     clk_on ? sub_clk_.p : nullptr, 64, noff_f)
     if (n_sub_) switch (sub_block_) { case 1024: SUBF(1024); break; case 512: SUBF(512); break; default: SUBF(256); break; }
@@ -1861,7 +1874,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
             li = fstreams_[fs++].l1 - 1;
             continue;
         }
-#define FWD(BL) hipLaunchKernelGGL((nt_ ? k_fwd<BL, NR, true> : k_fwd<BL, NR, false>), dim3(L.fwd_count), dim3(BL), K * L.lds_fwd, s, T, L.fwd_first, Gc_.p, \
+#define FWD(BL) hipLaunchKernelGGL((nt_rows_ ? k_fwd<BL, NR, true> : k_fwd<BL, NR, false>), dim3(L.fwd_count), dim3(BL), K * L.lds_fwd, s, T, L.fwd_first, Gc_.p, \
                                    ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
         if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
 #undef FWD
@@ -1903,13 +1916,13 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
             li = bstreams_[bs++].l0;
             continue;
         }
-#define BWD(BL) hipLaunchKernelGGL((nt_ ? k_bwd<BL, NR, true> : k_bwd<BL, NR, false>), dim3(L.bwd_count), dim3(BL), K * L.lds_bwd, s, T, L.bwd_first, Gr_.p, \
+#define BWD(BL) hipLaunchKernelGGL((nt_rows_ ? k_bwd<BL, NR, true> : k_bwd<BL, NR, false>), dim3(L.bwd_count), dim3(BL), K * L.lds_bwd, s, T, L.bwd_first, Gr_.p, \
                                    bnd_.p, Y_.p, x0, x1, ctrl, gate_reject)
         if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
 #undef BWD
         if (L.bt_count) launch_btiles<NR>(L.btw, L.bt_count, L.bt_first, x0, x1, 0, ctrl, gate_reject, s);
     }
-#define SUBB(BL) hipLaunchKernelGGL((nt_ ? k_bwd_sub<BL, NR, true> : k_bwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, false), s, sub_trees_.p, \
+#define SUBB(BL) hipLaunchKernelGGL((nt_rows_ ? k_bwd_sub<BL, NR, true> : k_bwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, false), s, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, \
                                     ctrl, gate_reject, clk_on ? sub_clk_.p + 64 * (size_t)n_sub_ : nullptr, 64, noff_b)
     if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }

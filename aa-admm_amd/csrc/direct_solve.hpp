@@ -18,6 +18,7 @@
 // sides (x, y, z coordinates) are processed together -- or six: solve2() runs two independent
 // solves in one pass over the factor (bit-identical to two solve() calls).
 #pragma once
+#include <cstdlib>
 #include <vector>
 
 #include "comm.hpp"
@@ -30,6 +31,11 @@ namespace aa {
 class DirectSolver {
 public:
     static constexpr int kTopRows = 2048;    // upper tree levels amalgamated into one dense root
+    // the amalgamation budget in pivots (AA_TOP_ROWS overrides kTopRows)
+    static int top_rows() {
+        const char* e = std::getenv("AA_TOP_ROWS");
+        return e ? std::atoi(e) : kTopRows;
+    }
     static constexpr int kPartTopRows = 4096;   // partitioned: a part's upper levels amalgamated (rows)
     static constexpr int kWaveP = 192;       // forward rows longer than this: wave per row
     static constexpr int kWaveR = 384;       // backward columns longer than this: wave per column
@@ -129,8 +135,8 @@ private:
     bool packed_ = true;
     // non-temporal factor loads (AA_FACTOR_NT=0/1 forces): on when both sweeps' factor bytes
     // exceed kNtBytes, i.e. the factor streams past the 256 MB Infinity Cache every solve
-    static constexpr double kNtBytes = 192e6;
-    bool nt_ = true;
+    static constexpr double kNtBytes = 192e6, kNtRowsMaxBytes = 512e6;
+    bool nt_ = true, nt_rows_ = true;
 
     DevBuf<Task> tasks_;
     DevBuf<BTile> btiles_;

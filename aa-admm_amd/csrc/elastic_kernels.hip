@@ -843,6 +843,18 @@ __global__ __launch_bounds__(kBlock) void k_finalize(int n, int nf, const double
 }
 
 // ------------------------------------------------------------------ Anderson acceleration
+// history columns (m x dim doubles: 0.9 GB on C4, streamed past the Infinity Cache every
+// iteration) are read with non-temporal loads (AA_AA_NT=0: plain, A/B)
+#ifndef AA_AA_NT
+#define AA_AA_NT 1
+#endif
+__device__ __forceinline__ double ld_h(const double* p) {
+#if AA_AA_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
 __device__ __forceinline__ double seg_get(const Seg2& s, long long i) { return i < s.na ? s.a[i] : s.b[i - s.na]; }
 __device__ __forceinline__ void seg_set(const Seg2& s, long long i, double v) { if (i < s.na) s.a[i] = v; else s.b[i - s.na] = v; }
 
@@ -885,13 +897,13 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
         // every load of the element first (cur, dF_j, the other history columns), then the
         // products: a load used right away serialises the loop on its latency
         const double ci = cur[i];
-        const double dfo = dF[(size_t)col * eff + i];
+        const double dfo = ld_h(dF + (size_t)col * eff + i);
         // (wide windows keep the loads in the product loop: MM doubles more would cost occupancy)
         constexpr bool kPre = MM <= 16;
         double dfc[kPre ? MM : 1];
         if constexpr (kPre) {
 #pragma unroll
-            for (int c = 0; c < MM; ++c) dfc[c] = (c < mk && c != col) ? dF[(size_t)c * eff + i] : 0.0;
+            for (int c = 0; c < MM; ++c) dfc[c] = (c < mk && c != col) ? ld_h(dF + (size_t)c * eff + i) : 0.0;
         }
         if (i >= G.na) {
             const long long j = i - G.na;
@@ -1187,12 +1199,12 @@ __global__ __launch_bounds__(kBlock) void k_aa_mix(Seg2 G, double* cur, long lon
         const double g = seg_get(G, i);
         const bool in_eff = i < eff;
         const double ci = in_eff ? cur[i] : 0.0;
-        const double dfo = (!first && in_eff) ? dF[(size_t)j * eff + i] : 0.0;
+        const double dfo = (!first && in_eff) ? ld_h(dF + (size_t)j * eff + i) : 0.0;
         constexpr bool kPre = MM <= 16;   // as in k_aa_reduce
         double dgc[kPre ? MM : 1];
         if constexpr (kPre) {
 #pragma unroll
-            for (int c = 0; c < MM; ++c) dgc[c] = (!first && c < mk) ? dG[(size_t)c * dim + i] : 0.0;
+            for (int c = 0; c < MM; ++c) dgc[c] = (!first && c < mk) ? ld_h(dG + (size_t)c * dim + i) : 0.0;
         }
         const double f = in_eff ? g - ci : 0.0;
         double res;

@@ -378,7 +378,7 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
             if (std::fabs(r[i] - P * h[i]) > 1e-12 * std::fabs(P * h[i]))
                 throw Error(ERR_ARG, "solve_ADMM: the ranks were given different problems");
     }
-    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::kTopRows, P > 1 ? P : 0, top_dense,
+    NdTree tree = nested_dissection(n_, init_x3, aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::top_rows(), P > 1 ? P : 0, top_dense,
                                      part_top_rows);
     top_beg_ = P > 1 ? tree.top_beg : n_;
     own_beg_ = P > 1 ? tree.part_beg[rank_] : 0;

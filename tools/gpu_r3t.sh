@@ -23,7 +23,7 @@ f=$(find "$R/gpurun_out/prof_r3t" -name "*kernel_trace.csv" | head -1); python3 
 cd "$R"
 timeout -k 10 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_r3t_c4.log 2> gpurun_out/bench_r3t_c4.err; rc=$?
 echo "bench c4 rc=$rc"; cut -c1-250 gpurun_out/bench_r3t_c4.log; [ $rc -ne 0 ] && { tail -20 gpurun_out/bench_r3t_c4.err; exit $rc; }
-for cfg in c2 c5; do
+for cfg in ${EXTRA_CFGS:-}; do
   timeout -k 10 600 python3 -u bench.py --config $cfg --steps 10 --warmup 3 > gpurun_out/bench_r3t_$cfg.log 2> gpurun_out/bench_r3t_$cfg.err; rc=$?
   echo "bench $cfg rc=$rc"; cut -c1-200 gpurun_out/bench_r3t_$cfg.log; [ $rc -ne 0 ] && { tail -20 gpurun_out/bench_r3t_$cfg.err; exit $rc; }
 done
