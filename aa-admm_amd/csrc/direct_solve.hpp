@@ -31,10 +31,14 @@ namespace aa {
 class DirectSolver {
 public:
     static constexpr int kTopRows = 2048;    // upper tree levels amalgamated into one dense root
-    // the amalgamation budget in pivots (AA_TOP_ROWS overrides kTopRows)
-    static int top_rows() {
+    // the amalgamation budget in pivots for an n-unknown system (AA_TOP_ROWS overrides): 4096 below
+    // 300 k unknowns, kTopRows above. Measured (same-box sweeps 2048 / 4096 / 6500 / 10000): C2
+    // (25 k) 6 740 -> 8 173 it/s at 4096 (solve 91 -> 66 us: the top levels of a small tree are
+    // latency, not bytes), C3 (101 k) 1 238 -> 1 300, C4 (211 k) flat, C5 (501 k) 167.9 -> 164.9
+    // (the larger dense top costs more bytes than its levels cost latency)
+    static int top_rows(int n) {
         const char* e = std::getenv("AA_TOP_ROWS");
-        return e ? std::atoi(e) : kTopRows;
+        return e ? std::atoi(e) : (n < 300000 ? 4096 : kTopRows);
     }
     static constexpr int kPartTopRows = 4096;   // partitioned: a part's upper levels amalgamated (rows)
     static constexpr int kWaveP = 192;       // forward rows longer than this: wave per row

@@ -332,7 +332,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
                                                               : DirectSolver::kPartTopRows;
     const int nd_leaf = default_nd_leaf(nf_);
     stamp("adjacency");
-    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::top_rows(), P > 1 ? P : 0, top_dense,
+    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::top_rows(nf_), P > 1 ? P : 0, top_dense,
                                      part_top_rows);
     stamp("nested dissection");
     node2int_.assign(n, -1);

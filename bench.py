@@ -607,12 +607,14 @@ def main():
 
     barrier(dist, ctx)
     t0 = time.perf_counter()
-    iters_run, tte = 0, []
+    iters_run, tte, rejects = 0, [], 0
     for _ in range(args.steps):
         solver.step()
         rt = solver.runtime()
         iters_run += rt.iterations
-        tte.append(eps_stats(solver.history()["comb"], solver.times(), EPS_ELASTIC))
+        h = solver.history()
+        rejects += int(np.sum(h["reject"]))
+        tte.append(eps_stats(h["comb"], solver.times(), EPS_ELASTIC))
     barrier(dist, ctx)
     elapsed = time.perf_counter() - t0
     elapsed_max = allreduce(dist, elapsed, _max_op(dist))
@@ -721,6 +723,8 @@ def main():
                        "global_solve": "supernodal direct", "nnz_factor": rt.nnz_factor,
                        "setup_ms": round(setup_ms, 1)},
             "iters_executed": int(iters_all),
+            # Anderson rejects in the timed steps (each re-runs a one-set solve: SURVEY App. B.11)
+            "anderson_rejects": rejects,
             # run-to-epsilon leg (cap 500, stop at 1e-8 comb_0); null when no step reached it
             "time_to_eps_ms": eps_leg["median_ms"] if eps_leg else None, "eps_rel": EPS_ELASTIC,
             "time_to_eps": eps_leg,
