@@ -17,7 +17,6 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
 #include <numeric>
 
 #include "dense_gpu.hpp"
@@ -167,31 +166,8 @@ int GeomSolver::add_ref_surface(const double* V3, int nv, const int* F3, int nf)
     S.nodes.reserve(nf);
     S.tris.reserve(nf);
     B.build(0, nf);
-    {   // every leaf's sibling path (bvh_closest's warm query) and every triangle's leaf
-        S.tleaf.assign(S.tris.size(), -1);
-        std::vector<int> path;   // siblings of the nodes on the current root path, top-down
-        std::function<void(int)> visit = [&](int i) {
-            BvhNode& nd = S.nodes[i];
-            const int nc = bvh_count(nd);
-            if (nc > 0) {
-                nd.sib = (int)S.sibs.size();
-                S.sibs.push_back((int)path.size());
-                for (auto it = path.rbegin(); it != path.rend(); ++it) S.sibs.push_back(*it);
-                for (int t = nd.a; t < nd.a + nc; ++t) S.tleaf[t] = i;
-                return;
-            }
-            path.push_back(nd.a);   // the left child's sibling: the right child
-            visit(i + 1);
-            path.back() = i + 1;    // the right child's sibling: the left child
-            visit(nd.a);
-            path.pop_back();
-        };
-        visit(0);
-    }
     S.dnodes.upload(S.nodes, s());
     S.dtris.upload(S.tris, s());
-    S.dtleaf.upload(S.tleaf, s());
-    S.dsibs.upload(S.sibs, s());
     AA_HIP(hipStreamSynchronize(s()));
     surfs_.push_back(std::move(S));
     return (int)surfs_.size() - 1;
@@ -512,7 +488,7 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
         d.idx = dg.idx.p;
         d.prm = dg.prm.p;
         d.warm = nullptr;
-        d.surf = SurfDev{nullptr, nullptr, 0, 0, nullptr, nullptr};
+        d.surf = SurfDev{nullptr, nullptr, 0, 0};
         if (hg.surf >= 0) {
             dg.warm.alloc(cnt);
             d.warm = dg.warm.p;

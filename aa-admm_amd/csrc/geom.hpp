@@ -62,13 +62,9 @@ private:
     struct Surface {
         std::vector<BvhNode> nodes;
         std::vector<BvhTri> tris;
-        std::vector<int> tleaf, sibs;
         DevBuf<BvhNode> dnodes;
         DevBuf<BvhTri> dtris;
-        DevBuf<int> dtleaf, dsibs;
-        SurfDev dev() const {
-            return SurfDev{dnodes.p, dtris.p, (int)nodes.size(), (int)tris.size(), dtleaf.p, dsibs.p};
-        }
+        SurfDev dev() const { return SurfDev{dnodes.p, dtris.p, (int)nodes.size(), (int)tris.size()}; }
     };
     struct Reg { std::vector<int> idx; std::vector<double> coef; double tgt[3]; };
     // reference-surface constraints processed in the points' nested-dissection order

@@ -249,10 +249,6 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
 #ifndef AA_WARM_TIGHT
 #define AA_WARM_TIGHT 64.0
 #endif
-// warm queries over the warm leaf's sibling path (0 = the root traversal for every query, A/B)
-#ifndef AA_SIB_PATH
-#define AA_SIB_PATH 1
-#endif
 
 // exact closest point on the surface. Stackless depth-first traversal over escape links
 // (`skip` = the node after a subtree): no per-lane stack, so no scratch memory. The upper
@@ -279,55 +275,6 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         const double e2 = (v[3] - v[0]) * (v[3] - v[0]) + (v[4] - v[1]) * (v[4] - v[1]) + (v[5] - v[2]) * (v[5] - v[2]);
         tight = best <= AA_WARM_TIGHT * e2;
     }
-#if AA_SIB_PATH
-    if (tight && S.sibs) {
-        // Warm query over the warm triangle's sibling path: its leaf, then the subtree of the
-        // sibling of every node on the leaf's root path, nearest level first. Those subtrees and
-        // the leaf partition the tree, and a subtree is skipped only when its box cannot beat the
-        // current best, so the minimum is the full traversal's; the root-to-leaf descent (a chain of
-        // ~2 x depth dependent node loads) becomes one path load and independent box tests, two at
-        // a time. Ties resolve toward the first found (the warm triangle, then nearest levels).
-        const int L = S.tleaf[warm];
-        const BvhNode nl = S.nodes[L];
-        for (int t = nl.a; t < nl.a + bvh_count(nl); ++t)
-            if (t != warm) test_tri(t);
-        const int* sp = S.sibs + nl.sib;
-        const int D = sp[0];
-        for (int k0 = 0; k0 < D; k0 += 2) {
-            const int i0 = sp[1 + k0], i1 = sp[1 + min(k0 + 1, D - 1)];
-            const BvhNode s0 = S.nodes[i0], s1 = S.nodes[i1];
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                if (k0 + m >= D) break;
-                const BvhNode& sn = m ? s1 : s0;
-                const int id = m ? i1 : i0;
-                if (!(box_d2(sn, px, py, pz) < best)) continue;
-                const int nc = bvh_count(sn);
-                if (nc > 0) {
-                    for (int t = sn.a; t < sn.a + nc; ++t) test_tri(t);
-                    continue;
-                }
-                int i = id + 1;
-                const int end = bvh_skip(sn);
-                while (i < end) {
-                    const BvhNode nd = S.nodes[i];
-                    if (box_d2(nd, px, py, pz) < best) {
-                        const int c = bvh_count(nd);
-                        if (c > 0) {
-                            for (int t = nd.a; t < nd.a + c; ++t) test_tri(t);
-                            i = bvh_skip(nd);
-                        } else {
-                            i = i + 1;
-                        }
-                    } else {
-                        i = bvh_skip(nd);
-                    }
-                }
-            }
-        }
-        return best_t;
-    }
-#endif
     if (!tight)
     {   // greedy descent to the nearest-box leaf: a tight bound even when the point slid far
         // from its previous triangle (the warm bound alone then lets the traversal open every

@@ -22,15 +22,11 @@ constexpr int kGeoMaxK = 8;   // planes up to this valence run in registers; lar
 // normal n and the range [dlo, dhi] of n . v over its vertices (rounded outward). The slab
 // bounds the distance to every triangle of the subtree from below like the box does, and is
 // far tighter for sloped, thin patches seen from afar (a point well off the surface).
-// sib (leaves): offset of the leaf's sibling path in SurfDev::sibs -- the count D, then the
-// sibling of every node on the leaf's root path, bottom-up (the leaf's own sibling first)
 struct BvhNode {
     float lo[3], hi[3];
     int a;
     unsigned sn;
-    float nrm[3], dlo, dhi;
-    int sib;
-    float pad[2];
+    float nrm[3], dlo, dhi, pad[3];
 };
 __host__ __device__ inline int bvh_skip(const BvhNode& n) { return (int)(n.sn & 0x1fffffffu); }
 __host__ __device__ inline int bvh_count(const BvhNode& n) { return (int)(n.sn >> 29); }
@@ -39,8 +35,6 @@ struct SurfDev {
     const BvhNode* nodes;
     const BvhTri* tris;
     int n_nodes, n_tris;
-    const int* tleaf;   // leaf node of every triangle (leaf order)
-    const int* sibs;    // sibling paths (BvhNode::sib)
 };
 
 // One homogeneous block of constraints (same type / index count / weight / hard-soft).
