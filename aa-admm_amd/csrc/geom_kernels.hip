@@ -249,6 +249,11 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
 #ifndef AA_WARM_TIGHT
 #define AA_WARM_TIGHT 64.0
 #endif
+// share of a wave's live lanes that must hold a leaf before the wave tests leaf triangles
+// (0 = one loop: test as soon as any lane reaches a leaf); see bvh_closest
+#ifndef AA_BVH_HOLD_PCT
+#define AA_BVH_HOLD_PCT 50
+#endif
 
 // exact closest point on the surface. Stackless depth-first traversal over escape links
 // (`skip` = the node after a subtree): no per-lane stack, so no scratch memory. The upper
@@ -292,6 +297,43 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
     }
     const int seed = best_t;
     int i = 0;
+#if AA_BVH_HOLD_PCT > 0
+    // Two-phase ("while-while") schedule of the same per-lane traversal: a lane that reaches a
+    // leaf whose box passes parks on it while the other lanes keep walking inner nodes; the
+    // wave tests leaf triangles only once at least AA_BVH_HOLD_PCT % of its live lanes hold a
+    // leaf (or none walks any more). Each lane visits the same nodes and tests the same
+    // triangles in the same order as the one-loop form below -- only the interleaving across
+    // the wave changes -- so the result is bit-identical. What changes is the SIMD use of the
+    // triangle tests: in one loop, every step where any lane sits on a leaf runs the whole
+    // (divergent) triangle body for the wave.
+    int hold_a = -1, hold_n = 0;
+    bool done = S.n_nodes <= 0;
+    for (;;) {
+        for (;;) {
+            if (!done && hold_a < 0) {
+                const BvhNode nd = S.nodes[i];
+                if (box_d2(nd, px, py, pz) < best) {
+                    const int nc = bvh_count(nd);
+                    if (nc > 0) { hold_a = nd.a; hold_n = nc; i = bvh_skip(nd); }
+                    else i = i + 1;
+                } else {
+                    i = bvh_skip(nd);
+                }
+                if (hold_a < 0 && i >= S.n_nodes) done = true;
+            }
+            const unsigned long long live = __ballot(!done), held = __ballot(hold_a >= 0);
+            const int nl = __popcll(live), nh = __popcll(held);
+            if (nh == nl || (nh > 0 && 100 * nh >= AA_BVH_HOLD_PCT * nl)) break;
+        }
+        if (__ballot(!done) == 0ull) break;
+        if (hold_a >= 0) {
+            for (int t = hold_a; t < hold_a + hold_n; ++t)
+                if (t != seed) test_tri(t);
+            hold_a = -1;
+            if (i >= S.n_nodes) done = true;
+        }
+    }
+#else
     while (i < S.n_nodes) {
         const BvhNode nd = S.nodes[i];
         if (box_d2(nd, px, py, pz) < best) {
@@ -307,6 +349,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
             i = bvh_skip(nd);
         }
     }
+#endif
     return best_t;
 }
 

@@ -71,8 +71,15 @@ def main():
             n2 = int(wall[k].get("n:" + paths[-1], 0))
             if extra in c and n2:
                 row[extra.lower()[3:] + "_per_dispatch"] = c[extra] / n2
-        if "SQ_WAVE_CYCLES" in c and "SQ_ACTIVE_INST_ANY" in c:
-            pass
+        if c.get("SQ_WAVES"):   # per-wave figures (SQ_WAVES counted in the first pass)
+            nw = c["SQ_WAVES"]
+            row["wave_cycles_per_wave"] = wc / nw
+            row["valu_insts_per_wave"] = c.get("SQ_INSTS_VALU", 0) / nw
+            if n and int(wall[k].get("n:" + paths[-1], 0)):
+                nw2 = nw / n * int(wall[k].get("n:" + paths[-1], 0))   # waves of the second pass
+                for extra in ("SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU"):
+                    if extra in c:
+                        row[extra.lower()[3:] + "_per_wave"] = c[extra] / nw2
         if "SQ_ACTIVE_INST_ANY" in c and "SQ_WAIT_INST_ANY" in c:
             tot = c["SQ_ACTIVE_INST_ANY"] + c["SQ_WAIT_INST_ANY"]
             row["issue_stall_share"] = c["SQ_WAIT_INST_ANY"] / tot if tot else 0
