@@ -868,6 +868,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
     reduce_partials();
     launch_control(CTL_PRIM_CHECK_Z, c, ga_, nullptr, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     if (accel) {   // reject branch (gated on the device; a no-op unless prim increased)
+        ev_begin("reject");
         launch_copy(u_.p, du_.p, Z_, c, 1, s());
         launch_copy(xfull_.p, dx_.p, nx, c, 1, s());
         launch_copy(z_.p, dz_.p, Z_, c, 1, s());
@@ -877,12 +878,15 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         solver_.solve(b_.p, xfull_.p, c, 1, s());
         prim_all(xfull_.p, z_.p, nullptr, 1);
         reduce_partials();
+        ev_end("reject");
     }
     launch_control(CTL_PRIM_FINAL_Z, c, ga_, nullptr, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     if (accel) {
         const int m = st_.anderson_m;
+        ev_begin("copy");
         launch_copy(dx_.p, xfull_.p, nx, c, 0, s());
         launch_copy(du_.p, u_.p, Z_, c, 0, s());
+        ev_end("copy");
         // default_z = update_z(curr_x, curr_u) (Solver.cpp:196-199); the same pass writes the
         // rhs slots of the combined-residual solve, w (w default_z + C - curr_u)
         // (Solver.cpp:220): curr_u is final for this iteration and the AA step does not touch it

@@ -642,7 +642,7 @@ def main():
         if comm is None:
             solver.bench_iterations(min(args.iters, 50))
         names = ("local_z", "solve", "resid", "rhs", "aa") if sc.variant == 1 else \
-                ("grad", "rhs", "solve", "solve1", "prim", "local_z", "aa", "comb")
+                ("grad", "rhs", "solve", "solve1", "prim", "local_z", "aa", "comb", "reject", "copy")
         stats = {k: solver.kernel_stats(k) for k in names}
         per_iter = {k: v["avg_ms"] * v["launches"] for k, v in stats.items()}
         k = "solve"   # the global solve: the dominant HBM-bound phase (north_star roofline)
