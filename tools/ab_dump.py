@@ -1,7 +1,7 @@
 """Run one scene through the library AA_ADMM_LIB points at and dump its trajectory (A/B builds:
 two runs, then `python tools/ab_dump.py --compare a.npz b.npz` checks they are bit-identical).
 
-    AA_ADMM_LIB=ab/lib_x.so python tools/ab_dump.py out.npz [drop40|c4small|cloth|pq]
+    AA_ADMM_LIB=ab/lib_x.so python tools/ab_dump.py out.npz [drop40|c4small|cloth|pq|wire]
 """
 import os
 import sys
@@ -23,9 +23,10 @@ def main():
     which = sys.argv[2] if len(sys.argv) > 2 else "drop40"
     ctx = pkg.capi.Context(0)
     out = {}
-    if which == "pq":
+    if which in ("pq", "wire"):
         gs = importlib.import_module("aa-admm_amd.geom_scenes")
-        sc = gs.pq_heightfield(64, 64, iters=60, aa_m=10, noise=0.3)
+        sc = gs.pq_heightfield(64, 64, iters=60, aa_m=10, noise=0.3) if which == "pq" else \
+            gs.wire_grid(40, 40, iters=60, aa_m=20)
         h, g = pkg.capi.run_geom(ctx, sc)
         out = {"comb": h["comb"], "x": h["x"]}
         g.close()

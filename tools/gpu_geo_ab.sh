@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 envof() { case $1 in *+*) echo "${1#*+}";; esac; }
 set -- $TAGS; base=$1
 for v in $TAGS; do
-  env $(envof $v) AA_ADMM_LIB=$PWD/ab/lib_${v%%+*}.so timeout -k 10 120 python -u tools/ab_dump.py gpurun_out/ab_pq_$v.npz pq > gpurun_out/ab_pq_$v.log 2>&1 || { echo "dump $v failed"; tail -5 gpurun_out/ab_pq_$v.log; exit 1; }
+  env $(envof $v) AA_ADMM_LIB=$PWD/ab/lib_${v%%+*}.so timeout -k 10 120 python -u tools/ab_dump.py gpurun_out/ab_pq_$v.npz ${DUMP:-pq} > gpurun_out/ab_pq_$v.log 2>&1 || { echo "dump $v failed"; tail -5 gpurun_out/ab_pq_$v.log; exit 1; }
   [ $v != $base ] && { echo -n "$v vs $base: "; python tools/ab_dump.py --compare gpurun_out/ab_pq_$base.npz gpurun_out/ab_pq_$v.npz || exit 1; }
 done
 for cfg in ${CFGS:-c5 c3}; do
