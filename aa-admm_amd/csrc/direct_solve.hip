@@ -568,6 +568,9 @@ __device__ __forceinline__ void stream_signal(int* sync, int sig, int lane) {
     if (lane == 0) __hip_atomic_fetch_add((gu32*)(sync + sig), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef AA_FWD_TRI
+#define AA_FWD_TRI 1   // k_fwd_ptile: padding rows load nothing, the zero upper triangle is skipped per lane
+#endif
 template <int NR, int CH, int kFwdTileCols, int DEPTH, bool STREAM, bool NT>
 __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __restrict__ tiles, int first,
                                                    const double* __restrict__ Gt, const long long* __restrict__ ell,
@@ -591,14 +594,26 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
     if (t.r0 + 64 <= t.p) nloc = min(nloc, t.r0 + 64 - (t.c0 + i0));   // zero upper triangle: not loaded
     const bool live = nloc > 0;   // wave-uniform: rows past R read the block's zero padding
     const int qmax = (nloc - 1) >> 1;   // last pair with a live column (later indices re-read it: cache hits)
+#if AA_FWD_TRI
+    // per lane (= row r0 + lane): rows past R are zero padding (load nothing), and a row of the
+    // diagonal block needs columns <= its own only (the upper triangle of L_PP^-1 is zero): its
+    // later pairs re-read its last needed pair (cache hits) and their terms are masked
+    const int row = t.r0 + lane;
+    const bool lane_live = row < t.R;
+    const int hi = row < t.p ? row - (t.c0 + i0) : per;   // last needed wave-local column
+    const int qlane = hi < 0 ? 0 : min(qmax, hi >> 1);
+#else
+    constexpr bool lane_live = true;
+    const int hi = per, qlane = qmax;
+#endif
     const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * (per / 2) * 64 + lane;
     constexpr int DP = DEPTH < NC ? DEPTH : NC;   // chunks in flight
     double2 gbuf[DP][C2];
     auto ld = [&](double2* g, int k) {
 #pragma unroll
-        for (int q = 0; q < C2; ++q) g[q] = ld_f2<NT>(G + (size_t)min(k * C2 + q, qmax) * 64);
+        for (int q = 0; q < C2; ++q) g[q] = ld_f2<NT>(G + (size_t)min(k * C2 + q, qlane) * 64);
     };
-    if (live) {
+    if (live && lane_live) {
 #pragma unroll
         for (int d = 0; d < DP; ++d) ld(gbuf[d], d);
     }
@@ -610,13 +625,13 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __
     __syncthreads();
     double a[NR];
     zero<NR>(a);
-    if (live) {
+    if (live && lane_live) {
         auto use = [&](const double2* g, int k) {
 #pragma unroll
             for (int q = 0; q < C2; ++q) {
                 const int i = k * C + 2 * q;
-                const double g0 = i < nloc ? g[q].x : 0.0;
-                const double g1 = i + 1 < nloc ? g[q].y : 0.0;
+                const double g0 = i < nloc && i <= hi ? g[q].x : 0.0;
+                const double g1 = i + 1 < nloc && i + 1 <= hi ? g[q].y : 0.0;
 #pragma unroll
                 for (int m = 0; m < NR; ++m) a[m] += g0 * f[NR * (i0 + i) + m];
 #pragma unroll
@@ -694,6 +709,9 @@ __device__ __forceinline__ void bwd_row_s(const N& t, int r, const int* __restri
     }
 }
 
+#ifndef AA_BWD_TRI
+#define AA_BWD_TRI 1   // k_bwd_ptile skips the zero upper triangle of L_PP^-1
+#endif
 template <int NR, int CH, int kBwdTileRows, int DEPTH, bool STREAM, bool NT>
 __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __restrict__ tiles, int first,
                                                    const double* __restrict__ Gt, const int* __restrict__ bnd,
@@ -716,16 +734,35 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
     const int i0 = w * per;
     const int nloc = min(per, t.nr - i0);
     const bool live = nloc > 0;   // wave-uniform: columns past p read the block's zero padding
-    const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * per * 64 + lane;
+    // narrow block (<= 64 columns, block-uniform): lane l holds column c0 + l, and its 16-B load
+    // covers two consecutive rows of it (k_pack_btiles) -- half the bytes of a 128-column block,
+    // whose upper half would be zero padding. Each column still sums its rows in ascending order.
+    const bool nar = t.p - t.c0 <= 64;
+    const int nld = nar ? (nloc + 1) >> 1 : nloc;   // 16-B rows of this wave
+    const double2* G = reinterpret_cast<const double2*>(Gt + t.toff) + (size_t)w * (nar ? per / 2 : per) * 64 + lane;
     constexpr int DP = DEPTH < NC ? DEPTH : NC;   // chunks in flight
+    constexpr int NCN = (per / 2 + C - 1) / C;     // chunks of a narrow wave (per / 2 row pairs)
+    // lanes whose columns all lie past p hold zero padding: they load nothing (no lines fetched)
+    const bool lane_live = (nar ? lane : 2 * lane) < t.p - t.c0;
+    // rows above the diagonal of L_PP^-1 (row < the lane's first column) are zeros: the lane's
+    // loads for them re-read its first needed 16-B row (cache hits) and their terms are masked
+    // (the stored zeros added nothing, so the sums are unchanged)
+#if AA_BWD_TRI
+    const int lo_row = t.c0 + (nar ? lane : 2 * lane) - (t.r0 + i0);
+    const int lo = lo_row <= 0 ? 0 : min(nar ? lo_row >> 1 : lo_row, nld - 1);
+#else
+    constexpr int lo = 0;
+#endif
     double2 gbuf[DP][C];
     auto ld = [&](double2* g, int k) {
 #pragma unroll
-        for (int q = 0; q < C; ++q) g[q] = ld_f2<NT>(G + (size_t)min(k * C + q, nloc - 1) * 64);
+        for (int q = 0; q < C; ++q)
+            g[q] = ld_f2<NT>(G + (size_t)min(max(k * C + q, lo), nld - 1) * 64);
     };
-    if (live) {
+    if (live && lane_live) {
 #pragma unroll
-        for (int d = 0; d < DP; ++d) ld(gbuf[d], d);
+        for (int d = 0; d < DP; ++d)
+            if (!nar || d < NCN) ld(gbuf[d], d);
     }
     if constexpr (STREAM) stream_wait(sync, t.dep, t.need, w, lane);   // the parent's x rows
     for (int i = tid; i < kBwdTileRows; i += 256) {
@@ -739,12 +776,12 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
     __syncthreads();
     double a[W];
     zero<W>(a);
-    if (live) {
+    if (live && lane_live && !nar) {
         auto use = [&](const double2* g, int k) {
 #pragma unroll
             for (int q = 0; q < C; ++q) {
                 const int i = k * C + q;
-                const double2 gq = i < nloc ? g[q] : make_double2(0.0, 0.0);
+                const double2 gq = i < nloc && i >= lo ? g[q] : make_double2(0.0, 0.0);
 #pragma unroll
                 for (int m = 0; m < NR; ++m) {
                     const double vk = v[NR * (i0 + i) + m];
@@ -757,6 +794,24 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
         for (int k = 0; k < NC; ++k) {
             use(gbuf[k % DP], k);
             if (k + DP < NC) ld(gbuf[k % DP], k + DP);
+        }
+    } else if (live && lane_live) {   // narrow: rows 2i, 2i+1 of column c0 + lane (the odd tail row is zero)
+        auto use = [&](const double2* g, int k) {
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                const int i = k * C + q;
+                const double2 gq = i < nld && i >= lo ? g[q] : make_double2(0.0, 0.0);
+                const double* v0 = v + NR * (i0 + 2 * min(i, nld - 1));   // masked terms: finite
+#pragma unroll
+                for (int m = 0; m < NR; ++m) a[m] += gq.x * v0[m];
+#pragma unroll
+                for (int m = 0; m < NR; ++m) a[m] += gq.y * v0[NR + m];
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < NCN; ++k) {
+            use(gbuf[k % DP], k);
+            if (k + DP < NCN) ld(gbuf[k % DP], k + DP);
         }
     }
     if (w > 0)
@@ -774,20 +829,22 @@ __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __
     const BRed rd = reds[t.rid];
     if (!arrive_last(cnt + t.rid, rd.nt, lane)) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (2 * lane < rd.nc) {
+    const int cl = nar ? lane : 2 * lane;   // this lane's first column in the block
+    if (cl < rd.nc) {
         double b[W];
         zero<W>(b);
         const double* q = part + (NR / 3) * rd.poff + W * lane;
         red_tiles<W, W * 64>(q, rd.nt, b);
-        const size_t xo = (size_t)(rd.beg + rd.c0 + 2 * lane - ext_off);
+        const bool two = !nar && cl + 1 < rd.nc;
+        const size_t xo = (size_t)(rd.beg + rd.c0 + cl - ext_off);
         st_ext<NR>(X0, X1, xo, b);
-        if (2 * lane + 1 < rd.nc) st_ext<NR>(X0, X1, xo + 1, b + NR);
+        if (two) st_ext<NR>(X0, X1, xo + 1, b + NR);
         if constexpr (STREAM) {
             if (rd.sig >= 0) {   // the children of this supernode read these rows in this launch
-                double* xs = Xs + NR * (size_t)(rd.xso + rd.c0 + 2 * lane);
+                double* xs = Xs + NR * (size_t)(rd.xso + rd.c0 + cl);
 #pragma unroll
                 for (int m = 0; m < NR; ++m) st_sc1(xs + m, b[m]);
-                if (2 * lane + 1 < rd.nc)
+                if (two)
 #pragma unroll
                     for (int m = 0; m < NR; ++m) st_sc1(xs + NR + m, b[NR + m]);
             }
@@ -816,10 +873,12 @@ __global__ void k_pack_btiles(const BTile* __restrict__ tiles, const int* __rest
                               const double* __restrict__ Gr, double* __restrict__ Gt) {
     const BTile t = tiles[blockIdx.x];
     const int W = width[blockIdx.x], R = t.p + t.nb;
-    const long long n = 128LL * W;
+    const bool nar = t.p - t.c0 <= 64;   // narrow block: lane = column, a 16-B pair = two rows
+    const long long n = (nar ? 64LL : 128LL) * W;
     for (long long idx = threadIdx.x; idx < n; idx += blockDim.x) {
-        const int j = (int)(idx & 1), lane = (int)((idx >> 1) & 63), q = (int)(idx >> 7);
-        const int row = t.r0 + q, col = t.c0 + 2 * lane + j;
+        const int j = (int)(idx & 1), lane = (int)((idx >> 1) & 63), q0 = (int)(idx >> 7);
+        const int q = nar ? 2 * q0 + j : q0;
+        const int row = t.r0 + q, col = nar ? t.c0 + lane : t.c0 + 2 * lane + j;
         Gt[t.toff + idx] = (q < t.nr && row < R && col < t.p) ? Gr[t.goff + (size_t)row * t.ldr + col] : 0.0;
     }
 }
@@ -1586,7 +1645,10 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     if (packed_ && (!ftiles.empty() || !btiles.empty())) {
         long long to = 0;
         for (size_t i = 0; i < ftiles.size(); ++i) { ftiles[i].toff = to; to += 64LL * fwid[i]; }
-        for (size_t i = 0; i < btiles.size(); ++i) { btiles[i].toff = to; to += 128LL * bwid[i]; }
+        for (size_t i = 0; i < btiles.size(); ++i) {   // narrow blocks (<= 64 columns): half (k_pack_btiles)
+            btiles[i].toff = to;
+            to += (btiles[i].p - btiles[i].c0 <= 64 ? 64LL : 128LL) * bwid[i];
+        }
         Gt_.alloc((size_t)to);
         DevBuf<FTile> dft;
         DevBuf<BTile> dbt;
