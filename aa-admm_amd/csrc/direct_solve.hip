@@ -569,7 +569,7 @@ __device__ __forceinline__ void stream_signal(int* sync, int sig, int lane) {
 }
 
 #ifndef AA_FWD_TRI
-#define AA_FWD_TRI 1   // k_fwd_ptile: padding rows load nothing, the zero upper triangle is skipped per lane
+#define AA_FWD_TRI 0   // 1: k_fwd_ptile padding rows load nothing, zero upper triangle skipped per lane (measured: no gain)
 #endif
 template <int NR, int CH, int kFwdTileCols, int DEPTH, bool STREAM, bool NT>
 __global__ __launch_bounds__(256, AA_TILE_MINW) void k_fwd_ptile(const FTile* __restrict__ tiles, int first,
@@ -710,7 +710,7 @@ __device__ __forceinline__ void bwd_row_s(const N& t, int r, const int* __restri
 }
 
 #ifndef AA_BWD_TRI
-#define AA_BWD_TRI 1   // k_bwd_ptile skips the zero upper triangle of L_PP^-1
+#define AA_BWD_TRI 0   // 1: k_bwd_ptile skips the zero upper triangle of L_PP^-1 per lane (measured slower)
 #endif
 template <int NR, int CH, int kBwdTileRows, int DEPTH, bool STREAM, bool NT>
 __global__ __launch_bounds__(256, AA_TILE_MINW) void k_bwd_ptile(const BTile* __restrict__ tiles, int first,
