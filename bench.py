@@ -386,20 +386,19 @@ def geom_line(args, world, rank, local, dist):
                        "nnz_factor": rt0.nnz_factor, "setup_ms": round(setup_ms, 1),
                        "factor_ms": round(rt0.factor_ms, 1), "setup_breakdown": setup_breakdown},
             "accepted_iters": int(acc_all), "x_updates": int(xupd),
-            "time_to_eps_ms": (round(statistics.median(tt), 3) if tt else None),
+            "time_to_eps_ms": all_steps_median([t[1] if t else None for t in tte]),
             "time_to_eps": {"eps_abs": eps, "criterion": "comb <= 2 (1e-8 avg_edge hard_cols)^2 (ALMGeometrySolver.h:173)",
                             "steps": len(tte), "reached": len(tt),
                             "iters_to_eps": [t[0] if t else None for t in tte],
                             "relative": {r: {"reached": sum(1 for x in tte_rel if x[r]),
-                                             "median_ms": (round(statistics.median([x[r]["ms"] for x in tte_rel if x[r]]), 3)
-                                                           if any(x[r] for x in tte_rel) else None),
+                                             "median_ms": all_steps_median([x[r]["ms"] if x[r] else None for x in tte_rel]),
                                              "iters": [x[r]["iters"] if x[r] else None for x in tte_rel]}
                                          for r in ("0.01", "0.0001", "1e-06")},
                             "clock": "device wall_clock64 from the loop start (elapsed_time_)"},
             "run_to_eps": geps,
             "roofline": roof, "cpu_baseline": cpu,
         }
-        if geps is not None and geps["reached"]:   # the headline time-to-eps: the run-to-eps leg
+        if geps is not None:   # the headline time-to-eps: the run-to-eps leg (all solves, unreached = "> cap")
             line["time_to_eps_ms"] = geps["median_ms"]
     g.close()
     if comm is not None:
@@ -438,7 +437,8 @@ def geom_run_to_eps(g, sc, eps, args):
     out = {"criterion": "comb < 2 (1e-8 avg_edge hard_cols)^2 (ALMGeometrySolver.h:172; its stop is commented out "
                         "at :258-260, enabled here by aa_geom_set_stop)", "eps_abs": eps, "cap_accepted": args.geom_eps_cap,
            "solves": len(runs), "reached": len(hit_ms),
-           "median_ms": round(statistics.median(hit_ms), 3) if hit_ms else None,
+           "median_ms": all_steps_median([r["eps_abs"]["ms"] if r["eps_abs"] else None for r in runs]),
+           "median_ms_reached_only": round(statistics.median(hit_ms), 3) if hit_ms else None,
            "clock": "device wall_clock64 from the loop start (elapsed_time_)", "per_solve": runs}
     if not hit_ms:
         out["note"] = (f"not reached in {len(runs)}/{len(runs)} solves with cap {args.geom_eps_cap} accepted iterations; "
@@ -543,20 +543,36 @@ def run_to_eps(solver, args, state0):
     hit = [s[key]["ms"] for s in steps if s[key] is not None]
     its = [s[key]["iters"] for s in steps if s[key] is not None]
     out = {"eps_rel": EPS_ELASTIC, "cap": args.eps_cap, "steps": len(steps), "reached": len(hit),
-           "median_ms": round(statistics.median(hit), 3) if hit else None,
-           "p90_ms": round(float(np.percentile(hit, 90)), 3) if hit else None,
+           # the headline: median over ALL steps, an unreached step counted as "> cap" (null when more
+           # than half of the steps are unreached -- the median is then itself "not reached")
+           "median_ms": all_steps_median([s[key]["ms"] if s[key] is not None else None for s in steps]),
+           "median_ms_reached_only": round(statistics.median(hit), 3) if hit else None,
+           "p90_ms_reached_only": round(float(np.percentile(hit, 90)), 3) if hit else None,
            "iters_to_eps": [s[key]["iters"] if s[key] is not None else None for s in steps],
-           "median_iters": statistics.median(its) if its else None,
+           "median_iters": all_steps_median([s[key]["iters"] if s[key] is not None else None for s in steps]),
            "not_reached_note": (None if len(hit) == len(steps) else
                                 f"not reached in {len(steps) - len(hit)}/{len(steps)} steps with cap {args.eps_cap}"),
            "clock": "device wall_clock64 from the step's start (prologue included) to the end of the iteration "
                     "reaching comb <= eps_rel * comb_0", "per_step": steps}
     for e in (1e-4, 1e-6):
         k = f"{e:g}"
-        v = [s[k]["ms"] for s in steps if s[k] is not None]
-        out[f"median_ms_{k}"] = round(statistics.median(v), 3) if v else None
-        out[f"reached_{k}"] = len(v)
+        v = [s[k]["ms"] if s[k] is not None else None for s in steps]
+        out[f"median_ms_{k}"] = all_steps_median(v)
+        out[f"reached_{k}"] = sum(1 for t in v if t is not None)
     return out
+
+
+def all_steps_median(vals):
+    """Median over every step, None (not reached) ranked above every reached value; None when the
+    median itself falls on an unreached step."""
+    if not vals:
+        return None
+    srt = sorted(vals, key=lambda t: (t is None, t if t is not None else 0.0))
+    n = len(srt)
+    lo, hi = srt[(n - 1) // 2], srt[n // 2]
+    if lo is None or hi is None:
+        return None
+    return round((lo + hi) / 2.0, 3)
 
 
 def main():
@@ -667,7 +683,7 @@ def main():
         except Exception as e:
             roof["read_peak_measured"] = None
             roof["read_peak_error"] = str(e)[:120]
-    if roof is not None:   # HBM bytes per solve from the committed PMC passes (tools/gpu_pmc.sh)
+    if roof is not None:   # HBM bytes per solve from the committed PMC passes (tools/gpu.sh pmc)
         pmc = next((q for q in (os.path.join(REPO, "profiles", f"r{k}_{args.config}_pmc.json") for k in (3, 2, 1))
                     if os.path.exists(q)), "")
         if pmc and comm is None:
@@ -729,7 +745,8 @@ def main():
             "time_to_eps_ms": eps_leg["median_ms"] if eps_leg else None, "eps_rel": EPS_ELASTIC,
             "time_to_eps": eps_leg,
             "eps_in_timed_steps": {"iters_cap": args.iters, "steps": len(tte), "reached": len(tt),
-                                   "median_ms": round(statistics.median(tt), 3) if tt else None},
+                                   "median_ms": all_steps_median([t[1] if t is not None else None for t in tte]),
+                                   "median_ms_reached_only": round(statistics.median(tt), 3) if tt else None},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if comm is not None:

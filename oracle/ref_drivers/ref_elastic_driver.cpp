@@ -196,7 +196,15 @@ int main(int argc, char** argv) {
     for (int k = 1; k <= n_steps; ++k) {
         solver.set_pins(pin_idx, pins_at(k));
         auto t0 = std::chrono::steady_clock::now();
-        solver.step();
+        try {
+            solver.step();
+        } catch (const std::exception& e) {
+            // the reference's own abort (e.g. mcloptlib LBFGS.hpp:192-199): the steps done so far
+            // are already in `out`; report the step and stop (exit 3) so callers keep them
+            fprintf(stderr, "REF_ABORT step %d: %s\n", k, e.what());
+            fclose(out);
+            return 3;
+        }
         step_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         std::vector<double> prim, comb;
         std::vector<int> rej;
@@ -218,6 +226,7 @@ int main(int argc, char** argv) {
         fwrite(rej.data(), sizeof(int), nrec, out);
         fwrite(solver.m_x.data(), sizeof(double), 3 * (size_t)n, out);
         fwrite(solver.m_v.data(), sizeof(double), 3 * (size_t)n, out);
+        fflush(out);
     }
     fwrite(step_ms.data(), sizeof(double), step_ms.size(), out);   // trailer: wall ms of each step()
     fclose(out);

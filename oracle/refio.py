@@ -72,11 +72,17 @@ def read_ref_result(path: str, n_nodes: int):
 
     n_steps = int(take("<i4", 1)[0])
     steps = []
+    step_bytes = 6 * 8 * n_nodes
     for _ in range(n_steps):
-        nrec = int(take("<i4", 1)[0])
+        if off + 4 > len(data):
+            break   # the reference aborted (driver exit 3): the steps it finished
+        nrec = int(np.frombuffer(data, "<i4", 1, off)[0])
+        if off + 4 + 20 * nrec + step_bytes > len(data):
+            break
+        off += 4
         steps.append(dict(prim=take("<f8", nrec), comb=take("<f8", nrec), reject=take("<i4", nrec),
                           x=take("<f8", 3 * n_nodes).reshape(-1, 3), v=take("<f8", 3 * n_nodes).reshape(-1, 3)))
-    if off + 8 * n_steps <= len(data):
+    if len(steps) == n_steps and off + 8 * n_steps <= len(data):
         for s, t in zip(steps, take("<f8", n_steps)):
             s["step_ms"] = float(t)
     return steps

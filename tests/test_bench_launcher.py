@@ -66,3 +66,21 @@ def test_bench_gpus2_partitioned_step_on_one_gpu():
     assert line["n_gpus"] == 2
     assert line["config"]["parallelism"] == "mesh-partitioned2 (host)"
     assert line["iters_executed"] == 20 and line["value"] > 0
+
+
+def test_time_to_eps_median_counts_unreached_steps():
+    """The time-to-epsilon headline is the median over ALL steps with an unreached step ranked
+    above every reached one ("> cap"), so a majority of unreached steps yields null instead of the
+    median of the survivors."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    m = b.all_steps_median
+    assert m([]) is None
+    assert m([10.0, 30.0, 20.0]) == 20.0
+    assert m([10.0, None, 20.0]) == 20.0            # 10, 20, >cap
+    assert m([10.0, None, None]) is None            # the middle step is unreached
+    assert m([10.0, 40.0, None, None]) is None      # even count: the upper middle is unreached
+    assert m([10.0, 40.0, 30.0, None]) == 35.0
+    assert m([None] * 13 + [5.0] * 7) is None       # round 3's 7/20 survivors no longer make a headline

@@ -30,6 +30,8 @@ ap.add_argument("--tets", default="20,8,10")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--cap", type=int, default=500)
 ap.add_argument("--out", required=True)
+ap.add_argument("--npz", default=None, help="also store the per-step curves (prim, comb, reject) here")
+ap.add_argument("--threads", type=int, default=0, help="OMP_NUM_THREADS for --ref (0: inherit)")
 a = ap.parse_args()
 scenes = importlib.import_module("aa-admm_amd.scenes")
 cx, cy, cz = (int(v) for v in a.tets.split(","))
@@ -47,16 +49,24 @@ def stats(comb):
 
 
 t0 = time.time()
+abort = None
+curves = []
 if a.ref:
     import subprocess
     import refio
     with tempfile.TemporaryDirectory() as tmp:
         refio.write_scene(sc, os.path.join(tmp, "s.bin"))
+        env = dict(os.environ)
+        if a.threads:
+            env["OMP_NUM_THREADS"] = str(a.threads)
         r = subprocess.run([os.path.join(REPO, "oracle", "_ref", "ref_elastic_x"), "s.bin", "o.bin"], cwd=tmp,
-                           capture_output=True, text=True)
-        if r.returncode:
+                           capture_output=True, text=True, env=env)
+        if r.returncode == 3:   # the reference threw inside step(): keep the finished steps, record why
+            abort = r.stderr.strip().splitlines()[-1]
+        elif r.returncode:
             sys.exit(r.stderr[-2000:])
         steps = refio.read_ref_result(os.path.join(tmp, "o.bin"), sc.n_nodes)
+    curves = [(s["prim"], s["comb"], s["reject"]) for s in steps]
     per = [stats(s["comb"]) for s in steps]
     src = "reference (oracle/_ref/ref_elastic_x, compiled from admm_anderson_xzu's own sources), this container's CPU"
 else:
@@ -65,15 +75,28 @@ else:
     s = pkg.capi.solver_from_scene(ctx, sc)
     s.initialize(pkg.capi.settings_from_scene(sc))
     per = []
-    for _ in range(a.steps):
-        s.step()
-        per.append(stats(s.history()["comb"]))
+    for k in range(a.steps):
+        try:
+            s.step()
+        except Exception as e:   # aa::Error ERR_NUMERIC: the same abort the reference raises
+            abort = f"GPU_ABORT step {k + 1}: {e}"
+            break
+        h = s.history()
+        curves.append((np.asarray(h["prim"]), np.asarray(h["comb"]), np.asarray(h["reject"])))
+        per.append(stats(h["comb"]))
         print(f"[eps] step {len(per)}: {per[-1]}", file=sys.stderr, flush=True)
     s.close()
     ctx.close()
     src = "GPU solver (libaa_admm.so), MI355X"
 summary = {k: sum(1 for p in per if p[k] is not None) for k in ("0.0001", "1e-06", "1e-08")}
 json.dump({"scene": sc.name, "tets": sc.n_elements(), "nodes": sc.n_nodes, "cap": a.cap, "steps": a.steps,
+           "steps_done": len(per), "abort": abort,
            "reached": summary, "per_step": per, "source": src, "wall_s": round(time.time() - t0, 1)},
           open(a.out, "w"), indent=1)
+if a.npz:
+    np.savez_compressed(a.npz, nrec=np.array([len(c[1]) for c in curves], np.int32),
+                        prim=np.concatenate([c[0] for c in curves]) if curves else np.zeros(0),
+                        comb=np.concatenate([c[1] for c in curves]) if curves else np.zeros(0),
+                        reject=np.concatenate([c[2] for c in curves]).astype(np.int32) if curves else np.zeros(0, np.int32),
+                        tets=np.array(a.tets), cap=a.cap, abort=np.array(abort or ""))
 print(json.dumps({"reached": summary, "wall_s": round(time.time() - t0, 1)}))

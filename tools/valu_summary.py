@@ -1,4 +1,4 @@
-"""Per-kernel VALU figures from the two SQ passes of tools/gpu_valu.sh.
+"""Per-kernel VALU figures from the two SQ passes (tools/gpu.sh pmc, SQ counter groups).
 
     python tools/valu_summary.py gpurun_out/pmc_valu_c4 [out.json]
 
