@@ -20,13 +20,15 @@ AA_VARIANT_Z, AA_VARIANT_UX = 0, 1
 NOACC, ANDERSON = 0, 1
 
 EXPORTS = [
-    "aa_last_error", "aa_version", "aa_ctx_create", "aa_ctx_destroy", "aa_ctx_synchronize", "aa_ctx_bench_read", "aa_lame_from_young",
+    "aa_last_error", "aa_version", "aa_ctx_create", "aa_ctx_destroy", "aa_ctx_synchronize", "aa_ctx_bench_read",
+    "aa_ctx_warm_dense", "aa_lame_from_young",
     "aa_settings_default", "aa_elastic_create", "aa_elastic_destroy", "aa_elastic_add_nodes", "aa_elastic_add_tets",
     "aa_elastic_add_tris", "aa_elastic_set_pins", "aa_elastic_initialize", "aa_elastic_step",
     "aa_elastic_add_obstacle", "aa_elastic_set_collisions", "aa_elastic_add_wind", "aa_elastic_set_wind",
     "aa_elastic_num_nodes", "aa_elastic_get_x", "aa_elastic_get_v", "aa_elastic_set_v", "aa_elastic_get_history",
     "aa_elastic_get_times", "aa_elastic_set_iterations", "aa_elastic_set_x",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats", "aa_elastic_local_stats",
+    "aa_elastic_setup_phases",
     "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_create_solo", "aa_comm_destroy", "aa_comm_info",
     "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
     "aa_geom_create", "aa_geom_create_kind", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
@@ -115,6 +117,12 @@ class Context:
         g = C.c_double()
         _chk(lib().aa_ctx_bench_read(self.h, C.c_longlong(nbytes), C.byref(g)))
         return g.value
+
+    def warm_dense(self):
+        """Wall ms of the one-time rocBLAS / rocSOLVER code-object load (aa_ctx_warm_dense); 0 when warm."""
+        ms = C.c_double()
+        _chk(lib().aa_ctx_warm_dense(self.h, C.byref(ms)))
+        return ms.value
 
     def synchronize(self):
         _chk(lib().aa_ctx_synchronize(self.h))
@@ -343,6 +351,15 @@ class Solver:
         ms = C.c_double()
         _chk(lib().aa_elastic_bench_iterations(self.h, C.c_int(iters), C.byref(ms)))
         return ms.value
+
+    def setup_phases(self):
+        """{phase: ms} of the last initialize() (aa_elastic_setup_phases), in order."""
+        names = C.create_string_buffer(4096)
+        ms = (C.c_double * 64)()
+        n = C.c_int()
+        _chk(lib().aa_elastic_setup_phases(self.h, names, 4096, ms, 64, C.byref(n)))
+        keys = names.value.decode().split("\n") if n.value else []
+        return {k: round(ms[i], 1) for i, k in enumerate(keys[:64])}
 
     def kernel_stats(self, name):
         a, b, n = C.c_double(), C.c_double(), C.c_int()

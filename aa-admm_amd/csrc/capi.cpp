@@ -7,6 +7,7 @@
 
 #include "../../include/aa_admm.h"
 #include "comm.hpp"
+#include "dense_gpu.hpp"
 #include "elastic.hpp"
 #include "geom.hpp"
 
@@ -75,6 +76,14 @@ int aa_ctx_bench_read(aa_ctx ctx, long long bytes, double* gbps) {
         NEED(ctx && gbps && bytes >= 16, "aa_ctx_bench_read: bad argument");
         AA_HIP(hipSetDevice(ctx->c.device));
         *gbps = aa::bench_stream_read(bytes, 10, ctx->c.stream);
+    });
+}
+
+int aa_ctx_warm_dense(aa_ctx ctx, double* ms) {
+    return guarded([&] {
+        NEED(ctx && ms, "aa_ctx_warm_dense: bad argument");
+        AA_HIP(hipSetDevice(ctx->c.device));
+        *ms = aa::warm_gpu_front_backend(ctx->c.stream);
     });
 }
 
@@ -321,6 +330,25 @@ int aa_elastic_local_stats(aa_elastic h, long long* out, int cap, int reset, int
         AA_HIP(hipSetDevice(h->ctx->c.device));
         const int n = h->s->local_stats(out, cap, reset != 0);
         if (count) *count = n;
+    });
+}
+
+int aa_elastic_setup_phases(aa_elastic h, char* names, int names_cap, double* ms, int cap, int* count) {
+    return guarded([&] {
+        NEED(h && cap >= 0 && names_cap >= 0, "bad argument");
+        const auto& ph = h->s->setup_phases();
+        std::string all;
+        for (size_t i = 0; i < ph.size(); ++i) {
+            if (i) all += '\n';
+            all += ph[i].first;
+            if ((int)i < cap && ms) ms[i] = ph[i].second;
+        }
+        if (names && names_cap > 0) {
+            const size_t k = std::min(all.size(), (size_t)names_cap - 1);
+            std::memcpy(names, all.data(), k);
+            names[k] = 0;
+        }
+        if (count) *count = (int)ph.size();
     });
 }
 

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -96,6 +97,11 @@ public:
     bool holds(int s) const override {
         std::lock_guard<std::mutex> g(mu_);
         return held_.count(s) > 0;
+    }
+    void drop(int s) override {
+        std::lock_guard<std::mutex> g(mu_);
+        AA_HIP(hipSetDevice(dev_));
+        held_.erase(s);
     }
     void factor(int s, int f, int p, const std::vector<int>& ai, const std::vector<int>& aj, const std::vector<double>& av,
                 const std::vector<Child>& kids, bool keep_update, std::vector<double>& Linv, std::vector<double>& LBP,
@@ -222,6 +228,31 @@ std::unique_ptr<DenseFrontBackend> make_gpu_front_backend(hipStream_t s) {
     auto b = std::unique_ptr<DenseFrontBackend>(new RocFrontBackend(s));
     if (const char* e = std::getenv("AA_DENSE_MIN_FRONT")) b->min_front = std::max(1, std::atoi(e));
     return b;
+}
+
+double warm_gpu_front_backend(hipStream_t s) {
+    const char* e = std::getenv("AA_DENSE_GPU");
+    if (e && e[0] == '0') return 0.0;
+    int dev = 0;
+    AA_HIP(hipStreamGetDevice(s, &dev));
+    static std::mutex mu;
+    static std::set<int> warm;
+    std::lock_guard<std::mutex> g(mu);
+    if (warm.count(dev)) return 0.0;
+    const auto t0 = std::chrono::steady_clock::now();
+    {   // a diagonally dominant front of the smallest GPU order with a boundary block: potrf, trsm,
+        // syrk, trtri, trmm and the assembly / layout kernels, as every GPU front of a factor runs
+        RocFrontBackend b(s);
+        const int p = b.min_front, f = p + 64;
+        std::vector<int> ai, aj;
+        std::vector<double> av;
+        for (int j = 0; j < p; ++j)
+            for (int i = j; i < f && i < j + 2; ++i) { ai.push_back(i); aj.push_back(j); av.push_back(i == j ? 4.0 : -1.0); }
+        std::vector<double> Linv, LBP, M, U;
+        b.factor(0, f, p, ai, aj, av, {}, false, Linv, LBP, M, &U);
+    }
+    warm.insert(dev);
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 std::unique_ptr<PartFactor> make_part_factor(Comm* comm, int rank, hipStream_t s) {

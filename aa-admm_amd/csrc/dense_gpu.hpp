@@ -13,6 +13,11 @@ namespace aa {
 // the GPU of stream s; AA_DENSE_GPU=0 keeps the whole factorization on the host
 std::unique_ptr<DenseFrontBackend> make_gpu_front_backend(hipStream_t s);
 
+// Loads the backend's rocBLAS / rocSOLVER code objects on the stream's device once per process
+// (one synthetic SPD front of the smallest GPU order through the same calls); returns the wall
+// ms it took (0 if that device is already warm, or AA_DENSE_GPU=0)
+double warm_gpu_front_backend(hipStream_t s);
+
 // multifrontal_cholesky with the GPU backend (or on the host only, AA_DENSE_GPU=0)
 // The partitioned factorization of rank `rank` over `comm` (PartFactor; part r = rank r): host
 // fronts summed by comm's host all-reduce, device fronts by its all-reduce on stream s.

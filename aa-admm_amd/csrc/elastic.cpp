@@ -622,10 +622,13 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     rt_.z_dim = (int)Z_;
     rt_.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     stamp("elements + buffers");
-    if (const char* e = std::getenv("AA_SETUP_TIMES"); e && e[0] == '1') {
+    setup_phases_.clear();
+    {
         double prev = 0;
-        for (auto& ph : phases) { std::fprintf(stderr, "[setup] %-24s %8.1f ms\n", ph.first, ph.second - prev); prev = ph.second; }
+        for (auto& ph : phases) { setup_phases_.push_back({ph.first, ph.second - prev}); prev = ph.second; }
     }
+    if (const char* e = std::getenv("AA_SETUP_TIMES"); e && e[0] == '1')
+        for (auto& ph : setup_phases_) std::fprintf(stderr, "[setup] %-24s %8.1f ms\n", ph.first.c_str(), ph.second);
     // algorithmic bytes per launch class (DESIGN.md "roofline accounting")
     kstats_.clear();
     double lz = 0, rs = 0;

@@ -57,6 +57,7 @@ public:
     bool kernel_stats(const std::string& name, double* avg_ms, double* bytes, int* launches) const;
     // the local-step work queue's diagnostics (kLqStats counters; 0 when not enabled); reset after
     int local_stats(long long* out, int cap, bool reset);
+    const std::vector<std::pair<std::string, double>>& setup_phases() const { return setup_phases_; }
 
 private:
     struct HostGroup {
@@ -133,6 +134,7 @@ private:
     std::vector<int> h_rej_;
     int nrec_ = 0;
     aa_runtime rt_{};
+    std::vector<std::pair<std::string, double>> setup_phases_;   // last initialize(): (phase, ms)
     bool pins_dirty_ = true;
 
     // the whole ADMM loop of a time step, captured once into a hipGraph and replayed per step

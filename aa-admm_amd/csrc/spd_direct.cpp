@@ -318,7 +318,11 @@ void factor_front(FrontCtx& C, int s, std::vector<int>& pos, bool inner_parallel
         std::vector<std::vector<int>> maps(tree.children[s].size());
         for (size_t q = 0; q < tree.children[s].size(); ++q) {
             const int c = tree.children[s][q];
-            if (!take_child(c)) continue;
+            if (!take_child(c)) {   // another rank's share: free what this rank holds of it now
+                if (C.dense->holds(c)) C.dense->drop(c);
+                else std::vector<double>().swap(C.U[c]);
+                continue;
+            }
             for (int i : F.bnd[c]) maps[q].push_back(pos[i]);
             kids.push_back({c, maps[q].data(), (int)maps[q].size(), C.dense->holds(c) ? nullptr : &C.U[c]});
         }
@@ -423,10 +427,32 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
     FrontCtx C{A, tree, F, U, flops, dense, part};
     if (part && (int)tree.part.size() != nn) throw std::runtime_error("multifrontal_cholesky: partitioned factor needs a partitioned tree");
     auto mine = [&](int s) { return !part || tree.part[s] == part->my_part; };
+    // partitioned: a rank whose own part fails (not positive definite) must not leave the others
+    // waiting in the first top front's sum -- every rank reports its own-part outcome first and
+    // all of them throw together (the top fronts are summed, so they fail or pass on all ranks)
+    auto agree = [&](const std::string& err) {
+        if (!part) {
+            if (!err.empty()) throw std::runtime_error(err);
+            return;
+        }
+        double bad = err.empty() ? 0.0 : 1.0;
+        part->reduce_host(&bad, 1);
+        if (!err.empty()) throw std::runtime_error(err);
+        if (bad > 0) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite (on another rank's part)");
+    };
     if (!dense) {   // host only: postorder, parallel inside the large fronts
         std::vector<int> pos(n, -1);
-        for (int s = 0; s < nn; ++s)
-            if (mine(s) || tree.part[s] == -1) factor_front(C, s, pos, true);
+        std::string err;
+        try {
+            for (int s = 0; s < nn; ++s)
+                if (part ? mine(s) : true) factor_front(C, s, pos, true);
+        } catch (const std::exception& e) {
+            err = e.what();
+        }
+        agree(err);
+        if (part)
+            for (int s = 0; s < nn; ++s)
+                if (tree.part[s] == -1) factor_front(C, s, pos, true);
     } else {
         // tree-parallel: independent subtrees are OpenMP tasks (a front waits for its children),
         // each host front is factored by one thread; the large fronts near the root go to the
@@ -477,7 +503,7 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
                 }
 #pragma omp taskwait
         }
-        if (!err.empty()) throw std::runtime_error(err);
+        agree(err);
         if (part) {
             std::vector<int> pos(n, -1);
             for (int s = 0; s < nn; ++s)

@@ -94,6 +94,7 @@ struct DenseFrontBackend {
                         std::vector<double>& Linv, std::vector<double>& LBP, std::vector<double>& M,
                         std::vector<double>* U) = 0;
     virtual bool holds(int s) const = 0;   // s's update matrix is held by the backend
+    virtual void drop(int s) = 0;          // free s's held update matrix (a parent that skips it)
     int min_front = 1024;                  // fronts of at least this order go to the backend
     // set for the partitioned top fronts (PartFactor): called on the assembled device front
     // (f x f doubles) before it is factored -- the sum of the ranks' partial fronts

@@ -282,6 +282,7 @@ def geom_line(args, world, rank, local, dist):
     ctx = capi.Context(0 if args.same_device else local)
     sc, desc = geom_scene(args)
     comm, part = make_comm(pkg, ctx, args, world, rank)
+    lib_first_use_ms = ctx.warm_dense()   # one-time rocBLAS / rocSOLVER load, outside setup_ms
     t0 = time.time()
     bind_phases = {}
     g = capi.geom_from_scene(ctx, sc, comm, bind_phases)   # add_*_constraint + setup_ADMM (rows, weights)
@@ -303,7 +304,8 @@ def geom_line(args, world, rank, local, dist):
                        "setup_admm_cpp_ms": round(rt0.setup_ms, 1),
                        "order_factor_upload_ms": round(rt0.factor_ms, 1),
                        "first_solve_loop_ms": round(first_ms - rt0.factor_ms, 1),
-                       "warmup_solves_ms": round(warm_ms, 1), "warmup_solves": max(1, args.warmup) - 1}
+                       "warmup_solves_ms": round(warm_ms, 1), "warmup_solves": max(1, args.warmup) - 1,
+                       "library_first_use_ms": round(lib_first_use_ms, 1)}
     print(f"[bench] {args.config} setup {setup_ms / 1e3:.2f} s ({setup_breakdown})", file=sys.stderr, flush=True)
     barrier(dist, ctx)
     t0 = time.perf_counter()
@@ -606,9 +608,13 @@ def main():
     solver = capi.solver_from_scene(ctx, sc, comm)
     if args.lq_stats:
         os.environ["AA_LQ_STATS"] = "1"
+    # the process's one-time rocBLAS / rocSOLVER code-object load, timed on its own (it would
+    # otherwise sit inside the first factorization: seconds on a fresh box's cold page cache)
+    lib_first_use_ms = ctx.warm_dense()
     t0 = time.time()
     solver.initialize(capi.settings_from_scene(sc))
     setup_ms = (time.time() - t0) * 1e3
+    setup_phases = solver.setup_phases()
     if os.environ.get("AA_DUMP_MAPS"):   # diagnostics: library map to resolve a crash's frames
         with open("/proc/self/maps") as fi, open(os.environ["AA_DUMP_MAPS"], "w") as fo:
             fo.write(fi.read())
@@ -737,7 +743,12 @@ def main():
                        "admm_iters_per_step": args.iters, "anderson_m": sc.aa_m,
                        "parallelism": (f"mesh-partitioned{world} ({part})" if comm is not None else f"replicas{world}"),
                        "global_solve": "supernodal direct", "nnz_factor": rt.nnz_factor,
-                       "setup_ms": round(setup_ms, 1)},
+                       "setup_ms": round(setup_ms, 1),
+                       # initialize()'s phases (Solver.cpp:373-498; their sum vs setup_ms: the binding's
+                       # own overhead) and, outside setup_ms, the process's one-time library load
+                       "setup_breakdown": {"phases_ms": setup_phases,
+                                           "phases_sum_ms": round(sum(setup_phases.values()), 1),
+                                           "library_first_use_ms": round(lib_first_use_ms, 1)}},
             "iters_executed": int(iters_all),
             # Anderson rejects in the timed steps (each re-runs a one-set solve: SURVEY App. B.11)
             "anderson_rejects": rejects,

@@ -79,6 +79,13 @@ int aa_ctx_synchronize(aa_ctx ctx);
 /* Measurement hook (no reference counterpart): GB/s of a 16-B-per-lane streaming read of `bytes`
  * on the context's stream -- the measured HBM read ceiling bench.py reports beside the spec. */
 int aa_ctx_bench_read(aa_ctx ctx, long long bytes, double* gbps);
+/* One-time library load, made explicit (no reference counterpart): the first rocBLAS / rocSOLVER
+ * calls of a process load their code objects (seconds on a fresh box with a cold page cache),
+ * which would otherwise land inside the first aa_elastic_initialize / aa_geom_setup that factors
+ * a front on the GPU (SolverCommon / Solver.cpp:414-482 factor step). Runs the dense-front
+ * backend once on a synthetic front of the smallest GPU order; *ms = its wall time (0 when
+ * already warm or AA_DENSE_GPU=0). */
+int aa_ctx_warm_dense(aa_ctx ctx, double* ms);
 
 /* ---- admm::Solver ------------------------------------------------------------------ */
 int aa_lame_from_young(double youngs, double poisson, aa_lame* out);    /* Lame(k, v)        */
@@ -184,6 +191,10 @@ int aa_elastic_kernel_stats(aa_elastic h, const char* name, double* avg_ms, doub
  * iteration for every busy lane of a wave), out[102] queue refills, out[103] waves. Writes
  * min(cap, 104) counters into *count. */
 int aa_elastic_local_stats(aa_elastic h, long long* out, int cap, int reset, int* count);
+/* Wall-clock phases of the last aa_elastic_initialize (Solver::initialize, Solver.cpp:373-498):
+ * names '\n'-separated into names[0..names_cap) (NUL-terminated), milliseconds into
+ * ms[0..cap); *count = number of phases. */
+int aa_elastic_setup_phases(aa_elastic h, char* names, int names_cap, double* ms, int cap, int* count);
 
 /* ==== Geometry: ALMGeometrySolver<3> + Constraint<3> (bldeng/AA-ADMM Geometry/) ============= */
 typedef struct aa_geom_s* aa_geom;        /* one ALMGeometrySolver<3> instance             */

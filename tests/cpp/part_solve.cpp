@@ -271,5 +271,51 @@ int main(int argc, char** argv) {
                     P, (int)dense, n, n - T.top_beg, ntop, F.nnz_L, rmax / bmax, emax / xmax, tdiff, top_rel, ok ? "OK" : "FAIL");
         if (!ok) ++fails;
     }
+    // a matrix that is not positive definite in ONE part only (one node's diagonal negated): the
+    // rank owning it fails in its own subtrees, before the first top front's sum -- every rank
+    // must still throw (aa::multifrontal_cholesky agrees on the own-part outcome first) instead
+    // of the others waiting forever in the top front's all-reduce
+    for (const int P : {2, 4}) {
+        aa::NdTree T = aa::nested_dissection(n, xyz.data(), aptr, aj, 8, 0, P, true, 0);
+        std::vector<int> inv(n);
+        for (int q = 0; q < n; ++q) inv[T.perm[q]] = q;
+        aa::CsrMatrix A;
+        A.n = n;
+        A.ptr.assign(n + 1, 0);
+        const int bad = T.part_beg[P - 1] + (T.part_end[P - 1] - T.part_beg[P - 1]) / 2;   // inside the last part
+        for (int q = 0; q < n; ++q) {
+            std::vector<std::pair<int, double>> r;
+            for (auto& e : rows[T.perm[q]]) r.push_back({inv[e.first], e.second});
+            std::sort(r.begin(), r.end());
+            for (size_t k = 0; k < r.size();) {
+                size_t k2 = k;
+                double sum = 0;
+                while (k2 < r.size() && r[k2].first == r[k].first) sum += r[k2++].second;
+                A.col.push_back(r[k].first); A.val.push_back(q == bad && r[k].first == q ? -sum : sum);
+                k = k2;
+            }
+            A.ptr[q + 1] = (int)A.col.size();
+        }
+        SumBarrier bar(P);
+        std::vector<int> threw(P, 0);
+        std::vector<std::thread> th;
+        for (int pp = 0; pp < P; ++pp)
+            th.emplace_back([&, pp] {
+                aa::PartFactor pf;
+                pf.my_part = pp;
+                pf.first = pp == 0;
+                pf.reduce_host = [&](double* v, size_t m) { bar.reduce(v, m); };
+                try {
+                    aa::multifrontal_cholesky(A, T, nullptr, &pf);
+                } catch (const std::exception&) {
+                    threw[pp] = 1;
+                }
+            });
+        for (auto& t : th) t.join();   // a rank left waiting in a collective would hang here
+        int nthrew = 0;
+        for (int v : threw) nthrew += v;
+        std::printf("singular part: parts=%d ranks_threw=%d %s\n", P, nthrew, nthrew == P ? "SINGULAR_OK" : "SINGULAR_FAIL");
+        if (nthrew != P) ++fails;
+    }
     return fails ? 1 : 0;
 }

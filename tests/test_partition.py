@@ -29,7 +29,7 @@ def test_partitioned_solve_matches_unpartitioned(tmp_path):
                            env=dict(os.environ, OMP_NUM_THREADS="2"))
         print(r.stdout)
         assert r.returncode == 0, r.stdout + r.stderr
-        assert r.stdout.count("OK") == 10
+        assert r.stdout.count(" OK") == 10 and r.stdout.count("SINGULAR_OK") == 2
 
 
 WORKER = r"""

@@ -61,12 +61,15 @@ if a.ref:
             env["OMP_NUM_THREADS"] = str(a.threads)
         r = subprocess.run([os.path.join(REPO, "oracle", "_ref", "ref_elastic_x"), "s.bin", "o.bin"], cwd=tmp,
                            capture_output=True, text=True, env=env)
-        if r.returncode == 3:   # the reference threw inside step(): keep the finished steps, record why
-            abort = r.stderr.strip().splitlines()[-1]
+        if r.returncode == 3 or "line search" in r.stderr:   # the reference threw inside step() (exit 3, or
+            # std::terminate when the throw leaves an OpenMP region): keep the finished steps, record why
+            abort = f"reference aborted (rc {r.returncode}) in step {{}}: " + r.stderr.strip().splitlines()[-1]
         elif r.returncode:
             sys.exit(r.stderr[-2000:])
         steps = refio.read_ref_result(os.path.join(tmp, "o.bin"), sc.n_nodes)
     curves = [(s["prim"], s["comb"], s["reject"]) for s in steps]
+    if abort:
+        abort = abort.format(len(steps) + 1)
     per = [stats(s["comb"]) for s in steps]
     src = "reference (oracle/_ref/ref_elastic_x, compiled from admm_anderson_xzu's own sources), this container's CPU"
 else:

@@ -6,7 +6,7 @@
 #   /usr/local/graft/bin/gpurun -- bash tools/gpu.sh tests smoke "bench c4 20 5" "ab c4 ab/lib_head.so,ab/lib_new.so"
 #
 # steps (fields separated by spaces inside one quoted argument):
-#   tests [pytest args]            pytest -m gpu (log gpurun_out/pytest_gpu.log)
+#   tests [K+EXPR]                 pytest -m gpu [-k 'K EXPR'] (log gpurun_out/pytest_gpu.log)
 #   smoke                          __graft_entry__.smoke()
 #   bench CFG [STEPS] [WARMUP] [bench args]   full bench line -> gpurun_out/bench_CFG.log
 #   ab CFG LIB1,LIB2,.. [bench args]          short bench per build (AA_ADMM_LIB), phases printed;
@@ -43,8 +43,9 @@ for step in "$@"; do
   kind=$1; shift
   echo "== step [$step]"
   case $kind in
-    tests)
-      timeout -k 10 ${T_TESTS:-1200} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
+    tests)   # "tests" or "tests a+or+b" (a -k expression, '+' for spaces)
+      kx=(); [ -n "${1:-}" ] && kx=(-k "${1//+/ }")
+      timeout -k 10 ${T_TESTS:-1200} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${kx[@]}" \
         > gpurun_out/pytest_gpu.log 2>&1; rc=$?
       grep -E "FAILED|ERROR|passed|failed" gpurun_out/pytest_gpu.log | tail -8; fatal $rc tests ;;
     smoke)
