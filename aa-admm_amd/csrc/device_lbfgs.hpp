@@ -97,9 +97,18 @@ __device__ __forceinline__ double d9(const double* a, const double* b) {
 // compile-time constant, so s, y stay in registers (the ring buffer's dynamic indices put 864 B
 // per thread in scratch). The two-loop recursion visits the pairs in the same order (newest ->
 // oldest, then back), so the arithmetic is the reference's.
+// AA_LBFGS_RHO (default 1): each pair keeps rho = 1 / y.s, computed once when it is pushed, and
+// the two-loop recursion multiplies by it (alpha = rho s.d, beta = rho y.d) instead of dividing by
+// y.s at every use -- 2 divisions per iteration instead of 13 (a division is ~8 dependent fp64
+// instructions incl. a quarter-rate v_rcp_f64). mcloptlib divides (LBFGS.hpp:272-287); the
+// quotients differ from the products by at most an ulp, inside the L-BFGS's own 1e-6 gradient
+// tolerance (TetEnergyTerm.cpp:151-162), which is what the reference goldens are held to.
+#ifndef AA_LBFGS_RHO
+#define AA_LBFGS_RHO 1
+#endif
 struct HyperLbfgs {
     static constexpr int M = 6;
-    double s[M][9], yv[M][9], ysh[M], g[9], drt[9];
+    double s[M][9], yv[M][9], ysh[M], g[9], drt[9];   // ysh: y.s, or rho = 1 / y.s (AA_LBFGS_RHO)
     double fx, fpast, step;
     int k_it;
 
@@ -153,14 +162,14 @@ struct HyperLbfgs {
             s[0][i] = si; yv[0][i] = yi;
             ys += yi * si; yy += yi * yi;
         }
-        ysh[0] = ys;
+        ysh[0] = AA_LBFGS_RHO ? 1.0 / ys : ys;
 #pragma unroll
         for (int i = 0; i < 9; ++i) drt[i] = -g[i];
         const int bound = k_it < M ? k_it : M;
 #pragma unroll
         for (int q = 0; q < M; ++q) {
             if (q < bound) {
-                alpha[q] = d9(s[q], drt) / ysh[q];
+                alpha[q] = AA_LBFGS_RHO ? d9(s[q], drt) * ysh[q] : d9(s[q], drt) / ysh[q];
 #pragma unroll
                 for (int t = 0; t < 9; ++t) drt[t] -= alpha[q] * yv[q][t];
             }
@@ -170,7 +179,7 @@ struct HyperLbfgs {
 #pragma unroll
         for (int q = M - 1; q >= 0; --q) {
             if (q < bound) {
-                const double beta = d9(yv[q], drt) / ysh[q];
+                const double beta = AA_LBFGS_RHO ? d9(yv[q], drt) * ysh[q] : d9(yv[q], drt) / ysh[q];
 #pragma unroll
                 for (int t = 0; t < 9; ++t) drt[t] += (alpha[q] - beta) * s[q][t];
             }
@@ -247,7 +256,7 @@ struct HyperLbfgsLds {
             s[0][i] = si; yh[i * stride] = yi;
             ys += yi * si; yy += yi * yi;
         }
-        yh[9 * stride] = ys;
+        yh[9 * stride] = AA_LBFGS_RHO ? 1.0 / ys : ys;   // as HyperLbfgs
 #pragma unroll
         for (int i = 0; i < 9; ++i) drt[i] = -g[i];
         const int bound = k_it < M ? k_it : M;
@@ -256,7 +265,7 @@ struct HyperLbfgsLds {
         for (int q = 0; q < M; ++q) {
             if (q < bound) {
                 const double* yq = yl + (size_t)sl * E * stride;
-                alpha[q] = d9(s[q], drt) / yq[9 * stride];
+                alpha[q] = AA_LBFGS_RHO ? d9(s[q], drt) * yq[9 * stride] : d9(s[q], drt) / yq[9 * stride];
 #pragma unroll
                 for (int t = 0; t < 9; ++t) drt[t] -= alpha[q] * yq[t * stride];
             }
@@ -273,153 +282,11 @@ struct HyperLbfgsLds {
                 double yd = 0;
 #pragma unroll
                 for (int t = 0; t < 9; ++t) yd += yq[t * stride] * drt[t];
-                const double beta = yd / yq[9 * stride];
+                const double beta = AA_LBFGS_RHO ? yd * yq[9 * stride] : yd / yq[9 * stride];
 #pragma unroll
                 for (int t = 0; t < 9; ++t) drt[t] += (alpha[q] - beta) * s[q][t];
             }
             sl = sl == M - 1 ? 0 : sl + 1;
-        }
-        step = 1.0;
-        ++k_it;
-        return false;
-    }
-};
-
-// HyperLbfgs with the history split by age (the default of the work-queue kernel): the NR = 2
-// newest pairs in registers (a 2-slot shift register), the NL = 4 older ones in an LDS ring whose
-// head is the CALLER's trip count mod NL -- the same for every lane of the wave, because every
-// active lane pushes exactly one pair per trip (a lane that finishes pushes nothing and needs its
-// history no more; a lane that starts has no live pair and masks the stale ones by k_it, as the
-// register form does). So the LDS slot of pair q (2..5) is a wave-uniform offset, no per-lane
-// address arithmetic, no moves of the old pairs. The whole state then fits the 256 arch VGPRs:
-// the all-register form (HyperLbfgs) holds 402 registers, 146 of them AGPRs, and pays one
-// v_accvgpr_read per history dword per use plus the AGPR shift (≈ 500 of its ≈ 1 400 VALU
-// instructions per trip). LDS per lane: NL x 19 doubles (pairs (s_i, y_i) as 16-B
-// entries, then y.s), lane-interleaved so a wave's 64 lanes read 1 KB contiguous per
-// ds_read_b128; 152 KB per 256-lane block. The pair leaving the registers is written to the LDS
-// slot of the pair the push retires, at the START of the iteration (that pair is dead then), so its
-// two register slots hold the line search's xp / gp and no extra temporaries are live.
-// Same operands in the same order as HyperLbfgs: bit-identical.
-struct HyperLbfgsSplit {
-    static constexpr int M = 6, NR = 2, NL = 4;
-    double s[NR][9], yv[NR][9], ysh[NR], g[9], drt[9];
-    double fx, fpast, step;
-    int k_it;
-    double2* lp;   // this lane's (s_i, y_i) entries: slot k, i at lp[(k * 9 + i) * lanes]
-    double* lys;   // this lane's y.s: slot k at lys[k * lanes]
-    int lanes;
-
-    static constexpr size_t lds_bytes(int block) { return (size_t)NL * 19 * sizeof(double) * block; }
-    __device__ __forceinline__ void bind(void* base, int tid, int block) {
-        lanes = block;
-        lp = (double2*)base + tid;
-        lys = (double*)((double2*)base + (size_t)NL * 9 * block) + tid;
-    }
-
-    __device__ __forceinline__ bool start(int mat, double mu, double lambda, double k, double vol, const double* v,
-                                          double* x) {
-        fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
-        const double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
-        fpast = fx;
-        k_it = 1;
-        if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return true;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) drt[i] = -g[i];
-        step = 1.0 / sqrt(d9(drt, drt));
-        return false;
-    }
-
-    // head: the caller's trip count mod NL (wave-uniform): the LDS slot this call's push writes
-    __device__ __forceinline__ bool iterate(int mat, double mu, double lambda, double k, double vol, const double* v,
-                                            double* x, int* fail, int head) {
-        // the pair leaving the registers (q = 1 -> 2) replaces the retiring one (q = 5) in LDS
-        {
-            double2* w = lp + (size_t)head * 9 * lanes;
-#pragma unroll
-            for (int i = 0; i < 9; ++i) w[(size_t)i * lanes] = make_double2(s[1][i], yv[1][i]);
-            lys[(size_t)head * lanes] = ysh[1];
-        }
-        // register slot 1 holds xp / gp during the line search
-#pragma unroll
-        for (int i = 0; i < 9; ++i) { s[1][i] = x[i]; yv[1][i] = g[i]; }
-        {
-            const double fx_init = fx, dg_test = 1e-4 * d9(g, drt);
-            for (int it = 0; it < 2000; ++it) {
-#pragma unroll
-                for (int i = 0; i < 9; ++i) x[i] = s[1][i] + step * drt[i];
-                fx = hyper_eval(mat, mu, lambda, k, vol, v, x, g);
-                if (!(fx > fx_init + step * dg_test)) break;
-                if (step < 1e-20 || step > 1e20) { *fail = 1; return true; }
-                step *= 0.5;
-            }
-        }
-        const double xnorm = sqrt(d9(x, x)), gnorm = sqrt(d9(g, g));
-        if (gnorm <= 1e-6 * fmax(xnorm, 1.0)) return true;
-        if (fabs(fpast - fx) < 1e-16) return true;
-        fpast = fx;
-        if (k_it >= 100) return true;
-        double ns[9], ny[9], ys = 0, yy = 0;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            ns[i] = x[i] - s[1][i];
-            ny[i] = g[i] - yv[1][i];
-            ys += ny[i] * ns[i]; yy += ny[i] * ny[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 9; ++i) { s[1][i] = s[0][i]; yv[1][i] = yv[0][i]; s[0][i] = ns[i]; yv[0][i] = ny[i]; }
-        ysh[1] = ysh[0];
-        ysh[0] = ys;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) drt[i] = -g[i];
-        const int bound = k_it < M ? k_it : M;
-        double alpha[M];
-        // LDS slot of pair q (2..5): pushed (q - 2) trips ago
-        auto slot = [&](int q) { return (head + 2 * NL + 2 - q) % NL; };
-#pragma unroll
-        for (int q = 0; q < M; ++q) {
-            if (q < bound) {
-                if (q < NR) {
-                    alpha[q] = d9(s[q], drt) / ysh[q];
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) drt[t] -= alpha[q] * yv[q][t];
-                } else {
-                    const double2* e = lp + (size_t)slot(q) * 9 * lanes;
-                    double2 sy[9];
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) sy[t] = e[(size_t)t * lanes];
-                    const double yq = lys[(size_t)slot(q) * lanes];
-                    double d = 0;
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) d += sy[t].x * drt[t];
-                    alpha[q] = d / yq;
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) drt[t] -= alpha[q] * sy[t].y;
-                }
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < 9; ++t) drt[t] *= ys / yy;
-#pragma unroll
-        for (int q = M - 1; q >= 0; --q) {
-            if (q < bound) {
-                if (q < NR) {
-                    const double beta = d9(yv[q], drt) / ysh[q];
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) drt[t] += (alpha[q] - beta) * s[q][t];
-                } else {
-                    const double2* e = lp + (size_t)slot(q) * 9 * lanes;
-                    double2 sy[9];
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) sy[t] = e[(size_t)t * lanes];
-                    const double yq = lys[(size_t)slot(q) * lanes];
-                    double d = 0;
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) d += sy[t].y * drt[t];
-                    const double beta = d / yq;
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) drt[t] += (alpha[q] - beta) * sy[t].x;
-                }
-            }
         }
         step = 1.0;
         ++k_it;

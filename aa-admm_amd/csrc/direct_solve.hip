@@ -1222,6 +1222,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     // whatever their count, so it takes fewer, taller ones (measured)
     const int min_sub = ms ? std::atoi(ms) : (comm_ ? std::max(32, 256 / comm_->size()) : 256);
     constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
+    constexpr long long kLdsMax = 160 * 1024;   // the fused kernels' LDS attribute (build, below)
     auto roots_at = [&](int H) {
         std::vector<int> r;
         for (int sn = 0; sn < nn_; ++sn)
@@ -1240,7 +1241,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         bool ok = true;
         for (int rt : r) {
             std::vector<long long> lf(H + 1, 0), lb(H + 1, 0), nodes_at(H + 1, 0);
-            for (int v : collect(rt)) {
+            const std::vector<int> all = collect(rt);
+            // the subtree's node records staged in LDS beside a level's vectors (two copies of
+            // each supernode: forward and backward offsets), 16-B aligned after the vectors
+            const long long rec = 16 + 2LL * (long long)all.size() * (long long)sizeof(SubNode);
+            for (int v : all) {
                 lf[F.height[v]] += 24LL * KS * p[v];
                 long long slots = 0;
                 for (int sg = 0; sg < (p[v] + nb[v] + kSubSegRows - 1) / kSubSegRows; ++sg)
@@ -1250,7 +1255,9 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 if (p[v] + nb[v] > kMaxItemRow) ok = false;
             }
             for (int h = 0; h <= H; ++h)
-                if (lf[h] > kSubLds || lb[h] > kSubLdsB || nodes_at[h] > kMaxItemRow) ok = false;
+                if (lf[h] > kSubLds || lb[h] > kSubLdsB || nodes_at[h] > kMaxItemRow || lf[h] + rec > kLdsMax ||
+                    lb[h] + rec > kLdsMax)
+                    ok = false;
             if (!ok) break;
         }
         if (ok) { cut_height_ = H; break; }
@@ -1800,6 +1807,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     Y_.alloc(3 * KS * (size_t)n_);
     U_.alloc(std::max<long long>(KS * uo, 3));
     // (LDS figures above are per 3 columns; a 6-column solve needs twice as much; + the staged nodes)
+    if (std::max(sub_lds_bytes(KS, true), sub_lds_bytes(KS, false)) > 160 * 1024)
+        throw Error(ERR_STATE, "DirectSolver: fused subtree exceeds 160 KiB of LDS (cut-height budget)");
     if (std::max(sub_lds_bytes(KS, true), sub_lds_bytes(KS, false)) > 64 * 1024)
         for (const void* k : {(const void*)k_fwd_sub<256, 3, false>, (const void*)k_fwd_sub<512, 3, false>, (const void*)k_fwd_sub<1024, 3, false>,
                               (const void*)k_bwd_sub<256, 3, false>, (const void*)k_bwd_sub<512, 3, false>, (const void*)k_bwd_sub<1024, 3, false>,

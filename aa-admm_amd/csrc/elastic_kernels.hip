@@ -189,14 +189,12 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
 // the optional rhs slots written) takes the next one from a queue (one atomic per wave and
 // refill, ballot-aggregated) and lanes advance one outer L-BFGS iteration per trip. Each
 // element's arithmetic is unchanged, so the results are bit-identical to k_local_z.
-// HV: where the L-BFGS history lives -- LQ_HIST_SPLIT (the default): the two newest pairs in
-// registers, the four older ones in an LDS ring with a wave-uniform head (dev::HyperLbfgsSplit,
-// dynamic LDS kLqSplitBytes); LQ_HIST_REGS: all in registers (dev::HyperLbfgs, AA_LQ_HIST=0);
-// LQ_HIST_YLDS: the y half in LDS (dev::HyperLbfgsLds, kLqLdsBytes, AA_LQ_LDS=1). Bit-identical.
+// HV: where the L-BFGS history lives -- LQ_HIST_REGS (default): all of it in registers
+// (dev::HyperLbfgs); LQ_HIST_YLDS: the y half in LDS (dev::HyperLbfgsLds, dynamic LDS kLqLdsBytes,
+// AA_LQ_LDS=1; measured slower). Bit-identical.
 template <int HV>
 struct LqHist {
-    using type = typename std::conditional<HV == LQ_HIST_SPLIT, dev::HyperLbfgsSplit,
-                 typename std::conditional<HV == LQ_HIST_YLDS, dev::HyperLbfgsLds, dev::HyperLbfgs>::type>::type;
+    using type = typename std::conditional<HV == LQ_HIST_YLDS, dev::HyperLbfgsLds, dev::HyperLbfgs>::type;
 };
 
 template <int NV, int HV>
@@ -218,13 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     if constexpr (HV == LQ_HIST_YLDS) {
         extern __shared__ double lq_hist[];
         L.bind(lq_hist + threadIdx.x, kBlock);
-    } else if constexpr (HV == LQ_HIST_SPLIT) {
-        extern __shared__ double lq_hist[];
-        L.bind(lq_hist, threadIdx.x, kBlock);
     }
-    // every active lane pushes one L-BFGS pair per trip: the split history's LDS ring head is the
-    // trip count mod NL, uniform over the wave
-    int ring = 0;
     double v[D], x[D];
     double vol = 0;
     int e = -1, fail = 0;
@@ -284,12 +276,11 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
                 }
             }
         }
-        if (active && L.iterate(g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail, __builtin_amdgcn_readfirstlane(ring))) {
+        if (active && L.iterate(g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail)) {
             active = false;
             pending = true;
             if (stats) atomicAdd(&hist[min(L.k_it, 100)], 1u);
         }
-        ring = (ring + 1) & 3;
     }
     if (stats) {
         if (lane == 0) {
@@ -330,7 +321,6 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hqa(GroupDev g, const double
     constexpr int D = 3 * (NV - 1), NC = NV - 1;
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
-    static_assert(HV != LQ_HIST_SPLIT, "the lookahead queue keeps no uniform trip count per push");
     typename LqHist<HV>::type L;
     if constexpr (HV == LQ_HIST_YLDS) {
         extern __shared__ double lq_hist[];
@@ -1301,17 +1291,13 @@ LocalQueue make_local_queue(int device, int* counter) {
     const char* r = std::getenv("AA_LQ_REFILL");
     const char* ah = std::getenv("AA_LQ_AHEAD");
     const char* lh = std::getenv("AA_LQ_LDS");
-    const char* hs = std::getenv("AA_LQ_HIST");
     q.ahead = ah && ah[0] == '1';   // opt-in: measured slower on C4
-    // history placement: split (default), all registers (AA_LQ_HIST=0), y half in LDS (AA_LQ_LDS=1)
-    q.hist = (lh && lh[0] == '1') ? LQ_HIST_YLDS : (hs && hs[0] == '0') ? LQ_HIST_REGS : LQ_HIST_SPLIT;
-    if (q.ahead && q.hist == LQ_HIST_SPLIT) q.hist = LQ_HIST_REGS;
+    q.hist = (lh && lh[0] == '1') ? LQ_HIST_YLDS : LQ_HIST_REGS;   // opt-in: no faster on C4
     const void* kq = q.ahead ? (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hqa<4, LQ_HIST_YLDS>
                                                        : (const void*)k_local_z_hqa<4, LQ_HIST_REGS>)
-                             : (q.hist == LQ_HIST_YLDS  ? (const void*)k_local_z_hq<4, LQ_HIST_YLDS>
-                                : q.hist == LQ_HIST_SPLIT ? (const void*)k_local_z_hq<4, LQ_HIST_SPLIT>
-                                                          : (const void*)k_local_z_hq<4, LQ_HIST_REGS>);
-    const size_t lds = q.hist == LQ_HIST_YLDS ? kLqLdsBytes : q.hist == LQ_HIST_SPLIT ? kLqSplitBytes : 0;
+                             : (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hq<4, LQ_HIST_YLDS>
+                                                       : (const void*)k_local_z_hq<4, LQ_HIST_REGS>);
+    const size_t lds = q.hist == LQ_HIST_YLDS ? kLqLdsBytes : 0;
     q.lds_bytes = lds;
     if (lds) AA_HIP(hipFuncSetAttribute(kq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kq, kBlock, lds));
@@ -1338,9 +1324,6 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
         else if (queue->ahead)
             hipLaunchKernelGGL((k_local_z_hqa<4, LQ_HIST_REGS>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
                                ctrl, queue->counter, refill, queue->margin, queue->stats);
-        else if (queue->hist == LQ_HIST_SPLIT)
-            hipLaunchKernelGGL((k_local_z_hq<4, LQ_HIST_SPLIT>), grid, dim3(kBlock), lds, s, g, xfull, u, z, y, nf, mode,
-                               ctrl, queue->counter, refill, queue->stats);
         else if (queue->hist == LQ_HIST_YLDS)
             hipLaunchKernelGGL((k_local_z_hq<4, LQ_HIST_YLDS>), grid, dim3(kBlock), lds, s, g, xfull, u, z, y, nf, mode,
                                ctrl, queue->counter, refill, queue->stats);

@@ -76,7 +76,7 @@ struct LocalQueue {
     int* counter = nullptr;
     int resident = 0, refill = 60, margin = 0;
     bool ahead = false;  // AA_LQ_AHEAD=1: k_local_z_hqa (one-element lookahead per lane)
-    int hist = 2;        // LqHistory: where the L-BFGS history lives (AA_LQ_HIST / AA_LQ_LDS)
+    int hist = 0;        // LqHistory: where the L-BFGS history lives (AA_LQ_LDS=1: y half in LDS)
     size_t lds_bytes = 0;
     // optional diagnostics (AA_LQ_STATS=1): [0..100] elements by L-BFGS iterations (0 = the start
     // point passed the gradient test), [101] trips, [102] refills, [103] waves; summed over launches
@@ -84,8 +84,7 @@ struct LocalQueue {
 };
 constexpr int kLqStats = 104;
 constexpr size_t kLqLdsBytes = sizeof(double) * 6 * 10 * kBlock;   // HyperLbfgsLds ring, one block
-constexpr size_t kLqSplitBytes = sizeof(double) * 4 * 19 * kBlock;  // HyperLbfgsSplit ring, one block
-enum LqHistory { LQ_HIST_REGS = 0, LQ_HIST_YLDS = 1, LQ_HIST_SPLIT = 2 };
+enum LqHistory { LQ_HIST_REGS = 0, LQ_HIST_YLDS = 1 };
 LocalQueue make_local_queue(int device, int* counter);
 // z = prox(P x + u/w); prim partials; optional y = w(w z + c - u). gate: !done (and reject for REDO)
 // queue given: hyperelastic groups without partials run as a persistent work queue

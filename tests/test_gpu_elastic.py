@@ -229,27 +229,19 @@ def test_gpu_streamed_levels_bit_identical(pkg, ctx, monkeypatch, capfd, knobs):
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
 
 
-@pytest.mark.parametrize("variant", [{"AA_LQ_LDS": "1"}, {}])
-@pytest.mark.parametrize("builder", [
-    lambda: scenes.tet_drop(12, 4, 6, iters=30, n_steps=2),
-    # StVK + a 64k-tet NeoHookean drop: thousands of waves, lanes at every L-BFGS depth
-    lambda: scenes.tet_drop(6, 3, 3, material=scenes.STVK, iters=20, n_steps=1),
-    lambda: scenes.tet_drop(40, 16, 20, iters=6, n_steps=1),
-])
-def test_gpu_local_queue_history_variants_bit_identical(pkg, ctx, monkeypatch, variant, builder):
-    """The NeoHookean / StVK local step with each placement of the L-BFGS history against the
-    all-register history (AA_LQ_HIST=0): the default split (two newest pairs in registers, four
-    older in an LDS ring with a wave-uniform head, dev::HyperLbfgsSplit), the y half in LDS
-    (AA_LQ_LDS=1): the same operations in the same order
-    (TetEnergyTerm.cpp:151-162 via mcloptlib LBFGS.hpp:205-305), so bit-identical trajectories."""
-    sc = builder()
-    monkeypatch.setenv("AA_LQ_HIST", "0")
+@pytest.mark.parametrize("ahead", ["0", "1"])
+def test_gpu_local_queue_lds_history_bit_identical(pkg, ctx, monkeypatch, ahead):
+    """The NeoHookean local step with the L-BFGS history's y half in LDS (dev::HyperLbfgsLds, a
+    ring per lane) against the all-register history (AA_LQ_LDS=0), with and without the lookahead
+    queue: the same operations in the same order (TetEnergyTerm.cpp:151-162 via mcloptlib
+    LBFGS.hpp:205-305), so bit-identical trajectories."""
+    sc = scenes.tet_drop(12, 4, 6, iters=30, n_steps=2)
+    monkeypatch.setenv("AA_LQ_AHEAD", ahead)
+    monkeypatch.setenv("AA_LQ_LDS", "0")
     reg, _ = pkg.capi.run_scene(ctx, sc)
-    monkeypatch.delenv("AA_LQ_HIST")
-    for k, v in variant.items():
-        monkeypatch.setenv(k, v)
-    got, _ = pkg.capi.run_scene(ctx, sc)
-    for a, b in zip(reg, got):
+    monkeypatch.setenv("AA_LQ_LDS", "1")
+    lds, _ = pkg.capi.run_scene(ctx, sc)
+    for a, b in zip(reg, lds):
         for k in ("prim", "comb", "reject", "x", "v"):
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
 

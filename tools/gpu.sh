@@ -109,7 +109,7 @@ PY
       tail -3 gpurun_out/eps_$tag.log; fatal $rc "eps $tag" ;;
     geps)
       cfg=$1; n=$2; tag=$3
-      timeout -k 10 ${T_EPS:-900} python -u tools/ref_geom_curve.py --gpu --config $cfg --n $n --out gpurun_out/geps_$tag.json \
+      timeout -k 10 ${T_EPS:-900} python -u tools/ref_geom_curve.py --gpu --config $cfg --nx $n --iters ${ITERS:-2000} --out gpurun_out/geps_$tag.json \
         > gpurun_out/geps_$tag.log 2>&1; rc=$?
       tail -3 gpurun_out/geps_$tag.log; fatal $rc "geps $tag" ;;
     *) echo "unknown step [$step]"; exit 2 ;;
