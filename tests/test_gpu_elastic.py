@@ -229,6 +229,27 @@ def test_gpu_streamed_levels_bit_identical(pkg, ctx, monkeypatch, capfd, knobs):
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
 
 
+@pytest.mark.parametrize("knob", [("AA_SOLVE_PACKED", "0", "1"), ("AA_FACTOR_NT", "0", "1"),
+                                  ("AA_FACTOR_NT_ROWS", "0", "1")])
+def test_gpu_packed_tiles_and_nt_loads_bit_identical(pkg, ctx, monkeypatch, knob):
+    """The packed split-K tiles (every tile's factor entries copied at setup into the order its
+    waves stream them; narrow backward blocks of <= 64 columns) against the strided tiles
+    (AA_SOLVE_PACKED=0), and non-temporal against plain factor loads (AA_FACTOR_NT /
+    AA_FACTOR_NT_ROWS): the same tiles, partials and sums in the same order, so bit-identical.
+    Tile-heavy knobs make most supernodes split-K tiled, with narrow (<= 64-column) blocks."""
+    sc = scenes.tet_drop(40, 16, 20, iters=10, n_steps=2)
+    for k, v in {"AA_SOLVE_WAVEP": "16", "AA_SOLVE_WAVER": "32", "AA_SOLVE_TILE": "64"}.items():
+        monkeypatch.setenv(k, v)
+    name, a, b = knob
+    monkeypatch.setenv(name, a)
+    ref, _ = pkg.capi.run_scene(ctx, sc)
+    monkeypatch.setenv(name, b)
+    got, _ = pkg.capi.run_scene(ctx, sc)
+    for x, y in zip(ref, got):
+        for k in ("prim", "comb", "reject", "x", "v"):
+            assert np.array_equal(np.asarray(x[k]), np.asarray(y[k])), (name, k)
+
+
 @pytest.mark.parametrize("ahead", ["0", "1"])
 def test_gpu_local_queue_lds_history_bit_identical(pkg, ctx, monkeypatch, ahead):
     """The NeoHookean local step with the L-BFGS history's y half in LDS (dev::HyperLbfgsLds, a
@@ -387,4 +408,59 @@ def test_gpu_obstacles_after_initialize(pkg, ctx):
     s.add_obstacle(scenes.OBS_FLOOR, [y0 + 0.2])
     s.step()
     assert s.x[:, 1].min() > y0 + 0.05
+    s.close()
+
+
+def test_gpu_c4_eps_regime_matches_reference(pkg, ctx):
+    """The C4 recipe's run-to-epsilon regime pinned to the reference itself:
+    tests/golden/eps_drop40_ref.npz holds the reference's per-iteration curves of the 64k-tet
+    drop (make_tet_blocks(40,16,20), NeoHookean, z-AA m=6) over 500 ADMM iterations per step with
+    no early stop (tools/elastic_eps_curves.py --ref, oracle/_ref/ref_elastic_x from
+    admm_anderson_xzu/src/Solver.cpp:122-251); the reference throws mcloptlib's line-search error
+    (LBFGS.hpp:192-199) in step 9, so 8 steps are recorded. Per step, the GPU solver must reach
+    comb <= r comb_0 (r = 1e-4, 1e-6, 1e-8) at the same iteration within EPS_ITER_TOL, or miss it
+    too -- where the curve crosses r cleanly (both floors below r / 10: a curve that levels off
+    near r crosses it at an ill-conditioned iteration, e.g. step 7's 1e-6 at 42 vs 73 with floors
+    of 5.2e-7 vs 6.3e-7) -- and its stall floor min(comb)/comb_0 must lie within a factor
+    EPS_FLOOR_FAC of the reference's: steps 1-5 reach 1e-8 in both, the block mid-fall (steps 6-8)
+    stalls above it in both. Step 9 must then raise the same line-search error on the GPU."""
+    import os
+    import sys
+    from golden_io import GOLDEN
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import scene_digest
+    EPS_ITER_TOL, EPS_FLOOR_FAC = 2, 3.0
+    ref = np.load(os.path.join(GOLDEN, "eps_drop40_ref.npz"))
+    nrec = ref["nrec"]
+    sc = scenes.tet_drop(40, 16, 20, iters=int(ref["cap"]), n_steps=12)
+    assert np.array_equal(scene_digest(sc), ref["digest"]), "regenerated scene differs from the fixture's"
+    s = pkg.capi.solver_from_scene(ctx, sc)
+    s.initialize(pkg.capi.settings_from_scene(sc))
+
+    def first(c, r):
+        h = np.nonzero(c <= r * c[0])[0]
+        return int(h[0]) + 1 if len(h) else None
+
+    o = 0
+    for k, n in enumerate(nrec):
+        s.step()
+        got = np.asarray(s.history()["comb"])
+        want = ref["comb"][o:o + n]
+        o += n
+        assert len(got) == len(want) == int(ref["cap"]), (k, len(got), len(want))
+        fg, fr = got.min() / got[0], want.min() / want[0]
+        for r in (1e-4, 1e-6, 1e-8):
+            a, b = first(got, r), first(want, r)
+            if max(fg, fr) < r / 10:   # a clean crossing in both
+                assert a is not None and b is not None and abs(a - b) <= EPS_ITER_TOL, (k + 1, r, a, b)
+            elif min(fg, fr) > r * 10:   # clearly stalled above r in both
+                assert a is None and b is None, (k + 1, r, a, b)
+        # floors below 1e-10 comb_0 are rounding noise of the residual itself: compared as "converged"
+        if max(fg, fr) > 1e-10:
+            assert fr / EPS_FLOOR_FAC <= fg <= fr * EPS_FLOOR_FAC, (k + 1, fg, fr)
+        else:
+            assert min(fg, fr) < 1e-10 and max(fg, fr) < 1e-9, (k + 1, fg, fr)
+    if "step 9" in str(ref["abort"]):   # the reference's abort, reproduced
+        with pytest.raises(pkg.capi.AAError, match="line search"):
+            s.step()
     s.close()
