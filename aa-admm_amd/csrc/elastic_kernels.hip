@@ -945,6 +945,118 @@ __global__ __launch_bounds__(kBlock) void k_aa_reduce(Seg2 G, const double* __re
     }
 }
 
+// Wide windows (m > 16, the C5 wire mesh's m = 20): the same partial sums, column-parallel. The
+// row-parallel form above keeps 2 + 2 MM accumulators and the MM history loads of an entry in every
+// thread's registers (221 VGPRs at MM = 32: 2 waves per SIMD, loads serialised on their latency).
+// Here a block walks a contiguous row range in tiles of kAaTile rows: it first stages the tile's
+// F_i = G_i - cur_i and dF_j,i + F_i in LDS (and accumulates |dF_j|^2, dF_j.F), then each wave
+// takes columns c = wave, wave + 4, ... of the history and streams them coalesced over the tile --
+// kAaTile / 64 independent loads per lane -- against the staged vectors: two accumulators per column
+// the wave owns. The block partials keep the row-parallel kernel's layout and are summed in block
+// order by k_aa_solve, so the reduction is as deterministic; the partial sums group differently, so
+// the products differ from the row-parallel kernel's by rounding only (Anderson's least-squares
+// coefficients, AndersonAcceleration.h:154-211, are held to the geometry goldens' tolerances).
+constexpr int kAaTile = 512;
+template <int MM>
+__global__ __launch_bounds__(kBlock) void k_aa_reduce_cols(Seg2 G, const double* __restrict__ cur, long long eff,
+                                                           double* __restrict__ dF, double* __restrict__ dG, Ctrl* ctrl,
+                                                           double* red, Seg2 copy_to, const double* comb_a,
+                                                           const double* comb_b, int comb_nb, double* hist_prim,
+                                                           double* hist_comb, int* hist_rej, AAMask mask) {
+    if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
+    constexpr int NVAL = 2 + 2 * MM, NW = kBlock / 64, QC = (MM + NW - 1) / NW, RL = kAaTile / 64;
+    __shared__ double sm[NW][NVAL];
+    __shared__ double sdf[kAaTile], sf[kAaTile];
+    if (comb_a) {   // as k_aa_reduce
+        __shared__ double sc[kBlock / 64];
+        const double comb = block_sum_all(comb_a, comb_nb, sc) + block_sum_all(comb_b, comb_nb, sc);
+        const bool brk = comb < kCombEps;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            ctrl->comb = comb;
+            ctrl->iters_run += 1;
+            if (brk) ctrl->done = 1;
+            else if (record_iter(ctrl, hist_prim, hist_comb, hist_rej, comb)) ctrl->eps_hit = 1;
+        }
+        if (brk) return;
+    }
+    const long long dim = G.na + G.nb;
+    const int iter = ctrl->aa_iter, col = ctrl->aa_col, m = ctrl->aa_m;
+    const int mk = iter < m ? iter : m;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // this block's rows: a contiguous range, whole tiles
+    const long long per = ((dim + gridDim.x - 1) / gridDim.x + kAaTile - 1) / kAaTile * kAaTile;
+    const long long r0 = (long long)blockIdx.x * per, r1 = r0 + per < dim ? r0 + per : dim;
+    double a0 = 0, a1 = 0, ac[QC], bc[QC];
+#pragma unroll
+    for (int q = 0; q < QC; ++q) { ac[q] = 0; bc[q] = 0; }
+    for (long long t0 = r0; t0 < r1; t0 += kAaTile) {
+        for (int k = threadIdx.x; k < kAaTile; k += kBlock) {
+            const long long i = t0 + k;
+            double dfj = 0, f = 0;
+            if (i < r1) {
+                const double g = seg_get(G, i);
+                if (copy_to.a) seg_set(copy_to, i, g);
+                bool in = iter != 0 && i < eff;
+                if (in && i >= G.na) {
+                    const long long j = i - G.na;
+                    in = (j >= mask.lo1 && j < mask.hi1) || (j >= mask.lo2 && j < mask.hi2);
+                }
+                if (in) {
+                    f = g - cur[i];
+                    dfj = ld_h(dF + (size_t)col * eff + i) + f;
+                    a0 += dfj * dfj;
+                    a1 += dfj * f;
+                }
+            }
+            sdf[k] = dfj;
+            sf[k] = f;
+        }
+        __syncthreads();
+        if (iter != 0) {
+#pragma unroll
+            for (int q = 0; q < QC; ++q) {
+                const int c = wid + NW * q;
+                if (c < mk && c != col) {   // wave-uniform
+                    const double* src = dF + (size_t)c * eff;
+                    double d[RL];
+#pragma unroll
+                    for (int j = 0; j < RL; ++j) {
+                        const long long i = t0 + lane + 64 * j;
+                        d[j] = i < r1 && i < eff ? ld_h(src + i) : 0.0;
+                    }
+#pragma unroll
+                    for (int j = 0; j < RL; ++j) {
+                        ac[q] += sdf[lane + 64 * j] * d[j];
+                        bc[q] += d[j] * sf[lane + 64 * j];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (iter == 0) return;
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    if (lane == 0) { sm[wid][0] = a0; sm[wid][1] = a1; }
+#pragma unroll
+    for (int q = 0; q < QC; ++q) {
+        const double x = wave_sum(ac[q]), y = wave_sum(bc[q]);
+        const int c = wid + NW * q;
+        if (lane == 0 && c < MM) {
+            for (int w = 0; w < NW; ++w)
+                if (w != wid) { sm[w][2 + c] = 0; sm[w][2 + MM + c] = 0; }
+            sm[wid][2 + c] = x;
+            sm[wid][2 + MM + c] = y;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < NVAL) {
+        double s2 = 0;
+        for (int w = 0; w < NW; ++w) s2 += sm[w][threadIdx.x];
+        red[(size_t)blockIdx.x * NVAL + threadIdx.x] = s2;
+    }
+}
+
 // Eigen CompleteOrthogonalDecomposition::solve of the small normal equations, block-cooperative:
 // column-pivoted Householder QR with LAPACK norm downdating (Eigen/src/QR/ColPivHouseholderQR.h
 // :482-579), rank = #|R_ii| > eps*n*|maxpivot| (:255-263), RZ step + minimum-norm solve
@@ -1484,6 +1596,11 @@ int aa_reduce_blocks(long long dim) {   // more partials only pay off on large v
 
 static int mm_bucket(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : 32); }
 
+static bool aa_cols() {
+    static const bool on = !(std::getenv("AA_AA_COLS") && std::getenv("AA_AA_COLS")[0] == '0');
+    return on;
+}
+
 void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, double* red,
                       int nblocks, Seg2 copy_to, int m, hipStream_t s, const double* comb_a, const double* comb_b,
                       int comb_nb, double* hist_prim, double* hist_comb, int* hist_rej, AAMask mask) {
@@ -1491,7 +1608,10 @@ void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, doub
     switch (mm_bucket(m)) {
         case 8: hipLaunchKernelGGL(k_aa_reduce<8>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
         case 16: hipLaunchKernelGGL(k_aa_reduce<16>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
-        default: hipLaunchKernelGGL(k_aa_reduce<32>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
+        default:   // m > 16: column-parallel (AA_AA_COLS=0: the row-parallel kernel)
+            if (aa_cols()) hipLaunchKernelGGL(k_aa_reduce_cols<32>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS);
+            else hipLaunchKernelGGL(k_aa_reduce<32>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS);
+            break;
     }
 #undef AA_RED_ARGS
     AA_CHECK_LAUNCH();
