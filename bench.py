@@ -555,7 +555,12 @@ def run_to_eps(solver, args, state0):
            "not_reached_note": (None if len(hit) == len(steps) else
                                 f"not reached in {len(steps) - len(hit)}/{len(steps)} steps with cap {args.eps_cap}"),
            "clock": "device wall_clock64 from the step's start (prologue included) to the end of the iteration "
-                    "reaching comb <= eps_rel * comb_0", "per_step": steps}
+                    "reaching comb <= eps_rel * comb_0",
+           "reference_regime": ("pinned on the 64k-tet drop of the same recipe (profiles/r4_c4_eps_ref_drop40.json vs "
+                                "r4_c4_eps_gpu_drop40.json, test_gpu_c4_eps_regime_matches_reference): the reference "
+                                "reaches 1e-8 comb_0 in steps 1-5 only, stalls at 2e-7 / 6e-7 / 2e-5 comb_0 in steps 6-8 "
+                                "and aborts in step 9 (LBFGS.hpp:192-199) -- the GPU at the same iterations and floors"),
+           "per_step": steps}
     for e in (1e-4, 1e-6):
         k = f"{e:g}"
         v = [s[k]["ms"] if s[k] is not None else None for s in steps]

@@ -15,7 +15,7 @@
 #                                  bit-for-bit with the first (scenes: drop40 c4small cloth pq wire)
 #   pmc CFG TAG COUNTER[,COUNTER]  one rocprofv3 --pmc pass per comma group (graph mode)
 #   prof CFG TAG [bench args]      rocprofv3 --kernel-trace --stats of a short eager run
-#   rehearse CFG P RANK [ENV=V,..] bench.py --rehearse P --rehearse-rank RANK
+#   rehearse CFG P RANK [ENV=V,..] [bench args]   bench.py --rehearse P --rehearse-rank RANK
 #   eps TETS STEPS TAG             tools/elastic_eps_curves.py --gpu (per-step curves + npz)
 #   geps CFG N TAG                 tools/geom_eps_curve.py --gpu on a reduced geometry scene
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -89,11 +89,11 @@ for step in "$@"; do
       echo "prof rc=$rc"; [ $rc -ne 0 ] && grep -v "^ *@" "$d.log" | tail -5; fatal $rc "prof $cfg"
       f=$(find "$d" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && head -12 "$f" | cut -c1-160
       t=$(find "$d" -name "*kernel_trace.csv" | head -1); [ -n "$t" ] && python3 tools/solve_levels.py "$t" 6 > "$d.levels.txt" 2>&1 && gzip -f "$t" ;;
-    rehearse)
-      cfg=$1; P=$2; rk=$3; envs=${4:-}
-      log=gpurun_out/rehearse_${cfg}_P${P}_r$rk.log
+    rehearse)   # rehearse CFG P RANK [ENV=V,ENV2=V] [bench args]
+      cfg=$1; P=$2; rk=$3; envs=${4:-}; shift; shift; shift; [ $# -gt 0 ] && shift
+      log=gpurun_out/rehearse_${cfg}_P${P}_r${rk}_${envs//[,=]/_}.log
       env ${envs//,/ } timeout -k 10 300 python -u bench.py --config $cfg --rehearse $P --rehearse-rank $rk --steps ${STEPS:-3} \
-        --warmup 1 > $log 2>&1; rc=$?
+        --warmup 1 "$@" > $log 2>&1; rc=$?
       [ $rc -ne 0 ] && tail -5 $log; fatal $rc "rehearse $cfg $P $rk"
       python3 - $log <<'PY'
 import json, sys
