@@ -332,40 +332,8 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
                                                               : DirectSolver::kPartTopRows;
     const int nd_leaf = default_nd_leaf(nf_);
     stamp("adjacency");
-    // partitioned: the forced bisections balance each rank's estimated time per ADMM iteration
-    // (AA_PART_BALANCE=0: by vertex count) -- its factor bytes, streamed by about 2.8 sweeps per
-    // iteration (two-set solve + the reject solves) at ~3 TB/s, plus its elements' local steps
-    // (measured per element and iteration: NeoHookean / StVK tets ~0.9 ns, linear tets and tris
-    // ~0.1 ns) -- instead of the vertex count, which leaves a boundary-heavy mesh's
-    // ranks with unequal separators and factor bytes
-    const bool balance = P > 1 && !(std::getenv("AA_PART_BALANCE") && std::getenv("AA_PART_BALANCE")[0] == '0');
-    std::vector<double> part_cost;
-    NdTree tree;
-    if (balance) {
-        std::vector<double> vcost(nf_, 0.0);
-        for (auto& g : hgroups_) {
-            const double te = (g.kind == 0 && g.material != AA_LINEAR) ? 0.9e-9 : 0.1e-9;
-            for (size_t t = 0; t < g.idx.size() / g.nv; ++t)
-                for (int a = 0; a < g.nv; ++a) {
-                    const int fa = node2free[g.idx[t * g.nv + a]];
-                    if (fa >= 0) vcost[fa] += te / g.nv;
-                }
-        }
-        tree = nested_dissection_balanced(nf_, coords.data(), aptr, aj, nd_leaf, P, top_dense, part_top_rows, vcost,
-                                          2.8 / 3e12, 6, &part_cost);
-    } else {
-        tree = nested_dissection(nf_, coords.data(), aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::top_rows(nf_), P > 1 ? P : 0,
-                                 top_dense, part_top_rows);
-    }
-    if (P > 1 && std::getenv("AA_SETUP_TIMES")) {
-        if (part_cost.empty()) {
-            part_cost = part_factor_bytes(tree, aptr, aj);
-            for (double& c : part_cost) c *= 2.8 / 3e12;
-        }
-        std::fprintf(stderr, "[setup] partition (%s): estimated us per iteration per part:", balance ? "balanced" : "by vertices");
-        for (double c : part_cost) std::fprintf(stderr, " %.1f", c * 1e6);
-        std::fprintf(stderr, "\n");
-    }
+    NdTree tree = nested_dissection(nf_, coords.data(), aptr, aj, nd_leaf, P > 1 ? 0 : DirectSolver::top_rows(nf_), P > 1 ? P : 0, top_dense,
+                                     part_top_rows);
     stamp("nested dissection");
     node2int_.assign(n, -1);
     int2node_.assign(n, -1);

@@ -80,12 +80,9 @@ struct NdBuilder {
     }
 
     // the top bisections are forced until there are `parts` parts (one per leaf of the top, in
-    // left-to-right order; an odd count is split floor(parts/2) : ceil(parts/2) by vertex count,
-    // or -- frac given -- at the vertex fraction frac[k] of the k-th forced split, pre-order);
+    // left-to-right order; an odd count is split floor(parts/2) : ceil(parts/2) by vertex count);
     // each part is then dissected by build(). part_of[node] = part id, -1 = top separator
     std::vector<int> part_of;
-    const std::vector<double>* frac = nullptr;
-    std::vector<NdSplit> splits;   // the forced splits, pre-order
     std::vector<int> build_parts(std::vector<int> verts, int parts, int& next_part) {
         if (parts <= 1) {
             const int id = next_part++;
@@ -97,15 +94,7 @@ struct NdBuilder {
         }
         std::vector<int> left, right, sep;
         const int pl = parts / 2, pr = parts - pl;
-        const int k = (int)splits.size();
-        splits.push_back({next_part, pl, pr, (double)pl / parts});
-        if (frac && k < (int)frac->size() && (*frac)[k] > 0.0 && (*frac)[k] < 1.0) {
-            splits[k].frac = (*frac)[k];
-            const long long den = 1LL << 30;
-            if (!verts.empty()) split(verts, left, right, sep, (int)std::llround(splits[k].frac * den), (int)den);
-        } else if (!verts.empty()) {
-            split(verts, left, right, sep, pl, parts);
-        }
+        if (!verts.empty()) split(verts, left, right, sep, pl, parts);
         if (left.empty() && right.empty() && !sep.empty()) std::swap(left, sep);   // tiny: keep it in a part
         std::vector<int> roots = build_parts(std::move(left), pl, next_part);
         std::vector<int> r2 = build_parts(std::move(right), pr, next_part);
@@ -119,10 +108,8 @@ struct NdBuilder {
 }  // namespace
 
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                         int leaf_size, int top_rows, int n_parts, bool merge_top, int part_top_rows,
-                         const std::vector<double>* frac, std::vector<NdSplit>* splits_out) {
+                         int leaf_size, int top_rows, int n_parts, bool merge_top, int part_top_rows) {
     NdBuilder b(n, xyz, adj_ptr, adj, std::max(1, leaf_size));
-    b.frac = frac;
     std::vector<int> all(n);
     std::iota(all.begin(), all.end(), 0);
     int nparts = 0;
@@ -130,7 +117,6 @@ NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_p
     std::vector<int> roots = part_levels > 0 ? b.build_parts(all, n_parts, nparts) : b.build(all);
     std::vector<std::vector<int>> piv = std::move(b.piv), kids = std::move(b.kids);
     std::vector<int> part_of = std::move(b.part_of);
-    if (splits_out) *splits_out = b.splits;
     part_of.resize(piv.size(), part_levels > 0 ? -1 : 0);
     if (part_levels > 0) top_rows = 0;   // the partition roots must stay separate supernodes
     // ---- amalgamate the top levels of the subtree under `root` into one dense supernode (up to
@@ -259,75 +245,6 @@ NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_p
         t.part_end[0] = n;
     }
     return t;
-}
-
-std::vector<double> part_factor_bytes(const NdTree& t, const std::vector<int>& adj_ptr, const std::vector<int>& adj) {
-    // symbolic factorization on the adjacency pattern in the tree's ordering: boundary rows of
-    // every supernode from its pivots' neighbours and its children's boundaries (as symbolic())
-    const int n = (int)t.perm.size(), nn = (int)t.beg.size();
-    std::vector<int> inv(n);
-    for (int q = 0; q < n; ++q) inv[t.perm[q]] = q;
-    std::vector<std::vector<int>> bnd(nn);
-    std::vector<double> bytes(std::max(1, t.n_parts), 0.0);
-    for (int s = 0; s < nn; ++s) {
-        const int b0 = t.beg[s], e0 = t.end[s], p = e0 - b0;
-        std::vector<int> B;
-        for (int j = b0; j < e0; ++j) {
-            const int v = t.perm[j];
-            for (int k = adj_ptr[v]; k < adj_ptr[v + 1]; ++k) if (inv[adj[k]] >= e0) B.push_back(inv[adj[k]]);
-        }
-        for (int c : t.children[s]) {
-            for (int i : bnd[c]) if (i >= e0) B.push_back(i);
-            std::vector<int>().swap(bnd[c]);
-        }
-        std::sort(B.begin(), B.end());
-        B.erase(std::unique(B.begin(), B.end()), B.end());
-        const double nb = (double)B.size();
-        bnd[s] = std::move(B);
-        if (t.part[s] >= 0) bytes[t.part[s]] += 8.0 * (0.5 * p * (p + 1.0) + p * nb);
-    }
-    return bytes;
-}
-
-NdTree nested_dissection_balanced(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                                  int leaf_size, int n_parts, bool merge_top, int part_top_rows,
-                                  const std::vector<double>& vertex_cost, double byte_cost, int iters,
-                                  std::vector<double>* part_cost_out) {
-    std::vector<double> frac;
-    NdTree best;
-    double best_imb = 1e300;
-    std::vector<double> best_cost;
-    for (int it = 0; it < std::max(1, iters); ++it) {
-        std::vector<NdSplit> sp;
-        NdTree t = nested_dissection(n, xyz, adj_ptr, adj, leaf_size, 0, n_parts, merge_top, part_top_rows,
-                                     frac.empty() ? nullptr : &frac, &sp);
-        std::vector<double> cost = part_factor_bytes(t, adj_ptr, adj);
-        for (double& c : cost) c *= byte_cost;
-        if (!vertex_cost.empty())
-            for (int q = 0; q < t.top_beg; ++q) {
-                int part = 0;
-                while (part + 1 < t.n_parts && q >= t.part_end[part]) ++part;
-                cost[part] += vertex_cost[t.perm[q]];
-            }
-        double mx = 0, sum = 0;
-        for (double c : cost) { mx = std::max(mx, c); sum += c; }
-        const double imb = sum > 0 ? mx * cost.size() / sum : 1.0;
-        if (imb < best_imb) { best_imb = imb; best = std::move(t); best_cost = cost; }
-        if (imb < 1.02 || it + 1 == iters) break;
-        // move each forced split toward equal cost per part on both sides (damped)
-        frac.resize(sp.size());
-        for (size_t k = 0; k < sp.size(); ++k) {
-            double cl = 0, cr = 0;
-            for (int q = 0; q < sp[k].pl; ++q) cl += cost[sp[k].p0 + q];
-            for (int q = 0; q < sp[k].pr; ++q) cr += cost[sp[k].p0 + sp[k].pl + q];
-            const double want = (double)sp[k].pl / (sp[k].pl + sp[k].pr), got = cl / std::max(1e-300, cl + cr);
-            double f = sp[k].frac * std::pow(want / std::max(1e-12, got), 0.7);
-            f = std::min(0.8, std::max(0.2, f));
-            frac[k] = f;
-        }
-    }
-    if (part_cost_out) *part_cost_out = best_cost;
-    return best;
 }
 
 // ------------------------------------------------------------------ multifrontal Cholesky

@@ -54,28 +54,9 @@ inline int default_nd_leaf(long long n_unknowns) {
 // their separators form the "top" of the tree (part -1): with merge_top one dense root
 // supernode, else one supernode per separator. No top_rows amalgamation when partitioned;
 // part_top_rows > 0 (with merge_top) amalgamates each part's own top levels instead.
-// frac (optional): the vertex fraction of each forced top split (pre-order), instead of
-// floor(P/2) / P; splits_out (optional): the forced splits actually made
-struct NdSplit {
-    int p0, pl, pr;   // parts [p0, p0 + pl) left, [p0 + pl, p0 + pl + pr) right
-    double frac;      // vertex fraction that went left
-};
 NdTree nested_dissection(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
                          int leaf_size, int top_rows = 0, int n_parts = 0, bool merge_top = true,
-                         int part_top_rows = 0, const std::vector<double>* frac = nullptr,
-                         std::vector<NdSplit>* splits_out = nullptr);
-// Per part: the factor's bytes (8 (p (p + 1) / 2 + p nb) over the part's supernodes), from a
-// symbolic factorization of the adjacency pattern in the tree's ordering
-std::vector<double> part_factor_bytes(const NdTree& t, const std::vector<int>& adj_ptr, const std::vector<int>& adj);
-// Partitioned nested dissection whose forced splits balance an estimated per-part cost instead of
-// the vertex count: cost(part) = byte_cost x part_factor_bytes + sum of vertex_cost over the part's
-// vertices (its elements' local-step cost). Up to `iters` dissections, each moving every split's
-// vertex fraction toward equal cost per part on both of its sides; the most balanced is returned
-// (part_cost_out: its per-part costs).
-NdTree nested_dissection_balanced(int n, const double* xyz, const std::vector<int>& adj_ptr, const std::vector<int>& adj,
-                                  int leaf_size, int n_parts, bool merge_top, int part_top_rows,
-                                  const std::vector<double>& vertex_cost, double byte_cost, int iters,
-                                  std::vector<double>* part_cost_out = nullptr);
+                         int part_top_rows = 0);
 
 struct SupernodalFactor {
     int n = 0;
