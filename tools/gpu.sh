@@ -88,7 +88,8 @@ for step in "$@"; do
         --no-cpu-baseline --eps-steps 0 --no-secondary --geom-eps-solves 0 "$@" > "$d.log" 2>&1); rc=$?
       echo "prof rc=$rc"; [ $rc -ne 0 ] && grep -v "^ *@" "$d.log" | tail -5; fatal $rc "prof $cfg"
       f=$(find "$d" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && head -12 "$f" | cut -c1-160
-      t=$(find "$d" -name "*kernel_trace.csv" | head -1); [ -n "$t" ] && python3 tools/solve_levels.py "$t" 6 > "$d.levels.txt" 2>&1 && gzip -f "$t" ;;
+      nrs=3; [ "$cfg" = c4 ] && nrs=6   # the Z variant's two-set solve; the others solve one set
+      t=$(find "$d" -name "*kernel_trace.csv" | head -1); [ -n "$t" ] && python3 tools/solve_levels.py "$t" $nrs > "$d.levels.txt" 2>&1; [ -n "$t" ] && gzip -f "$t" ;;
     rehearse)   # rehearse CFG P RANK [ENV=V,ENV2=V] [bench args]
       cfg=$1; P=$2; rk=$3; envs=${4:-}; shift; shift; shift; [ $# -gt 0 ] && shift
       log=gpurun_out/rehearse_${cfg}_P${P}_r${rk}_${envs//[,=]/_}.log
