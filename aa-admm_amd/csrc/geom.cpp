@@ -7,8 +7,8 @@
 //   ALMGeometrySolver<3>::solve_ADMM           Geometry/ALMGeometrySolver.h:163-283
 // Every ALM iteration is enqueued on one HIP stream; the accept/reject decision of the
 // reference (comb < prev, reset, Anderson reset) is taken by a device control kernel that
-// gates the following kernels, so the loop runs as replays of a captured hipGraph with one
-// host synchronisation at the end (plus one per extra chunk when rejections extend the loop).
+// gates the following kernels, so the loop runs as replays of captured hipGraphs with one
+// host synchronisation per launch of the passes still needed (GeomSolver::solve).
 #include "geom.hpp"
 
 #include <algorithm>
@@ -142,10 +142,12 @@ GeomSolver::~GeomSolver() {
 }
 
 void GeomSolver::drop_graph() {
-    if (gexec_) (void)hipGraphExecDestroy(gexec_);
-    if (graph_) (void)hipGraphDestroy(graph_);
-    gexec_ = nullptr;
-    graph_ = nullptr;
+    for (int i = 0; i < kNChunks; ++i) {
+        if (gexec_[i]) (void)hipGraphExecDestroy(gexec_[i]);
+        if (graph_[i]) (void)hipGraphDestroy(graph_[i]);
+        gexec_[i] = nullptr;
+        graph_[i] = nullptr;
+    }
 }
 
 int GeomSolver::add_ref_surface(const double* V3, int nv, const int* F3, int nf) {
@@ -804,42 +806,49 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
     prologue(init_x3, max_iter, m, max_iter, eps_abs, stop_rel_);
     const bool may_stop = eps_abs > 0.0 || stop_rel_ > 0.0;
     const int target = std::max(1, max_iter);
-    const int chunk = std::min(target, 64);
+    const int chunk = std::min(target, kChunks[0]);
     bool use_graph = !(std::getenv("AA_ADMM_NO_GRAPH") && std::getenv("AA_ADMM_NO_GRAPH")[0] == '1') &&
                      !(comm_ && !comm_->capturable());
-    auto run_chunk = [&]() {
-        if (use_graph && (!gexec_ || graph_chunk_ != chunk || graph_m_ != m)) {
-            drop_graph();
-            bool ok = capture_graph(s(), [&] { enqueue_chunk(chunk, m); }, &graph_, &gexec_);
-            if (comm_) {   // the ranks replay or launch eagerly together
-                double f = ok ? 0.0 : 1.0;
-                comm_->allreduce_sum_host(&f, 1);
-                if (f > 0 && ok) { drop_graph(); ok = false; }
+    if (graph_m_ != m) { drop_graph(); graph_m_ = m; }
+    // n loop passes: replays of the captured 64 / 16 / 4 / 1-pass graphs (each captured on first use)
+    auto run_passes = [&](int n) {
+        if (!use_graph) { enqueue_chunk(n, m); return; }
+        for (int i = 0; i < kNChunks && n > 0; ++i) {
+            for (; n >= kChunks[i]; n -= kChunks[i]) {
+                if (!gexec_[i]) {
+                    bool ok = capture_graph(s(), [&] { enqueue_chunk(kChunks[i], m); }, &graph_[i], &gexec_[i]);
+                    if (comm_) {   // the ranks replay or launch eagerly together
+                        double f = ok ? 0.0 : 1.0;
+                        comm_->allreduce_sum_host(&f, 1);
+                        if (f > 0 && ok) ok = false;
+                    }
+                    if (!ok) { drop_graph(); use_graph = false; enqueue_chunk(n, m); return; }
+                }
+                AA_HIP(hipGraphLaunch(gexec_[i], s()));
             }
-            use_graph = ok;
-            graph_chunk_ = chunk;
-            graph_m_ = m;
-        }
-        if (use_graph) {
-            AA_HIP(hipGraphLaunch(gexec_, s()));
-        } else {
-            enqueue_chunk(chunk, m);
         }
     };
-    // no rejection: exactly ceil(target / chunk) chunks; each rejection adds one x-update
-    // (a rejected iteration is always followed by an accepted one, so <= 2 target + 1 passes)
-    // (with a run-to-epsilon stop: two chunks in flight, then one per done check)
-    const int first = may_stop ? std::min(2, (target + chunk - 1) / chunk) : (target + chunk - 1) / chunk;
-    for (int i = 0; i < first; ++i) run_chunk();
-    int passes = first * chunk;
+    // A pass accepts at most one iteration and a rejected pass is always followed by an accepted
+    // one (alm_reset), so the loop needs between `target` and 2 target passes. Without a
+    // run-to-epsilon stop it launches exactly the passes still needed at least -- target, then
+    // target - accepted after each check -- so no pass runs gated after the last acceptance (the
+    // fixed 64-pass chunks of round 3 ran up to 63 such passes per solve: ~3 % of C3's loop).
+    // With a stop (unknown end): two 64-pass chunks in flight, then one per done check.
+    // AA_GEOM_EXACT_TAIL=0 restores the fixed chunks for both (A/B).
+    static const bool exact_tail = !(std::getenv("AA_GEOM_EXACT_TAIL") && std::getenv("AA_GEOM_EXACT_TAIL")[0] == '0');
+    const bool exact = exact_tail && !may_stop;
+    const int first = exact ? target : (may_stop ? std::min(2, (target + chunk - 1) / chunk) : (target + chunk - 1) / chunk) * chunk;
+    run_passes(first);
+    int passes = first;
     for (;;) {
         Ctrl c;
         AA_HIP(hipMemcpyAsync(&c, ctrl_.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s()));
         AA_HIP(hipStreamSynchronize(s()));
         if (c.done) break;
         if (passes > 2 * target + 2 * chunk) throw Error(ERR_NUMERIC, "solve_ADMM: the loop did not terminate");
-        run_chunk();
-        passes += chunk;
+        const int next = exact ? std::max(1, target - c.nrec) : chunk;
+        run_passes(next);
+        passes += next;
     }
     fetch_results();
     if (comm_) {   // every rank ends with the full solution: zero what it does not own, sum

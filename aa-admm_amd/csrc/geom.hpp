@@ -122,9 +122,12 @@ private:
     aa_geom_runtime rt_{};
     double clock_khz_ = 0;
 
-    hipGraph_t graph_ = nullptr;
-    hipGraphExec_t gexec_ = nullptr;
-    int graph_chunk_ = 0, graph_m_ = -1;
+    // captured loop passes, one graph per chunk size kChunks[i] (captured on first use)
+    static constexpr int kNChunks = 4;
+    static constexpr int kChunks[kNChunks] = {64, 16, 4, 1};
+    hipGraph_t graph_[kNChunks] = {};
+    hipGraphExec_t gexec_[kNChunks] = {};
+    int graph_m_ = -1;
     void drop_graph();
 
     DevBuf<int> mk_log_;   // (aa_mk, aa_skip) per instrumented Anderson launch
