@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <numeric>
 
 #include "dense_gpu.hpp"
@@ -133,6 +134,45 @@ struct BvhBuilder {
     }
 };
 
+// The BVH collapsed to G children per node (layout: SurfDev::wide). Returns the number of
+// wide levels below the root (the group traversal's stack holds at most (G - 1) per level).
+int build_wide(const std::vector<BvhNode>& N, int G, std::vector<BvhNode>& W) {
+    W.clear();
+    int depth = 0;
+    // descendants of n log2(G) levels down, left to right; a leaf met earlier stands for itself
+    auto expand = [&](int n) {
+        std::vector<int> c{n};
+        for (int l = 1; l < G; l <<= 1) {
+            std::vector<int> nx;
+            for (int i : c) {
+                if (bvh_count(N[i]) > 0) nx.push_back(i);
+                else { nx.push_back(i + 1); nx.push_back(N[i].a); }
+            }
+            c.swap(nx);
+        }
+        return c;
+    };
+    std::function<int(int, int)> make = [&](int n, int level) -> int {
+        const int w = (int)(W.size() / G);
+        W.resize(W.size() + G);
+        depth = std::max(depth, level);
+        const std::vector<int> c = expand(n);
+        for (int k = 0; k < G; ++k) {
+            BvhNode r{};
+            r.a = -1;
+            if (k < (int)c.size()) {
+                r = N[c[k]];
+                if (bvh_count(r) > 0) r.sn = (unsigned)bvh_count(r) << 29;
+                else { r.sn = 0; r.a = make(c[k], level + 1); }
+            }
+            W[(size_t)w * G + k] = r;
+        }
+        return w;
+    };
+    if (!N.empty()) make(0, 1);
+    return depth;
+}
+
 }  // namespace
 
 GeomSolver::~GeomSolver() {
@@ -170,6 +210,19 @@ int GeomSolver::add_ref_surface(const double* V3, int nv, const int* F3, int nf)
     B.build(0, nf);
     S.dnodes.upload(S.nodes, s());
     S.dtris.upload(S.tris, s());
+    {   // group traversal (AA_CP_GROUP = lanes per query: 4 or 8; 0 = one lane per query)
+        const char* ev = std::getenv("AA_CP_GROUP");
+        const int G = ev ? std::atoi(ev) : 4;
+        if (G == 4 || G == 8) {
+            const int depth = build_wide(S.nodes, G, S.wide);
+            if ((G - 1) * depth <= kCpStack) {
+                S.wide_g = G;
+                S.dwide.upload(S.wide, s());
+            } else {
+                S.wide.clear();   // too deep for the stack: one lane per query
+            }
+        }
+    }
     AA_HIP(hipStreamSynchronize(s()));
     surfs_.push_back(std::move(S));
     return (int)surfs_.size() - 1;

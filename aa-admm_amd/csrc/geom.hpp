@@ -63,8 +63,13 @@ private:
         std::vector<BvhNode> nodes;
         std::vector<BvhTri> tris;
         DevBuf<BvhNode> dnodes;
+        std::vector<BvhNode> wide;   // collapsed tree of the group traversal (wide_g children)
+        DevBuf<BvhNode> dwide;
+        int wide_g = 0;
         DevBuf<BvhTri> dtris;
-        SurfDev dev() const { return SurfDev{dnodes.p, dtris.p, (int)nodes.size(), (int)tris.size()}; }
+        SurfDev dev() const {
+            return SurfDev{dnodes.p, dtris.p, (int)nodes.size(), (int)tris.size(), wide_g ? dwide.p : nullptr, wide_g};
+        }
     };
     struct Reg { std::vector<int> idx; std::vector<double> coef; double tgt[3]; };
     // reference-surface constraints processed in the points' nested-dissection order

@@ -12,6 +12,8 @@
 //   edge   -- v |v|^-1 L;   closeness -- identity (Constraint.h:319-322 never overrides);
 //   closest point on a reference surface -- stackless traversal of a depth-first BVH with exact
 //             box pruning, warm-started from the previous iteration's triangle.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "geom_kernels.hpp"
 
@@ -194,38 +196,51 @@ __device__ void angle_project(double* v, double min_r, double max_r) {
     }
 }
 
-// Ericson closest point on a triangle (igl point_simplex_squared_distance.cpp:40-108)
+// Ericson closest point on a triangle (igl point_simplex_squared_distance.cpp:40-108). Every
+// product-sum is an explicit fma and contraction is off, so the bits do not depend on how the
+// compiler fuses the inlined code at each call site (the one-lane and the group traversal must
+// agree bit for bit).
+__device__ __forceinline__ double dot3(double ax, double ay, double az, double bx, double by, double bz) {
+#pragma clang fp contract(off)
+    return fma(ax, bx, fma(ay, by, az * bz));
+}
+__device__ __forceinline__ double dist2(double px, double py, double pz, double qx, double qy, double qz) {
+#pragma clang fp contract(off)
+    const double dx = px - qx, dy = py - qy, dz = pz - qz;
+    return fma(dx, dx, fma(dy, dy, dz * dz));
+}
 __device__ __forceinline__ void closest_on_tri(const double* t, double px, double py, double pz, double& cx,
                                                double& cy, double& cz) {
+#pragma clang fp contract(off)
     const double ax = t[0], ay = t[1], az = t[2], bx = t[3], by = t[4], bz = t[5], qx = t[6], qy = t[7], qz = t[8];
     const double abx = bx - ax, aby = by - ay, abz = bz - az, acx = qx - ax, acy = qy - ay, acz = qz - az;
     const double apx = px - ax, apy = py - ay, apz = pz - az;
-    const double d1 = abx * apx + aby * apy + abz * apz, d2 = acx * apx + acy * apy + acz * apz;
+    const double d1 = dot3(abx, aby, abz, apx, apy, apz), d2 = dot3(acx, acy, acz, apx, apy, apz);
     if (d1 <= 0.0 && d2 <= 0.0) { cx = ax; cy = ay; cz = az; return; }
     const double bpx = px - bx, bpy = py - by, bpz = pz - bz;
-    const double d3 = abx * bpx + aby * bpy + abz * bpz, d4 = acx * bpx + acy * bpy + acz * bpz;
+    const double d3 = dot3(abx, aby, abz, bpx, bpy, bpz), d4 = dot3(acx, acy, acz, bpx, bpy, bpz);
     if (d3 >= 0.0 && d4 <= d3) { cx = bx; cy = by; cz = bz; return; }
-    const double vc = d1 * d4 - d3 * d2;
+    const double vc = fma(d1, d4, -(d3 * d2));
     if (!(ax == bx && ay == by && az == bz) && vc <= 0.0 && d1 >= 0.0 && d3 <= 0.0) {
         const double v = d1 / (d1 - d3);
-        cx = ax + v * abx; cy = ay + v * aby; cz = az + v * abz; return;
+        cx = fma(v, abx, ax); cy = fma(v, aby, ay); cz = fma(v, abz, az); return;
     }
     const double cpx = px - qx, cpy = py - qy, cpz = pz - qz;
-    const double d5 = abx * cpx + aby * cpy + abz * cpz, d6 = acx * cpx + acy * cpy + acz * cpz;
+    const double d5 = dot3(abx, aby, abz, cpx, cpy, cpz), d6 = dot3(acx, acy, acz, cpx, cpy, cpz);
     if (d6 >= 0.0 && d5 <= d6) { cx = qx; cy = qy; cz = qz; return; }
-    const double vb = d5 * d2 - d1 * d6;
+    const double vb = fma(d5, d2, -(d1 * d6));
     if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {
         const double w = d2 / (d2 - d6);
-        cx = ax + w * acx; cy = ay + w * acy; cz = az + w * acz; return;
+        cx = fma(w, acx, ax); cy = fma(w, acy, ay); cz = fma(w, acz, az); return;
     }
-    const double va = d3 * d6 - d5 * d4;
+    const double va = fma(d3, d6, -(d5 * d4));
     if (va <= 0.0 && (d4 - d3) >= 0.0 && (d5 - d6) >= 0.0) {
         const double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-        cx = bx + w * (qx - bx); cy = by + w * (qy - by); cz = bz + w * (qz - bz); return;
+        cx = fma(w, qx - bx, bx); cy = fma(w, qy - by, by); cz = fma(w, qz - bz, bz); return;
     }
     const double denom = 1.0 / (va + vb + vc);
     const double v = vb * denom, w = vc * denom;
-    cx = ax + abx * v + acx * w; cy = ay + aby * v + acy * w; cz = az + abz * v + acz * w;
+    cx = fma(acx, w, fma(abx, v, ax)); cy = fma(acy, w, fma(aby, v, ay)); cz = fma(acz, w, fma(abz, v, az));
 }
 
 __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py, double pz) {
@@ -270,7 +285,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
     auto test_tri = [&](int t) {
         double qx, qy, qz;
         closest_on_tri(S.tris[t].v, px, py, pz, qx, qy, qz);
-        const double d2 = (px - qx) * (px - qx) + (py - qy) * (py - qy) + (pz - qz) * (pz - qz);
+        const double d2 = dist2(px, py, pz, qx, qy, qz);
         if (d2 < best) { best = d2; best_t = t; cx = qx; cy = qy; cz = qz; }
     };
     bool tight = false;
@@ -353,15 +368,126 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
     return best_t;
 }
 
+// The same query run by a group of G lanes (G = 4 or 8, aligned within the wave) over the
+// collapsed tree S.wide: each step the G lanes load and test the G children of one node at once
+// (one dependent load per log2(G) levels of the binary tree), a leaf's <= 4 triangles are tested
+// one per lane, and the children that pass are visited nearest first through a per-query stack
+// in LDS (stk_i / stk_d, kCpStack entries; the host checks (G - 1) x depth fits). A query then
+// costs about 1 / log2(G) of the dependent node loads of bvh_closest and G lanes' worth of
+// occupancy, which is what a latency-bound traversal with few queries per SIMD lacks.
+// Same result as bvh_closest: the seed / descent part is bvh_closest's own (every lane alike),
+// giving t0; bvh_closest then keeps t0 if no triangle is strictly closer, else the first
+// triangle in its depth-first order -- the smallest leaf-order index -- among the closest ones.
+// Here the visit order differs, so a tie is broken explicitly by that rule (t0 first, then the
+// smaller index), and a box whose bound EQUALS the best distance is still opened.
+template <int G>
+__device__ int bvh_closest_grp(const SurfDev& S, double px, double py, double pz, int warm, int* __restrict__ stk_i,
+                               float* __restrict__ stk_d, double& cx, double& cy, double& cz) {
+    const int lane = threadIdx.x & 63, base = lane & ~(G - 1), j = lane - base;
+    const unsigned long long gm = ((1ull << G) - 1ull) << base;
+    double best = INFINITY;
+    int best_t = -1;
+    cx = px; cy = py; cz = pz;
+    if (S.n_nodes == 0) return -1;
+    auto test_tri = [&](int t) {
+        double qx, qy, qz;
+        closest_on_tri(S.tris[t].v, px, py, pz, qx, qy, qz);
+        const double d2 = dist2(px, py, pz, qx, qy, qz);
+        if (d2 < best) { best = d2; best_t = t; cx = qx; cy = qy; cz = qz; }
+    };
+    bool tight = false;
+    if (warm >= 0 && warm < S.n_tris) {
+        test_tri(warm);
+        const double* v = S.tris[warm].v;
+        const double e2 = (v[3] - v[0]) * (v[3] - v[0]) + (v[4] - v[1]) * (v[4] - v[1]) + (v[5] - v[2]) * (v[5] - v[2]);
+        tight = best <= AA_WARM_TIGHT * e2;
+    }
+    if (!tight) {
+        int i = 0;
+        for (;;) {
+            const BvhNode& nd = S.nodes[i];
+            if (bvh_count(nd) > 0) {
+                for (int t = nd.a; t < nd.a + bvh_count(nd); ++t) test_tri(t);
+                break;
+            }
+            const double dl = box_d2(S.nodes[i + 1], px, py, pz), dr = box_d2(S.nodes[nd.a], px, py, pz);
+            i = dl <= dr ? i + 1 : nd.a;
+        }
+    }
+    const int t0 = best_t;
+    int cur = 0, sp = 0;
+    for (;;) {
+        const BvhNode rec = S.wide[(size_t)cur * G + j];
+        const bool valid = rec.a >= 0;
+        const int cnt = bvh_count(rec);
+        const double d = valid ? box_d2(rec, px, py, pz) : INFINITY;
+        // leaf children: one after the other, a triangle per lane, group arg-min by (distance, index)
+        for (unsigned long long lm = __ballot(valid && cnt > 0 && d <= best) & gm; lm; lm &= lm - 1) {
+            const int src = __ffsll((long long)lm) - 1;
+            if (!(__shfl(d, src) <= best)) continue;   // group-uniform
+            const int ak = __shfl(rec.a, src), nk = __shfl(cnt, src);
+            double qd = INFINITY, qx = 0, qy = 0, qz = 0;
+            int qt = 0x7fffffff;
+            if (j < nk) {
+                qt = ak + j;
+                closest_on_tri(S.tris[qt].v, px, py, pz, qx, qy, qz);
+                qd = dist2(px, py, pz, qx, qy, qz);
+            }
+#pragma unroll
+            for (int off = G / 2; off > 0; off >>= 1) {
+                const double od = __shfl_xor(qd, off, G), ox = __shfl_xor(qx, off, G), oy = __shfl_xor(qy, off, G),
+                             oz = __shfl_xor(qz, off, G);
+                const int ot = __shfl_xor(qt, off, G);
+                if (od < qd || (od == qd && ot < qt)) { qd = od; qt = ot; qx = ox; qy = oy; qz = oz; }
+            }
+            if (qd < best || (qd == best && best_t != t0 && qt < best_t)) {
+                best = qd; best_t = qt; cx = qx; cy = qy; cz = qz;
+            }
+        }
+        // inner children: descend into the nearest, push the others (farthest deepest)
+        const bool inner = valid && cnt == 0 && d <= best;
+        const unsigned long long im = __ballot(inner) & gm;
+        const int ni = __popcll(im);
+        if (ni == 0) {
+            bool next = false;
+            while (sp > 0) {
+                --sp;
+                if ((double)stk_d[sp] <= best) { cur = stk_i[sp]; next = true; break; }
+            }
+            if (!next) break;
+            continue;
+        }
+        int rank = 0;   // position in descending distance (ties: lower lane first)
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const double dk = __shfl(d, base + k);
+            if (((im >> (base + k)) & 1ull) && (dk > d || (dk == d && k < j))) ++rank;
+        }
+        if (inner && rank < ni - 1) {
+            float f = (float)d;   // rounded down: the pop test never drops a box it should open
+            if ((double)f > d) f = nextafterf(f, -INFINITY);
+            stk_i[sp + rank] = rec.a;
+            stk_d[sp + rank] = f;
+        }
+        const unsigned long long nm = __ballot(inner && rank == ni - 1) & gm;
+        cur = __shfl(rec.a, __ffsll((long long)nm) - 1);
+        sp += ni - 1;
+    }
+    return best_t;
+}
+
 // ------------------------------------------------------------------ z step
 // One constraint: v = T(x) (+u), z = P(v); PLAIN (GeometrySolver<3>): soft groups combine
 // z = a v + (1 - a) P(v) (Constraint::project_and_combine, Constraint.h:118-130) and the
 // return value is this constraint's |T(x) - z|^2 (GeometrySolver::get_ADMM_residual,
 // GeometrySolver.h:459-461); ALM: returns 0.
-template <int T, int K, bool PLAIN>
+// G > 1: the element's closest-point query runs on a group of G lanes (bvh_closest_grp, stack
+// stk_i / stk_d); every lane of the group computes the transform alike, the first one writes.
+template <int T, int K, bool PLAIN, int G = 1>
 __device__ __forceinline__ double geo_z_one(const GeoGroupDev& g, int e, const double* __restrict__ x,
                                             const double* __restrict__ u, double* __restrict__ z,
-                                            double* __restrict__ y) {
+                                            double* __restrict__ y, int* stk_i = nullptr, float* stk_d = nullptr) {
+    const bool writer = G == 1 || (threadIdx.x & (G - 1)) == 0;
     constexpr int C = (T == GEO_ANGLE || T == GEO_EDGE) ? K - 1 : K;
     double v[3 * C], uu[3 * C];
     double t[PLAIN ? 3 * C : 1];
@@ -388,8 +514,10 @@ __device__ __forceinline__ double geo_z_one(const GeoGroupDev& g, int e, const d
         for (int c = 0; c < C; ++c) {
             double qx, qy, qz;
             const int w0 = g.warm ? g.warm[e] : -1;
-            const int tr = bvh_closest(g.surf, v[3 * c], v[3 * c + 1], v[3 * c + 2], w0, qx, qy, qz);
-            if (g.warm) g.warm[e] = tr;
+            int tr;
+            if constexpr (G > 1) tr = bvh_closest_grp<G>(g.surf, v[3 * c], v[3 * c + 1], v[3 * c + 2], w0, stk_i, stk_d, qx, qy, qz);
+            else tr = bvh_closest(g.surf, v[3 * c], v[3 * c + 1], v[3 * c + 2], w0, qx, qy, qz);
+            if (g.warm && writer) g.warm[e] = tr;
             v[3 * c] = qx; v[3 * c + 1] = qy; v[3 * c + 2] = qz;
         }
     }   // CLOSENESS: identity
@@ -403,6 +531,7 @@ __device__ __forceinline__ double geo_z_one(const GeoGroupDev& g, int e, const d
 #pragma unroll
         for (int i = 0; i < 3 * C; ++i) { const double r = t[i] - v[i]; part += r * r; }
     }
+    if (!writer) return part;
     if (g.hard) {
 #pragma unroll
         for (int i = 0; i < 3 * C; ++i) { z[g.uoff + (size_t)i * g.count + e] = v[i]; uu[i] = v[i] - uu[i]; }
@@ -421,6 +550,21 @@ __global__ __launch_bounds__(kBlock) void k_geo_z(GeoGroupDev g, const double* _
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= g.count) return;
     (void)geo_z_one<T, K, false>(g, e, x, u, z, y);
+}
+
+// single-point closest-point groups (PointToRef / ReferenceSurface, K = 1) with G lanes per
+// constraint (bvh_closest_grp)
+template <int T, int G>
+__global__ __launch_bounds__(kBlock) void k_geo_z_cp(GeoGroupDev g, const double* __restrict__ x,
+                                                     const double* __restrict__ u, double* __restrict__ z,
+                                                     double* __restrict__ y, const Ctrl* ctrl) {
+    if (gated(ctrl)) return;
+    __shared__ int stk_i[kBlock / G * kCpStack];
+    __shared__ float stk_d[kBlock / G * kCpStack];
+    const int e = (int)((blockIdx.x * (long long)blockDim.x + threadIdx.x) / G);
+    if (e >= g.count) return;   // whole groups
+    const int q = threadIdx.x / G;
+    (void)geo_z_one<T, 1, false, G>(g, e, x, u, z, y, stk_i + q * kCpStack, stk_d + q * kCpStack);
 }
 
 // GeometrySolver z-update with the residual's block partials; gate 1 = only after a residual
@@ -733,6 +877,19 @@ __global__ __launch_bounds__(kBlock) void k_closest(SurfDev S, const double* __r
     c[3 * (size_t)i] = qx; c[3 * (size_t)i + 1] = qy; c[3 * (size_t)i + 2] = qz;
 }
 
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_closest_grp(SurfDev S, const double* __restrict__ p, double* __restrict__ c, int n) {
+    __shared__ int stk_i[kBlock / G * kCpStack];
+    __shared__ float stk_d[kBlock / G * kCpStack];
+    const int i = (int)((blockIdx.x * (long long)blockDim.x + threadIdx.x) / G);
+    if (i >= n) return;
+    const int q = threadIdx.x / G;
+    double qx, qy, qz;
+    bvh_closest_grp<G>(S, p[3 * (size_t)i], p[3 * (size_t)i + 1], p[3 * (size_t)i + 2], -1, stk_i + q * kCpStack,
+                       stk_d + q * kCpStack, qx, qy, qz);
+    if ((threadIdx.x & (G - 1)) == 0) { c[3 * (size_t)i] = qx; c[3 * (size_t)i + 1] = qy; c[3 * (size_t)i + 2] = qz; }
+}
+
 // test hook: Constraint::project_impl of plane (any k) / angle / edge on transformed points
 template <int K>
 __device__ void test_plane(double* v) { plane_project<K>(v); }
@@ -793,7 +950,26 @@ void launch_geo_z(const GeoGroupDev& g, const double* x, const double* u, double
                   hipStream_t s) {
     if (g.count == 0) return;
     const dim3 grid(blocks_for(g.count));
-    if (g.type == GEO_PLANE && g.K > kGeoMaxK) {
+    // Group traversal only where one lane per query leaves the chip short of waves: below about
+    // 5 waves per SIMD (256 CUs x 4 SIMDs x 64 lanes x 5 = 327 680 queries) the traversal is a
+    // latency chain with nothing to hide it (C3, 101 k queries: z 236 -> 194 us); above, the
+    // single-lane traversal already fills the SIMDs and the group's redundant seed test and
+    // shuffles cost more than they save (C5, 500 k: 493 -> 507 ms per solve). AA_CP_GROUP_MAX
+    // overrides the bound.
+    static const long long cp_max = std::getenv("AA_CP_GROUP_MAX") ? std::atoll(std::getenv("AA_CP_GROUP_MAX")) : 327680;
+    const bool cp = (g.type == GEO_POINT_TO_REF || g.type == GEO_REF_SURFACE) && g.K == 1 && g.surf.wide_g > 0 &&
+                    g.count < cp_max;
+    if (cp) {   // G lanes per query
+        const int G = g.surf.wide_g;
+        const dim3 gg(blocks_for((long long)g.count * G));
+        if (g.type == GEO_POINT_TO_REF) {
+            if (G == 8) hipLaunchKernelGGL((k_geo_z_cp<GEO_POINT_TO_REF, 8>), gg, dim3(kBlock), 0, s, g, x, u, z, y, ctrl);
+            else hipLaunchKernelGGL((k_geo_z_cp<GEO_POINT_TO_REF, 4>), gg, dim3(kBlock), 0, s, g, x, u, z, y, ctrl);
+        } else {
+            if (G == 8) hipLaunchKernelGGL((k_geo_z_cp<GEO_REF_SURFACE, 8>), gg, dim3(kBlock), 0, s, g, x, u, z, y, ctrl);
+            else hipLaunchKernelGGL((k_geo_z_cp<GEO_REF_SURFACE, 4>), gg, dim3(kBlock), 0, s, g, x, u, z, y, ctrl);
+        }
+    } else if (g.type == GEO_PLANE && g.K > kGeoMaxK) {
         hipLaunchKernelGGL(k_geo_z_plane_dyn<false>, grid, dim3(kBlock), 0, s, g, x, u, z, y, ctrl, nullptr, 0, 0);
     } else {
         GEO_DISPATCH(k_geo_z, g, x, u, z, y, ctrl)
@@ -858,7 +1034,9 @@ void launch_geo_restore(double* cu, double* cx, double* aacur, const double* du,
 
 void launch_closest(const SurfDev& sd, const double* p, double* c, int n, hipStream_t s) {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_closest, dim3(blocks_for(n)), dim3(kBlock), 0, s, sd, p, c, n);
+    if (sd.wide_g == 8) hipLaunchKernelGGL(k_closest_grp<8>, dim3(blocks_for(8LL * n)), dim3(kBlock), 0, s, sd, p, c, n);
+    else if (sd.wide_g == 4) hipLaunchKernelGGL(k_closest_grp<4>, dim3(blocks_for(4LL * n)), dim3(kBlock), 0, s, sd, p, c, n);
+    else hipLaunchKernelGGL(k_closest, dim3(blocks_for(n)), dim3(kBlock), 0, s, sd, p, c, n);
     AA_CHECK_LAUNCH();
 }
 

@@ -31,10 +31,18 @@ struct BvhNode {
 __host__ __device__ inline int bvh_skip(const BvhNode& n) { return (int)(n.sn & 0x1fffffffu); }
 __host__ __device__ inline int bvh_count(const BvhNode& n) { return (int)(n.sn >> 29); }
 struct BvhTri { double v[9]; };   // triangle corners, stored in leaf order
+// The same tree collapsed to `wide_g` (4 or 8) children per node for the group traversal
+// (wide_g lanes per query, see bvh_closest_grp): node w's children are the records
+// wide[w * wide_g + k], copies of the BvhNode of a descendant log2(wide_g) levels down (or of a
+// leaf met earlier), with `a` = the child's wide node (inner) or its first triangle (leaf) and
+// sn = triangle count << 29 (0 = inner); unused slots have a = -1. wide_g = 0: not built.
+constexpr int kCpStack = 64;   // per-query traversal stack entries of the group traversal
 struct SurfDev {
     const BvhNode* nodes;
     const BvhTri* tris;
     int n_nodes, n_tris;
+    const BvhNode* wide = nullptr;
+    int wide_g = 0;
 };
 
 // One homogeneous block of constraints (same type / index count / weight / hard-soft).

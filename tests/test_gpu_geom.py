@@ -94,6 +94,33 @@ def test_gpu_geom_matches_oracle(builder, pkg, ctx, oracle):
     g.close()
 
 
+@pytest.mark.parametrize("group", ["4", "8"])
+def test_gpu_closest_point_group_traversal_bit_identical(group, pkg, ctx, monkeypatch):
+    """The group traversal (AA_CP_GROUP lanes per query over the collapsed tree, read when a
+    reference surface is added) returns bvh_closest's triangle and point bit for bit: its tie
+    rule restates the depth-first first-found order. Closest points of the reference's own test
+    surface and whole PQ / wire solves (their warm-started queries) against one lane per query."""
+    d = np.load(os.path.join(GOLDEN, "geom_elements.npz"))
+    scenes = [pkg.geom_scenes.pq_heightfield(48, 48, iters=40, aa_m=10, noise=0.3),
+              pkg.geom_scenes.wire_grid(32, 32, iters=40, aa_m=20)]
+    out = {}
+    for g_ in ("0", group):
+        monkeypatch.setenv("AA_CP_GROUP", g_)
+        g = pkg.capi.GeomSolver(ctx)
+        sid = g.add_ref_surface(d["closest_V"], d["closest_F"])
+        rng = np.random.default_rng(5)
+        P = d["closest_in"]
+        P = np.concatenate([P, P[rng.integers(0, len(P), 4000)] + rng.normal(0, 0.05, (4000, 3))])
+        out[g_] = [g.closest_points(sid, P)]
+        g.close()
+        for sc in scenes:
+            got, gs = pkg.capi.run_geom(ctx, sc)
+            out[g_] += [got["comb"], got["x"]]
+            gs.close()
+    for a, b in zip(out["0"], out[group]):
+        assert np.array_equal(a, b)
+
+
 def test_gpu_geom_deterministic(pkg, ctx):
     sc = pkg.geom_scenes.wire_grid(24, 24, iters=30, aa_m=6)
     a, ga = pkg.capi.run_geom(ctx, sc)
