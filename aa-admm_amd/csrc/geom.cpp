@@ -106,6 +106,48 @@ struct BvhBuilder {
                 }
             if (l > 0) { nd.dlo = down(dl); nd.dhi = up(dh); }
             else { nd.dlo = -FLT_MAX; nd.dhi = FLT_MAX; }   // degenerate patch: no slab bound
+            // tangent axes: the principal directions of the vertices projected on the plane
+            // normal to the (fp32) n, then their ranges (AA_CP_OBB=0: unbounded, slab only)
+            for (int d = 0; d < 3; ++d) { nd.t1[d] = nd.t2[d] = 0.0f; }
+            nd.t1lo = nd.t2lo = -FLT_MAX; nd.t1hi = nd.t2hi = FLT_MAX;
+            static const bool obb = !(std::getenv("AA_CP_OBB") && std::getenv("AA_CP_OBB")[0] == '0');
+            if (l > 0 && obb) {
+                const double n[3] = {nd.nrm[0], nd.nrm[1], nd.nrm[2]};
+                const double nl = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+                const double nn[3] = {n[0] / nl, n[1] / nl, n[2] / nl};
+                // any unit e1 normal to n, e2 = n x e1
+                const int k = std::fabs(nn[0]) < 0.6 ? 0 : (std::fabs(nn[1]) < 0.6 ? 1 : 2);
+                double e1[3] = {0, 0, 0};
+                e1[k] = 1.0;
+                const double pr = e1[0] * nn[0] + e1[1] * nn[1] + e1[2] * nn[2];
+                for (int d = 0; d < 3; ++d) e1[d] -= pr * nn[d];
+                const double el = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+                for (int d = 0; d < 3; ++d) e1[d] /= el;
+                const double e2[3] = {nn[1] * e1[2] - nn[2] * e1[1], nn[2] * e1[0] - nn[0] * e1[2], nn[0] * e1[1] - nn[1] * e1[0]};
+                double m1 = 0, m2 = 0, c11 = 0, c22 = 0, c12 = 0, cnt = 0;
+                for (int i = b; i < e; ++i)
+                    for (int a = 0; a < 3; ++a) {
+                        const double* P = V + 3 * (size_t)F[3 * (size_t)ids[i] + a];
+                        const double x1 = e1[0] * P[0] + e1[1] * P[1] + e1[2] * P[2], x2 = e2[0] * P[0] + e2[1] * P[1] + e2[2] * P[2];
+                        m1 += x1; m2 += x2; c11 += x1 * x1; c22 += x2 * x2; c12 += x1 * x2; cnt += 1;
+                    }
+                m1 /= cnt; m2 /= cnt;
+                c11 = c11 / cnt - m1 * m1; c22 = c22 / cnt - m2 * m2; c12 = c12 / cnt - m1 * m2;
+                const double th = 0.5 * std::atan2(2.0 * c12, c11 - c22);
+                const double a1[3] = {std::cos(th) * e1[0] + std::sin(th) * e2[0], std::cos(th) * e1[1] + std::sin(th) * e2[1],
+                                      std::cos(th) * e1[2] + std::sin(th) * e2[2]};
+                const double a2[3] = {nn[1] * a1[2] - nn[2] * a1[1], nn[2] * a1[0] - nn[0] * a1[2], nn[0] * a1[1] - nn[1] * a1[0]};
+                for (int d = 0; d < 3; ++d) { nd.t1[d] = (float)a1[d]; nd.t2[d] = (float)a2[d]; }
+                double l1 = DBL_MAX, h1 = -DBL_MAX, l2 = DBL_MAX, h2 = -DBL_MAX;
+                for (int i = b; i < e; ++i)
+                    for (int a = 0; a < 3; ++a) {
+                        const double* P = V + 3 * (size_t)F[3 * (size_t)ids[i] + a];
+                        const double x1 = (double)nd.t1[0] * P[0] + (double)nd.t1[1] * P[1] + (double)nd.t1[2] * P[2];
+                        const double x2 = (double)nd.t2[0] * P[0] + (double)nd.t2[1] * P[1] + (double)nd.t2[2] * P[2];
+                        l1 = std::min(l1, x1); h1 = std::max(h1, x1); l2 = std::min(l2, x2); h2 = std::max(h2, x2);
+                    }
+                nd.t1lo = down(l1); nd.t1hi = up(h1); nd.t2lo = down(l2); nd.t2hi = up(h2);
+            }
         }
         const int me = (int)nodes->size();
         if (me >= (1 << 29)) throw Error(ERR_ARG, "add_ref_surface: too many BVH nodes");
@@ -904,6 +946,9 @@ void GeomSolver::solve(const double* init_x3, double rel_residual_eps, int max_i
         passes += next;
     }
     fetch_results();
+#ifdef AA_CP_STATS
+    cp_stats_dump();
+#endif
     if (comm_) {   // every rank ends with the full solution: zero what it does not own, sum
         double* sol = solution_buf();
         auto zero = [&](int q0, int q1) {

@@ -249,11 +249,13 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
     const double ty = py < l1 ? l1 - py : (py > h1 ? py - h1 : 0.0);
     const double tz = pz < l2 ? l2 - pz : (pz > h2 ? pz - h2 : 0.0);
     const double b = tx * tx + ty * ty + tz * tz;
-    // slab lower bound |n.p - [dlo, dhi]| (n unit to fp32 accuracy: shrunk by 1e-6 to stay below)
-    const double dn = (double)nd.nrm[0] * px + (double)nd.nrm[1] * py + (double)nd.nrm[2] * pz;
-    const double lo = nd.dlo, hi = nd.dhi;
-    const double t = dn < lo ? lo - dn : (dn > hi ? dn - hi : 0.0);
-    const double sl = t * t * (1.0 - 1e-6);
+    // oriented-box lower bound: the distances of (n.p, t1.p, t2.p) outside the node's ranges
+    // (the axes are orthonormal to fp32 accuracy: shrunk by 4e-6 to stay below)
+    auto outside = [](double v, float lo, float hi) { return v < lo ? lo - v : (v > hi ? v - hi : 0.0); };
+    const double t = outside((double)nd.nrm[0] * px + (double)nd.nrm[1] * py + (double)nd.nrm[2] * pz, nd.dlo, nd.dhi);
+    const double u1 = outside((double)nd.t1[0] * px + (double)nd.t1[1] * py + (double)nd.t1[2] * pz, nd.t1lo, nd.t1hi);
+    const double u2 = outside((double)nd.t2[0] * px + (double)nd.t2[1] * py + (double)nd.t2[2] * pz, nd.t2lo, nd.t2hi);
+    const double sl = (t * t + u1 * u1 + u2 * u2) * (1.0 - 4e-6);
     return b > sl ? b : sl;
 }
 
@@ -270,6 +272,11 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
 #define AA_BVH_HOLD_PCT 50
 #endif
 
+#ifdef AA_CP_STATS
+// diagnostics build only (-DAA_CP_STATS): per-query traversal counts of bvh_closest
+__device__ unsigned long long g_cp_stats[64];
+#define CP_STAT(i, v) atomicAdd(&g_cp_stats[(i)], (unsigned long long)(v))
+#endif
 // exact closest point on the surface. Stackless depth-first traversal over escape links
 // (`skip` = the node after a subtree): no per-lane stack, so no scratch memory. The upper
 // bound comes from `warm` (the previous iteration's triangle: points move little between ALM
@@ -282,7 +289,17 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
     int best_t = -1;
     cx = px; cy = py; cz = pz;
     if (S.n_nodes == 0) return -1;
+#ifdef AA_CP_STATS
+    unsigned nbox = 0, ntri = 0;
+    double e2s = 0;
+#define CP_BOX() (++nbox)
+#define CP_TRI() (++ntri)
+#else
+#define CP_BOX() ((void)0)
+#define CP_TRI() ((void)0)
+#endif
     auto test_tri = [&](int t) {
+        CP_TRI();
         double qx, qy, qz;
         closest_on_tri(S.tris[t].v, px, py, pz, qx, qy, qz);
         const double d2 = dist2(px, py, pz, qx, qy, qz);
@@ -294,6 +311,9 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         const double* v = S.tris[warm].v;
         const double e2 = (v[3] - v[0]) * (v[3] - v[0]) + (v[4] - v[1]) * (v[4] - v[1]) + (v[5] - v[2]) * (v[5] - v[2]);
         tight = best <= AA_WARM_TIGHT * e2;
+#ifdef AA_CP_STATS
+        e2s = e2;
+#endif
     }
     if (!tight)
     {   // greedy descent to the nearest-box leaf: a tight bound even when the point slid far
@@ -307,6 +327,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
                 break;
             }
             const double dl = box_d2(S.nodes[i + 1], px, py, pz), dr = box_d2(S.nodes[nd.a], px, py, pz);
+            CP_BOX(); CP_BOX();
             i = dl <= dr ? i + 1 : nd.a;
         }
     }
@@ -327,6 +348,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         for (;;) {
             if (!done && hold_a < 0) {
                 const BvhNode nd = S.nodes[i];
+                CP_BOX();
                 if (box_d2(nd, px, py, pz) < best) {
                     const int nc = bvh_count(nd);
                     if (nc > 0) { hold_a = nd.a; hold_n = nc; i = bvh_skip(nd); }
@@ -351,6 +373,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
 #else
     while (i < S.n_nodes) {
         const BvhNode nd = S.nodes[i];
+        CP_BOX();
         if (box_d2(nd, px, py, pz) < best) {
             const int nc = bvh_count(nd);
             if (nc > 0) {
@@ -365,6 +388,17 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         }
     }
 #endif
+#ifdef AA_CP_STATS
+    {
+        auto lg = [](double v) { int b = 0; while (v >= 2.0 && b < 15) { v *= 0.5; ++b; } return b; };
+        CP_STAT(0, 1); CP_STAT(1, nbox); CP_STAT(2, ntri); CP_STAT(3, tight ? 1 : 0); CP_STAT(4, best_t != warm ? 1 : 0);
+        CP_STAT(8 + lg((double)nbox), 1);
+        // distance / warm edge length, log2 buckets from 2^-12
+        if (e2s > 0) { double r = sqrt(best / e2s) * 4096.0; CP_STAT(24 + lg(r), 1); }
+    }
+#endif
+#undef CP_BOX
+#undef CP_TRI
     return best_t;
 }
 
@@ -1031,6 +1065,21 @@ void launch_geo_restore(double* cu, double* cx, double* aacur, const double* du,
     hipLaunchKernelGGL(k_geo_restore, dim3(grid_for(nu + nx)), dim3(kBlock), 0, s, cu, cx, aacur, du, dx, nu, nx, ctrl);
     AA_CHECK_LAUNCH();
 }
+
+#ifdef AA_CP_STATS
+void cp_stats_dump() {
+    unsigned long long h[64];
+    AA_HIP(hipDeviceSynchronize());
+    AA_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cp_stats), sizeof(h)));
+    fprintf(stderr, "CP_STATS queries %llu box %llu tri %llu tight %llu moved %llu\nCP_BOX_HIST", h[0], h[1], h[2], h[3], h[4]);
+    for (int i = 0; i < 16; ++i) fprintf(stderr, " %llu", h[8 + i]);
+    fprintf(stderr, "\nCP_DIST_HIST");
+    for (int i = 0; i < 16; ++i) fprintf(stderr, " %llu", h[24 + i]);
+    fprintf(stderr, "\n");
+    const unsigned long long z[64] = {};
+    AA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_cp_stats), z, sizeof(z)));
+}
+#endif
 
 void launch_closest(const SurfDev& sd, const double* p, double* c, int n, hipStream_t s) {
     if (n == 0) return;

@@ -22,12 +22,19 @@ constexpr int kGeoMaxK = 8;   // planes up to this valence run in registers; lar
 // normal n and the range [dlo, dhi] of n . v over its vertices (rounded outward). The slab
 // bounds the distance to every triangle of the subtree from below like the box does, and is
 // far tighter for sloped, thin patches seen from afar (a point well off the surface).
-struct BvhNode {
+// With the two tangent axes t1, t2 (principal directions of the subtree's vertices in the plane
+// normal to n) and their ranges the slab becomes an oriented box: a point far above a flat
+// patch has the same normal distance to every patch around its foot point, and only the
+// tangent ranges tell those patches apart. 128 B, one cache line.
+struct alignas(128) BvhNode {
     float lo[3], hi[3];
     int a;
     unsigned sn;
-    float nrm[3], dlo, dhi, pad[3];
+    float nrm[3], dlo, dhi;
+    float t1[3], t1lo, t1hi;
+    float t2[3], t2lo, t2hi;
 };
+static_assert(sizeof(BvhNode) == 128, "BvhNode is one 128-B line");
 __host__ __device__ inline int bvh_skip(const BvhNode& n) { return (int)(n.sn & 0x1fffffffu); }
 __host__ __device__ inline int bvh_count(const BvhNode& n) { return (int)(n.sn >> 29); }
 struct BvhTri { double v[9]; };   // triangle corners, stored in leaf order
@@ -93,6 +100,9 @@ void launch_geo_restore(double* cu, double* cx, double* aacur, const double* du,
                         long long nx, const Ctrl* ctrl, hipStream_t s);
 // closest points of `n` points (test hook / soft-energy evaluation)
 void launch_closest(const SurfDev& sd, const double* p, double* c, int n, hipStream_t s);
+#ifdef AA_CP_STATS
+void cp_stats_dump();   // diagnostics build: print and reset the traversal counters
+#endif
 
 // test hook (aa_test_geom_project): project_impl of n constraints of one type on transformed points
 void launch_test_geo_project(int type, int k, const double* prm2, const double* in, int n, double* out, hipStream_t s);
