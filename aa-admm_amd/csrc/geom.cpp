@@ -62,6 +62,8 @@ struct BvhBuilder {
     std::vector<double> cen;
     std::vector<BvhNode>* nodes;
     std::vector<BvhTri>* tris;
+    int leaf = 4;            // triangles per leaf (AA_CP_LEAF, 1..7)
+    bool split_t1 = false;   // split along the principal tangent axis (AA_CP_SPLIT=t1)
     static float down(double v) {   // largest float <= v
         float f = (float)v;
         if ((double)f > v) f = std::nextafter(f, -INFINITY);
@@ -152,7 +154,7 @@ struct BvhBuilder {
         const int me = (int)nodes->size();
         if (me >= (1 << 29)) throw Error(ERR_ARG, "add_ref_surface: too many BVH nodes");
         nodes->push_back(nd);
-        if (e - b <= 4) {
+        if (e - b <= leaf) {
             (*nodes)[me].a = (int)tris->size();
             (*nodes)[me].sn = (unsigned)(me + 1) | ((unsigned)(e - b) << 29);
             for (int i = b; i < e; ++i) {
@@ -163,11 +165,17 @@ struct BvhBuilder {
             }
             return me;
         }
-        int ax = 0;
-        for (int d = 1; d < 3; ++d) if (chi[d] - clo[d] > chi[ax] - clo[ax]) ax = d;
         const int mid = (b + e) / 2;
-        std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e,
-                         [&](int p, int q) { return cen[3 * (size_t)p + ax] < cen[3 * (size_t)q + ax]; });
+        if (split_t1 && (nd.t1hi - nd.t1lo) < FLT_MAX) {   // median along the principal tangent axis
+            const double a1[3] = {nd.t1[0], nd.t1[1], nd.t1[2]};
+            auto key = [&](int p) { return a1[0] * cen[3 * (size_t)p] + a1[1] * cen[3 * (size_t)p + 1] + a1[2] * cen[3 * (size_t)p + 2]; };
+            std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e, [&](int p, int q) { return key(p) < key(q); });
+        } else {   // median along the longest axis of the centroids' box
+            int ax = 0;
+            for (int d = 1; d < 3; ++d) if (chi[d] - clo[d] > chi[ax] - clo[ax]) ax = d;
+            std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e,
+                             [&](int p, int q) { return cen[3 * (size_t)p + ax] < cen[3 * (size_t)q + ax]; });
+        }
         build(b, mid);
         const int r = build(mid, e);
         (*nodes)[me].a = r;
@@ -247,6 +255,8 @@ int GeomSolver::add_ref_surface(const double* V3, int nv, const int* F3, int nf)
             B.cen[3 * (size_t)t + d] = (V3[3 * (size_t)F3[3 * t] + d] + V3[3 * (size_t)F3[3 * t + 1] + d] + V3[3 * (size_t)F3[3 * t + 2] + d]) / 3.0;
     B.nodes = &S.nodes;
     B.tris = &S.tris;
+    if (const char* ev = std::getenv("AA_CP_LEAF")) B.leaf = std::min(7, std::max(1, std::atoi(ev)));
+    if (const char* ev = std::getenv("AA_CP_SPLIT")) B.split_t1 = std::string(ev) == "t1";
     S.nodes.reserve(nf);
     S.tris.reserve(nf);
     B.build(0, nf);

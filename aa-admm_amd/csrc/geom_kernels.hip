@@ -248,7 +248,11 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
     const double tx = px < l0 ? l0 - px : (px > h0 ? px - h0 : 0.0);
     const double ty = py < l1 ? l1 - py : (py > h1 ? py - h1 : 0.0);
     const double tz = pz < l2 ? l2 - pz : (pz > h2 ? pz - h2 : 0.0);
+#ifdef AA_CP_NO_AABB
+    const double b = 0.0 * (tx + ty + tz);
+#else
     const double b = tx * tx + ty * ty + tz * tz;
+#endif
     // oriented-box lower bound: the distances of (n.p, t1.p, t2.p) outside the node's ranges
     // (the axes are orthonormal to fp32 accuracy: shrunk by 4e-6 to stay below)
     auto outside = [](double v, float lo, float hi) { return v < lo ? lo - v : (v > hi ? v - hi : 0.0); };
@@ -462,10 +466,11 @@ __device__ int bvh_closest_grp(const SurfDev& S, double px, double py, double pz
             const int ak = __shfl(rec.a, src), nk = __shfl(cnt, src);
             double qd = INFINITY, qx = 0, qy = 0, qz = 0;
             int qt = 0x7fffffff;
-            if (j < nk) {
-                qt = ak + j;
-                closest_on_tri(S.tris[qt].v, px, py, pz, qx, qy, qz);
-                qd = dist2(px, py, pz, qx, qy, qz);
+            for (int k = j; k < nk; k += G) {   // ascending index: strict < keeps the first
+                double rx, ry, rz;
+                closest_on_tri(S.tris[ak + k].v, px, py, pz, rx, ry, rz);
+                const double rd = dist2(px, py, pz, rx, ry, rz);
+                if (rd < qd) { qd = rd; qt = ak + k; qx = rx; qy = ry; qz = rz; }
             }
 #pragma unroll
             for (int off = G / 2; off > 0; off >>= 1) {
