@@ -263,6 +263,39 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
     return b > sl ? b : sl;
 }
 
+// The same lower bound in fp32 arithmetic for the traversal's prune tests (AA_CP_F32=1, the
+// default): the query is rounded to fp32 once, and every per-axis distance is shrunk by
+// eps = 8 u (|qx| + |qy| + |qz|) (u = 2^-24), which covers the rounding of the query and of the
+// fp32 dot products (|n_i| <= 1), so the bound stays below the true distance -- it only prunes
+// less. No conversions per node, half the registers per operand. The greedy descent keeps the
+// fp64 bound: its left / right choice picks the seed triangle, which decides ties. Single-lane
+// traversal only (C5 z 1 366 -> 1 195 us); the group traversal measured slower with it (C3).
+#ifndef AA_CP_F32
+#define AA_CP_F32 1
+#endif
+struct QueryF { float x, y, z, eps; };
+__device__ __forceinline__ QueryF query_f(double px, double py, double pz) {
+    QueryF q;
+    q.x = (float)px; q.y = (float)py; q.z = (float)pz;
+    q.eps = 8.0f * 5.9604645e-8f * 1.0001f * (fabsf(q.x) + fabsf(q.y) + fabsf(q.z));
+    return q;
+}
+__device__ __forceinline__ double box_d2f(const BvhNode& nd, const QueryF& q) {
+    auto outside = [&](float v, float lo, float hi) { return fmaxf(fmaxf(fmaxf(lo - v, v - hi), 0.0f) - q.eps, 0.0f); };
+    const float tx = outside(q.x, nd.lo[0], nd.hi[0]), ty = outside(q.y, nd.lo[1], nd.hi[1]),
+                tz = outside(q.z, nd.lo[2], nd.hi[2]);
+    const float t = outside(nd.nrm[0] * q.x + nd.nrm[1] * q.y + nd.nrm[2] * q.z, nd.dlo, nd.dhi);
+    const float u1 = outside(nd.t1[0] * q.x + nd.t1[1] * q.y + nd.t1[2] * q.z, nd.t1lo, nd.t1hi);
+    const float u2 = outside(nd.t2[0] * q.x + nd.t2[1] * q.y + nd.t2[2] * q.z, nd.t2lo, nd.t2hi);
+    const float b = tx * tx + ty * ty + tz * tz, sl = t * t + u1 * u1 + u2 * u2;
+    return (double)fmaxf(b, sl) * (1.0 - 4e-6);   // fp32 squares and sums: a few ulp
+}
+#if AA_CP_F32
+#define CP_PRUNE_BOUND(nd) box_d2f((nd), Q)
+#else
+#define CP_PRUNE_BOUND(nd) box_d2((nd), px, py, pz)
+#endif
+
 // (warm distance / warm triangle's first edge)^2 up to which the warm bound is used alone: the
 // greedy root-to-leaf descent (a chain of dependent node loads) only runs for points that slid
 // farther than ~8 edges from their previous triangle (and on cold starts). Measured (round 2):
@@ -336,6 +369,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         }
     }
     const int seed = best_t;
+    [[maybe_unused]] const QueryF Q = query_f(px, py, pz);
     int i = 0;
 #if AA_BVH_HOLD_PCT > 0
     // Two-phase ("while-while") schedule of the same per-lane traversal: a lane that reaches a
@@ -353,7 +387,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
             if (!done && hold_a < 0) {
                 const BvhNode nd = S.nodes[i];
                 CP_BOX();
-                if (box_d2(nd, px, py, pz) < best) {
+                if (CP_PRUNE_BOUND(nd) < best) {
                     const int nc = bvh_count(nd);
                     if (nc > 0) { hold_a = nd.a; hold_n = nc; i = bvh_skip(nd); }
                     else i = i + 1;
@@ -378,7 +412,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
     while (i < S.n_nodes) {
         const BvhNode nd = S.nodes[i];
         CP_BOX();
-        if (box_d2(nd, px, py, pz) < best) {
+        if (CP_PRUNE_BOUND(nd) < best) {
             const int nc = bvh_count(nd);
             if (nc > 0) {
                 for (int t = nd.a; t < nd.a + nc; ++t)
@@ -458,7 +492,7 @@ __device__ int bvh_closest_grp(const SurfDev& S, double px, double py, double pz
         const BvhNode rec = S.wide[(size_t)cur * G + j];
         const bool valid = rec.a >= 0;
         const int cnt = bvh_count(rec);
-        const double d = valid ? box_d2(rec, px, py, pz) : INFINITY;
+        const double d = valid ? box_d2(rec, px, py, pz) : INFINITY;   // fp64 here: measured faster (C3)
         // leaf children: one after the other, a triangle per lane, group arg-min by (distance, index)
         for (unsigned long long lm = __ballot(valid && cnt > 0 && d <= best) & gm; lm; lm &= lm - 1) {
             const int src = __ffsll((long long)lm) - 1;
