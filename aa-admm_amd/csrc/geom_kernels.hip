@@ -433,6 +433,20 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
         CP_STAT(8 + lg((double)nbox), 1);
         // distance / warm edge length, log2 buckets from 2^-12
         if (e2s > 0) { double r = sqrt(best / e2s) * 4096.0; CP_STAT(24 + lg(r), 1); }
+        // oracle: the same walk started with the final distance as the bound (what a perfect
+        // seed would leave to test)
+        unsigned ob = 0, ot = 0;
+        for (int k = 0; k < S.n_nodes;) {
+            const BvhNode nd = S.nodes[k];
+            ++ob;
+            if (CP_PRUNE_BOUND(nd) < best) {
+                const int nc = bvh_count(nd);
+                if (nc > 0) { ot += nc; k = bvh_skip(nd); } else k = k + 1;
+            } else {
+                k = bvh_skip(nd);
+            }
+        }
+        CP_STAT(40, ob); CP_STAT(41, ot);
     }
 #endif
 #undef CP_BOX
@@ -1114,7 +1128,7 @@ void cp_stats_dump() {
     for (int i = 0; i < 16; ++i) fprintf(stderr, " %llu", h[8 + i]);
     fprintf(stderr, "\nCP_DIST_HIST");
     for (int i = 0; i < 16; ++i) fprintf(stderr, " %llu", h[24 + i]);
-    fprintf(stderr, "\n");
+    fprintf(stderr, "\nCP_ORACLE box %llu tri %llu\n", h[40], h[41]);
     const unsigned long long z[64] = {};
     AA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_cp_stats), z, sizeof(z)));
 }
