@@ -76,10 +76,12 @@ for step in "$@"; do
       cfg=$1; tag=$2; ctrs=$3; shift; shift; shift
       for grp in ${ctrs//;/ }; do
         d="$R/gpurun_out/pmc_${tag}_${cfg}_${grp//,/_}"
+        [ -n "${PMC_KERNEL:-}" ] && d="/tmp/pmc_${tag}_${cfg}_${grp//,/_}"   # raw CSVs stay on the box
         (cd /tmp && TMPDIR=/tmp timeout -k 10 -s KILL 300 rocprofv3 --pmc ${grp//,/ } --output-format csv -d "$d" -o run -- \
           python3 "$R/bench.py" --config $cfg --steps 1 --warmup 0 --iters ${ITERS:-10} --no-cpu-baseline --eps-steps 0 \
           --no-secondary --geom-eps-solves 0 "$@" > "$d.log" 2>&1); rc=$?
         echo "pmc $grp rc=$rc"; [ $rc -ne 0 ] && grep -v "^ *@" "$d.log" | tail -5; fatal $rc "pmc $grp"
+        [ -n "${PMC_KERNEL:-}" ] && python3 tools/pmc_sum.py "$d" "$PMC_KERNEL" "gpurun_out/pmc_${tag}_${cfg}.json"
       done ;;
     prof)
       cfg=$1; tag=$2; shift; shift; d="$R/gpurun_out/prof_${tag}_$cfg"
