@@ -243,11 +243,15 @@ __device__ __forceinline__ void closest_on_tri(const double* t, double px, doubl
     cx = fma(acx, w, fma(abx, v, ax)); cy = fma(acy, w, fma(aby, v, ay)); cz = fma(acz, w, fma(abz, v, az));
 }
 
+// Branch-free: max(lo - v, v - hi, 0) is the distance outside [lo, hi] bit for bit (one of the two
+// differences is positive at most, and it is the one the comparisons would pick). The ternary
+// form compiled to branches with each field's load sunk into its branch -- a load and a wait per
+// field, serialised -- which made the greedy descent (a third of C5's queries) a long chain.
 __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py, double pz) {
     const double l0 = nd.lo[0], l1 = nd.lo[1], l2 = nd.lo[2], h0 = nd.hi[0], h1 = nd.hi[1], h2 = nd.hi[2];
-    const double tx = px < l0 ? l0 - px : (px > h0 ? px - h0 : 0.0);
-    const double ty = py < l1 ? l1 - py : (py > h1 ? py - h1 : 0.0);
-    const double tz = pz < l2 ? l2 - pz : (pz > h2 ? pz - h2 : 0.0);
+    const double tx = fmax(fmax(l0 - px, px - h0), 0.0);
+    const double ty = fmax(fmax(l1 - py, py - h1), 0.0);
+    const double tz = fmax(fmax(l2 - pz, pz - h2), 0.0);
 #ifdef AA_CP_NO_AABB
     const double b = 0.0 * (tx + ty + tz);
 #else
@@ -255,7 +259,7 @@ __device__ __forceinline__ double box_d2(const BvhNode& nd, double px, double py
 #endif
     // oriented-box lower bound: the distances of (n.p, t1.p, t2.p) outside the node's ranges
     // (the axes are orthonormal to fp32 accuracy: shrunk by 4e-6 to stay below)
-    auto outside = [](double v, float lo, float hi) { return v < lo ? lo - v : (v > hi ? v - hi : 0.0); };
+    auto outside = [](double v, float lo, float hi) { return fmax(fmax((double)lo - v, v - (double)hi), 0.0); };
     const double t = outside((double)nd.nrm[0] * px + (double)nd.nrm[1] * py + (double)nd.nrm[2] * pz, nd.dlo, nd.dhi);
     const double u1 = outside((double)nd.t1[0] * px + (double)nd.t1[1] * py + (double)nd.t1[2] * pz, nd.t1lo, nd.t1hi);
     const double u2 = outside((double)nd.t2[0] * px + (double)nd.t2[1] * py + (double)nd.t2[2] * pz, nd.t2lo, nd.t2hi);
@@ -363,7 +367,8 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
                 for (int t = nd.a; t < nd.a + bvh_count(nd); ++t) test_tri(t);
                 break;
             }
-            const double dl = box_d2(S.nodes[i + 1], px, py, pz), dr = box_d2(S.nodes[nd.a], px, py, pz);
+            const BvhNode cl = S.nodes[i + 1], cr = S.nodes[nd.a];   // both children's loads issued together
+            const double dl = box_d2(cl, px, py, pz), dr = box_d2(cr, px, py, pz);
             CP_BOX(); CP_BOX();
             i = dl <= dr ? i + 1 : nd.a;
         }
@@ -496,7 +501,8 @@ __device__ int bvh_closest_grp(const SurfDev& S, double px, double py, double pz
                 for (int t = nd.a; t < nd.a + bvh_count(nd); ++t) test_tri(t);
                 break;
             }
-            const double dl = box_d2(S.nodes[i + 1], px, py, pz), dr = box_d2(S.nodes[nd.a], px, py, pz);
+            const BvhNode cl = S.nodes[i + 1], cr = S.nodes[nd.a];   // both children's loads issued together
+            const double dl = box_d2(cl, px, py, pz), dr = box_d2(cr, px, py, pz);
             i = dl <= dr ? i + 1 : nd.a;
         }
     }
