@@ -117,18 +117,37 @@ __device__ __forceinline__ void write_slots(const GroupDev& g, int e, int nf, do
     double yc[3 * NC];
 #pragma unroll
     for (int i = 0; i < 3 * NC; ++i) yc[i] = w * (w * zz[i] - w * Cp[i] - uu[i]);
+    // every load before the per-node branch: a load inside `if (pos >= 0)` is issued only after
+    // the branch resolves, i.e. after a wait on pos (one serialised round trip per node)
+    int pos[NV];
+    double gk[NC * NV];
+#pragma unroll
+    for (int a = 0; a < NV; ++a) pos[a] = g.spos[(size_t)a * g.count + e];
+#pragma unroll
+    for (int k = 0; k < NC * NV; ++k) gk[k] = g.G[(size_t)k * g.count + e];
 #pragma unroll
     for (int a = 0; a < NV; ++a) {
-        const int pos = g.spos[(size_t)a * g.count + e];
-        if (pos < 0) continue;   // pinned: no rhs row
+        if (pos[a] < 0) continue;   // pinned: no rhs row
         double f0 = 0, f1 = 0, f2 = 0;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
+            const double gc = gk[c * NV + a];
             f0 += gc * yc[3 * c]; f1 += gc * yc[3 * c + 1]; f2 += gc * yc[3 * c + 2];
         }
-        double* o = y + 3 * (size_t)pos;
+        double* o = y + 3 * (size_t)pos[a];
         o[0] = f0; o[1] = f1; o[2] = f2;
+    }
+}
+
+// u of an element (0 without u): the null test outside the loads, so they issue together
+template <int D>
+__device__ __forceinline__ void load_u(const GroupDev& g, int e, const double* __restrict__ u, double* uu) {
+    if (u) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) uu[i] = u[g.zoff + (size_t)i * g.count + e];
+    } else {
+#pragma unroll
+        for (int i = 0; i < D; ++i) uu[i] = 0.0;
     }
 }
 
@@ -147,11 +166,9 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
         double F[D], Cp[D], uu[D], vin[D], zz[D];
         gather_F<NV>(g, e, xfull, nf, F, Cp);
         const double w = g.w[e];
+        load_u<D>(g, e, u, uu);
 #pragma unroll
-        for (int i = 0; i < D; ++i) {
-            uu[i] = u ? u[g.zoff + (size_t)i * g.count + e] : 0.0;
-            vin[i] = F[i] + uu[i] / w;
-        }
+        for (int i = 0; i < D; ++i) vin[i] = F[i] + uu[i] / w;
         if constexpr (NV == 1) {
             // the (u,x) variant's candidate exactly as EnergyTerm::update_z forms it for an identity
             // row (EnergyTerm.hpp:166-178: z = W^-1 (W x + u - c), W^-1 stored as 1/w): the
@@ -231,8 +248,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
         if (y) {
             double F[D], Cp[D], uu[D];
             gather_F<NV>(g, e, xfull, nf, F, Cp);
-#pragma unroll
-            for (int i = 0; i < D; ++i) uu[i] = u ? u[g.zoff + (size_t)i * g.count + e] : 0.0;
+            load_u<D>(g, e, u, uu);
             write_slots<NV>(g, e, nf, g.w[e], x, Cp, uu, y);
         }
     };
@@ -261,9 +277,11 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
                     double F[D], Cp[D];
                     gather_F<NV>(g, e, xfull, nf, F, Cp);
                     const double w = g.w[e];
+                    double uu[D];
+                    load_u<D>(g, e, u, uu);
 #pragma unroll
                     for (int i = 0; i < D; ++i) {
-                        v[i] = F[i] + (u ? u[g.zoff + (size_t)i * g.count + e] : 0.0) / w;
+                        v[i] = F[i] + uu[i] / w;
                         x[i] = v[i];
                     }
                     vol = g.vol[e];
@@ -355,8 +373,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hqa(GroupDev g, const double
                     }
                 }
             }
-#pragma unroll
-            for (int i = 0; i < D; ++i) uu[i] = u ? u[g.zoff + (size_t)i * g.count + e] : 0.0;
+            load_u<D>(g, e, u, uu);
             write_slots<NV>(g, e, nf, g.w[e], x, Cp, uu, y);
         }
     };
@@ -376,9 +393,11 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hqa(GroupDev g, const double
             }
         }
         const double w = g.w[e];
+        double uu[D];
+        load_u<D>(g, e, u, uu);
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            v[i] = F[i] + (u ? u[g.zoff + (size_t)i * g.count + e] : 0.0) / w;
+            v[i] = F[i] + uu[i] / w;
             x[i] = v[i];
         }
         vol = g.vol[e];
@@ -560,13 +579,18 @@ __global__ __launch_bounds__(kBlock) void k_prim_z(GroupDev g, const double* __r
         double F[D];
         gather_P<NV>(g, e, xfull, F);
         const double w = g.w[e];
+        double zi[D], zr[D];   // all loads first (a load under `if (zref)` waited per entry)
+#pragma unroll
+        for (int i = 0; i < D; ++i) zi[i] = z[g.zoff + (size_t)i * g.count + e];
+        if (zref) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) zr[i] = zref[g.zoff + (size_t)i * g.count + e];
+        }
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const size_t o = g.zoff + (size_t)i * g.count + e;
-            const double zi = z[o];
-            const double r = w * (F[i] - zi);
+            const double r = w * (F[i] - zi[i]);
             pa += r * r;
-            if (zref) { const double d = w * (zi - zref[o]); pb += d * d; }
+            if (zref) { const double d = w * (zi[i] - zr[i]); pb += d * d; }
         }
     }
     const double sa = block_sum(pa, sm);
