@@ -885,8 +885,10 @@ __device__ __forceinline__ double ld_h(const double* p) {
     return *p;
 #endif
 }
-__device__ __forceinline__ double seg_get(const Seg2& s, long long i) { return i < s.na ? s.a[i] : s.b[i - s.na]; }
-__device__ __forceinline__ void seg_set(const Seg2& s, long long i, double v) { if (i < s.na) s.a[i] = v; else s.b[i - s.na] = v; }
+// the segment is picked by address, not by branch (a load in each arm of a branch is issued only
+// once the branch resolves, behind the loads before it)
+__device__ __forceinline__ double seg_get(const Seg2& s, long long i) { return *(i < s.na ? s.a + i : s.b + (i - s.na)); }
+__device__ __forceinline__ void seg_set(const Seg2& s, long long i, double v) { *(i < s.na ? s.a + i : s.b + (i - s.na)) = v; }
 
 // pass 1: the partial sums for |dF_j|^2, dF_j.F, dF_j.dF_c, dF_c.F with dF_j = dF_j + F formed on
 // the fly (read only: k_aa_mix forms dF_j + F and dG_j + G again and stores them, so the history

@@ -360,9 +360,10 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
     {   // greedy descent to the nearest-box leaf: a tight bound even when the point slid far
         // from its previous triangle (the warm bound alone then lets the traversal open every
         // box within that distance)
+        // the chosen child's record comes with the pair just loaded: one dependent load per level
         int i = 0;
+        BvhNode nd = S.nodes[0];
         for (;;) {
-            const BvhNode& nd = S.nodes[i];
             if (bvh_count(nd) > 0) {
                 for (int t = nd.a; t < nd.a + bvh_count(nd); ++t) test_tri(t);
                 break;
@@ -370,7 +371,7 @@ __device__ int bvh_closest(const SurfDev& S, double px, double py, double pz, in
             const BvhNode cl = S.nodes[i + 1], cr = S.nodes[nd.a];   // both children's loads issued together
             const double dl = box_d2(cl, px, py, pz), dr = box_d2(cr, px, py, pz);
             CP_BOX(); CP_BOX();
-            i = dl <= dr ? i + 1 : nd.a;
+            if (dl <= dr) { i = i + 1; nd = cl; } else { i = nd.a; nd = cr; }
         }
     }
     const int seed = best_t;
@@ -495,15 +496,15 @@ __device__ int bvh_closest_grp(const SurfDev& S, double px, double py, double pz
     }
     if (!tight) {
         int i = 0;
+        BvhNode nd = S.nodes[0];
         for (;;) {
-            const BvhNode& nd = S.nodes[i];
             if (bvh_count(nd) > 0) {
                 for (int t = nd.a; t < nd.a + bvh_count(nd); ++t) test_tri(t);
                 break;
             }
             const BvhNode cl = S.nodes[i + 1], cr = S.nodes[nd.a];   // both children's loads issued together
             const double dl = box_d2(cl, px, py, pz), dr = box_d2(cr, px, py, pz);
-            i = dl <= dr ? i + 1 : nd.a;
+            if (dl <= dr) { i = i + 1; nd = cl; } else { i = nd.a; nd = cr; }
         }
     }
     const int t0 = best_t;
