@@ -38,9 +38,25 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
 }
 
 // deterministic block sum of red[0..nb) visible to every thread (same order in every block)
-__device__ __forceinline__ double block_sum_all(const double* red, int nb, double* sm) {
+// a thread's share of nb partials, summed in index order; loads issued 8 at a time (a thread
+// strides through ~15 partials on C4: one round trip each when loaded one by one)
+__device__ __forceinline__ double thread_sum_strided(const double* red, int nb) {
     double a = 0;
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) a += red[i];
+    int i = threadIdx.x;
+    const int st = blockDim.x;
+    for (; i + 7 * st < nb; i += 8 * st) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = red[i + q * st];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a += v[q];
+    }
+    for (; i < nb; i += st) a += red[i];
+    return a;
+}
+
+__device__ __forceinline__ double block_sum_all(const double* red, int nb, double* sm) {
+    double a = thread_sum_strided(red, nb);
     a = block_sum(a, sm);
     if (threadIdx.x == 0) sm[0] = a;
     __syncthreads();
@@ -708,8 +724,7 @@ __global__ __launch_bounds__(kCtlBlock) void k_control(int op, Ctrl* ctrl, const
                                                     int* hist_rej) {
     if (ctrl->done) return;
     __shared__ double sm[kCtlBlock / 64];
-    double a = 0, b = 0;
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) { a += red_a[i]; if (red_b) b += red_b[i]; }
+    double a = thread_sum_strided(red_a, nb), b = red_b ? thread_sum_strided(red_b, nb) : 0.0;
     a = block_sum(a, sm);
     b = block_sum(b, sm);
     if (threadIdx.x != 0) return;

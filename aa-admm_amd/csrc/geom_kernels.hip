@@ -41,6 +41,22 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
 
 __device__ __forceinline__ bool gated(const Ctrl* c) { return c && c->done; }
 
+// a thread's share of nb partials in index order, loads issued 8 at a time (as in elastic_kernels)
+__device__ __forceinline__ double thread_sum_strided(const double* red, int nb) {
+    double a = 0;
+    int i = threadIdx.x;
+    const int st = blockDim.x;
+    for (; i + 7 * st < nb; i += 8 * st) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = red[i + q * st];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a += v[q];
+    }
+    for (; i < nb; i += st) a += red[i];
+    return a;
+}
+
 // ------------------------------------------------------------------ transforms (Constraint.h:73-94)
 // out: 3*cols values, column-major (column c at out[3c..3c+2])
 template <int T, int K>
@@ -886,8 +902,7 @@ __global__ __launch_bounds__(kBlock) void k_geo_control(Ctrl* ctrl, const double
                                                         double* hist_comb, unsigned long long* hist_clock) {
     if (ctrl->done) return;
     __shared__ double sm[kBlock / 64];
-    double a = 0;
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) a += red[i];
+    double a = thread_sum_strided(red, nb);
     a = block_sum(a, sm);
     if (threadIdx.x != 0) return;
     const double comb = a;
@@ -929,8 +944,7 @@ __global__ __launch_bounds__(kBlock) void k_plain_control(Ctrl* ctrl, const doub
                                                           double* hist_comb, unsigned long long* hist_clock) {
     if (ctrl->done || (op == 1 && !ctrl->reject)) return;
     __shared__ double sm[kBlock / 64];
-    double a = 0;
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) a += red[i];
+    double a = thread_sum_strided(red, nb);
     a = block_sum(a, sm);
     if (threadIdx.x != 0) return;
     const double res = sqrt(a);
