@@ -1631,7 +1631,8 @@ void launch_finalize(int n, int nf, const double* xsrc, const double* xfull, dou
 }
 
 int aa_reduce_blocks(long long dim) {   // more partials only pay off on large vectors (k_aa_solve sums them)
-    const int cap = dim > (4LL << 20) ? 2048 : 512;
+    static const int cap_env = std::getenv("AA_AA_BLOCKS") ? std::atoi(std::getenv("AA_AA_BLOCKS")) : 0;
+    const int cap = cap_env > 0 ? cap_env : (dim > (4LL << 20) ? 2048 : 512);
     return grid_for(dim) < cap ? grid_for(dim) : cap;
 }
 
