@@ -546,6 +546,8 @@ __global__ __launch_bounds__(kBlock) void k_u_and_y(GroupDev g, const double* __
     // temporaries and the gathered G / P x never hold registers together
     double F[D], Cp[D], zz[D], uu[D];
     const double w = g.w[e];
+    // the element volume with the other loads (loaded where it is used, it waited alone mid-gradient)
+    const double vol = (NV == 4 && mode == 1) ? g.vol[e] : 0.0;
 #pragma unroll
     for (int i = 0; i < D; ++i) zz[i] = z[g.zoff + (size_t)i * g.count + e];
     if (mode != 1) {
@@ -560,11 +562,11 @@ __global__ __launch_bounds__(kBlock) void k_u_and_y(GroupDev g, const double* __
 #pragma unroll
             for (int i = 0; i < D; ++i) gr[i] = 0;
         } else if constexpr (HYPER == 0) {
-            dev::tet_linear_grad(zz, g.k * g.vol[e], gr);
+            dev::tet_linear_grad(zz, g.k * vol, gr);
         } else {
             dev::hyper_psi_grad(g.mat, g.mu, g.lambda, zz, gr);
 #pragma unroll
-            for (int i = 0; i < D; ++i) gr[i] *= g.vol[e];
+            for (int i = 0; i < D; ++i) gr[i] *= vol;
         }
 #pragma unroll
         for (int i = 0; i < D; ++i) uu[i] = gr[i] / w;
@@ -694,7 +696,7 @@ __global__ __launch_bounds__(kBlock) void k_rhs_slots(int nf, const int* __restr
     const int c = lane % 3;
     if (i >= nf) return;
     const size_t o = 3 * (size_t)i + c;
-    if (xlast) xlast[o] = xsrc[o];   // last_x = curr_x (Solver.cpp:170)
+    const double mx = Mxbar[o];   // issued with the run bounds, not after the sum
     double sum = 0;
     const int k0 = ptr[i], k1 = ptr[i + 1];
     const double* q = y + 3 * (size_t)k0 + c;
@@ -713,7 +715,8 @@ __global__ __launch_bounds__(kBlock) void k_rhs_slots(int nf, const int* __restr
 #pragma unroll 4
     for (int k = k0; k < k1; ++k, q += 3) sum += *q;
 #endif
-    b[o] = Mxbar[o] + pdt2 * sum;
+    b[o] = mx + pdt2 * sum;
+    if (xlast) xlast[o] = xsrc[o];   // last_x = curr_x (Solver.cpp:170); after the sum: its load is not in the chain
 }
 
 // ------------------------------------------------------------------ control (one block)
