@@ -601,6 +601,17 @@ __device__ __forceinline__ double geo_z_one(const GeoGroupDev& g, int e, const d
     constexpr int C = (T == GEO_ANGLE || T == GEO_EDGE) ? K - 1 : K;
     double v[3 * C], uu[3 * C];
     double t[PLAIN ? 3 * C : 1];
+    // the loads that do not depend on the point positions first (u, the parameters, the warm
+    // triangle): issued after the transform's gathers, each one had added a round trip
+    if (g.hard) {
+#pragma unroll
+        for (int i = 0; i < 3 * C; ++i) uu[i] = u[g.uoff + (size_t)i * g.count + e];
+    }
+    double pr0 = 0.0, pr1 = 0.0;
+    if constexpr (T == GEO_ANGLE) { pr0 = g.prm[e]; pr1 = g.prm[(size_t)g.count + e]; }
+    else if constexpr (T == GEO_EDGE) pr0 = g.prm[e];
+    [[maybe_unused]] int w0 = -1;
+    if constexpr (T == GEO_POINT_TO_REF || T == GEO_REF_SURFACE) w0 = g.warm ? g.warm[e] : -1;
     transform<T, K>(g, e, x, v);
     if constexpr (PLAIN) {
 #pragma unroll
@@ -608,14 +619,14 @@ __device__ __forceinline__ double geo_z_one(const GeoGroupDev& g, int e, const d
     }
     if (g.hard) {
 #pragma unroll
-        for (int i = 0; i < 3 * C; ++i) { uu[i] = u[g.uoff + (size_t)i * g.count + e]; v[i] += uu[i]; }
+        for (int i = 0; i < 3 * C; ++i) v[i] += uu[i];
     }
     if constexpr (T == GEO_PLANE) {
         plane_project<K>(v);
     } else if constexpr (T == GEO_ANGLE) {
-        angle_project(v, g.prm[e], g.prm[(size_t)g.count + e]);
+        angle_project(v, pr0, pr1);
     } else if constexpr (T == GEO_EDGE) {
-        const double L = g.prm[e];
+        const double L = pr0;
         const double s2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
         const double r = s2 > 0 ? L / sqrt(s2) : L;
         v[0] *= r; v[1] *= r; v[2] *= r;
@@ -623,7 +634,6 @@ __device__ __forceinline__ double geo_z_one(const GeoGroupDev& g, int e, const d
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             double qx, qy, qz;
-            const int w0 = g.warm ? g.warm[e] : -1;
             int tr;
             if constexpr (G > 1) tr = bvh_closest_grp<G>(g.surf, v[3 * c], v[3 * c + 1], v[3 * c + 2], w0, stk_i, stk_d, qx, qy, qz);
             else tr = bvh_closest(g.surf, v[3 * c], v[3 * c + 1], v[3 * c + 2], w0, qx, qy, qz);
