@@ -94,6 +94,80 @@ def test_gpu_geom_matches_oracle(builder, pkg, ctx, oracle):
     g.close()
 
 
+def _closest_brute(V, F, P, chunk=256):
+    """Exact squared distance from each point of P to the triangle set (V, F): numpy restatement
+    of the point-triangle test (Ericson's regions) over every triangle; test infrastructure."""
+    A, B, C = V[F[:, 0]], V[F[:, 1]], V[F[:, 2]]
+    out = np.empty(len(P))
+    for s in range(0, len(P), chunk):
+        p = P[s:s + chunk, None, :]
+        ab, ac, ap = B - A, C - A, p - A
+        d1, d2 = (ab * ap).sum(-1), (ac * ap).sum(-1)
+        bp = p - B
+        d3, d4 = (ab * bp).sum(-1), (ac * bp).sum(-1)
+        cp = p - C
+        d5, d6 = (ab * cp).sum(-1), (ac * cp).sum(-1)
+        va, vb, vc = d3 * d6 - d5 * d4, d5 * d2 - d1 * d6, d1 * d4 - d3 * d2
+        with np.errstate(divide="ignore", invalid="ignore"):
+            den = 1.0 / (va + vb + vc)
+            q = A + ab * (vb * den)[..., None] + ac * (vc * den)[..., None]
+            v_ab = d1 / (d1 - d3)
+            w_ac = d2 / (d2 - d6)
+            w_bc = (d4 - d3) / ((d4 - d3) + (d5 - d6))
+        regions = [
+            ((d1 <= 0) & (d2 <= 0), A + 0 * p),
+            ((d3 >= 0) & (d4 <= d3), B + 0 * p),
+            ((vc <= 0) & (d1 >= 0) & (d3 <= 0), A + ab * v_ab[..., None]),
+            ((d6 >= 0) & (d5 <= d6), C + 0 * p),
+            ((vb <= 0) & (d2 >= 0) & (d6 <= 0), A + ac * w_ac[..., None]),
+            ((va <= 0) & ((d4 - d3) >= 0) & ((d5 - d6) >= 0), B + (C - B) * w_bc[..., None]),
+        ]
+        done = np.zeros(d1.shape, bool)
+        for m, qq in regions:
+            sel = m & ~done
+            q = np.where(sel[..., None], qq, q)
+            done |= sel
+        out[s:s + chunk] = ((p - q) ** 2).sum(-1).min(1)
+    return out
+
+
+@pytest.mark.parametrize("group", ["0", "4"])
+def test_gpu_closest_points_brute_force(group, pkg, ctx, monkeypatch):
+    """The BVH walk's node bounds (AABB, oriented box in fp32 with slack, fp64 descent) never prune
+    the closest triangle: GPU closest-point distances equal a brute-force minimum over every
+    triangle (1e-10 relative, 1e-13 of the surface's span absolute) on a smooth height field, a
+    sheared one, a random triangle soup (intersecting slivers) and two stacked layers, for points
+    on, near and far from the surface, with one lane and with four lanes per query."""
+    monkeypatch.setenv("AA_CP_GROUP", group)
+    rng = np.random.default_rng(11)
+    surfs = []
+    gs = pkg.geom_scenes
+    surfs.append(gs.field_trimesh(40, 40))
+    surfs.append(gs.field_trimesh(30, 50, shear=1.2))
+    Vs = rng.uniform(-1, 1, (900, 3))
+    surfs.append((Vs, rng.integers(0, 900, (1500, 3)).astype(np.int32)))
+    V2, F2 = gs.field_trimesh(25, 25)
+    V3 = np.concatenate([V2, V2 + [0.0, 0.0, 0.02]])
+    surfs.append((V3, np.concatenate([F2, F2 + len(V2)]).astype(np.int32)))
+    for V, F in surfs:
+        V = np.asarray(V, np.float64); F = np.asarray(F, np.int32)
+        F = F[(F[:, 0] != F[:, 1]) & (F[:, 1] != F[:, 2]) & (F[:, 0] != F[:, 2])]
+        lo, hi = V.min(0), V.max(0)
+        span = (hi - lo).max()
+        P = np.concatenate([rng.uniform(lo - 0.3 * span, hi + 0.3 * span, (600, 3)),
+                            V[rng.integers(0, len(V), 600)] + rng.normal(0, 0.01 * span, (600, 3)),
+                            V[rng.integers(0, len(V), 200)]])
+        g = pkg.capi.GeomSolver(ctx)
+        sid = g.add_ref_surface(V, F)
+        q = g.closest_points(sid, P)
+        g.close()
+        d_gpu = ((P - q) ** 2).sum(1)
+        d_ref = _closest_brute(V, F, P)
+        # distances, not their squares: a point on the surface has |p - q| ~ 1e-4 and its square
+        # carries the rounding of p - q (~1e-16 |p|) relative to a tiny value
+        np.testing.assert_allclose(np.sqrt(d_gpu), np.sqrt(d_ref), rtol=1e-10, atol=1e-13 * span)
+
+
 @pytest.mark.parametrize("group", ["4", "8"])
 def test_gpu_closest_point_group_traversal_bit_identical(group, pkg, ctx, monkeypatch):
     """The group traversal (AA_CP_GROUP lanes per query over the collapsed tree, read when a
