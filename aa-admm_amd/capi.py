@@ -416,7 +416,9 @@ def run_scene(ctx: Context, scene, n_steps=None, comm=None):
         s.step()
         h = s.history()
         h["x"], h["v"] = s.x, s.v
-        h["step_ms"] = s.runtime().step_ms
+        rt = s.runtime()
+        h["step_ms"] = rt.step_ms
+        h["iterations"], h["rejects"] = rt.iterations, rt.rejects
         out.append(h)
     return out, s
 

@@ -49,6 +49,14 @@ const Rccl& rccl() {
     return r;
 }
 
+// Whether a partitioned step records its device all-reduces into the step's hipGraph (see
+// RcclComm::capturable). The rehearsal transport follows the same rule, so bench.py --rehearse
+// times the launch mode a real P-GPU run uses.
+bool rccl_graph() {
+    const char* e = std::getenv("AA_RCCL_GRAPH");
+    return e && e[0] == '1';
+}
+
 void nccl_check(ncclResult_t rc, const char* what) {
     if (rc != ncclSuccess) throw Error(ERR_DEVICE, std::string(what) + ": " + rccl().error_string(rc));
 }
@@ -87,10 +95,7 @@ public:
     // kernels are long enough for the host to stay ahead). AA_RCCL_GRAPH=1 records
     // ncclAllReduce into the step's graph instead (a failed capture on any rank drops every
     // rank back to eager launches) -- opt-in until a multi-rank RCCL capture has been verified.
-    bool capturable() const override {
-        const char* e = std::getenv("AA_RCCL_GRAPH");
-        return e && e[0] == '1';
-    }
+    bool capturable() const override { return rccl_graph(); }
 
 private:
     ncclComm_t comm_ = nullptr;
@@ -124,7 +129,8 @@ private:
 // A device all-reduce leaves the local values (dst = src), a host all-reduce multiplies by P
 // (as if every rank held the same values: the setup's scene-identity checks pass, agreement
 // flags stay set). The numbers it produces are not a solution -- it exists to time one rank's
-// kernels of a P-GPU run (bench.py --rehearse P) with the step graph captured as in production.
+// kernels of a P-GPU run (bench.py --rehearse P), launched the way production launches them
+// (eager unless AA_RCCL_GRAPH=1, as the RCCL transport).
 class SoloComm final : public Comm {
 public:
     SoloComm(int rank, int size) { rank_ = rank; size_ = size; }
@@ -134,7 +140,7 @@ public:
     void allreduce_sum_host(double* buf, size_t n) override {
         for (size_t i = 0; i < n; ++i) buf[i] *= size_;
     }
-    bool capturable() const override { return true; }
+    bool capturable() const override { return rccl_graph(); }
     bool rehearsal() const override { return true; }
 };
 

@@ -1,5 +1,6 @@
 // GPU supernodal triangular solves (see direct_solve.hpp).
 #include "direct_solve.hpp"
+#include "solve_plan.hpp"
 
 #include <omp.h>
 
@@ -1221,8 +1222,6 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     // share of the tree is P times smaller, and its fused subtrees cost a latency chain per level
     // whatever their count, so it takes fewer, taller ones (measured)
     const int min_sub = ms ? std::atoi(ms) : (comm_ ? std::max(32, 256 / comm_->size()) : 256);
-    constexpr int kSubLds = 64 * 1024, kSubLdsB = 144 * 1024, kMaxItemRow = 0xffff;
-    constexpr long long kLdsMax = 160 * 1024;   // the fused kernels' LDS attribute (build, below)
     auto roots_at = [&](int H) {
         std::vector<int> r;
         for (int sn = 0; sn < nn_; ++sn)
@@ -1234,33 +1233,13 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         while (!st.empty()) { int v = st.back(); st.pop_back(); out.push_back(v); for (int c : kids[v]) st.push_back(c); }
         return out;
     };
-    cut_height_ = -1;
-    for (int H = F.max_height - 1; H >= 1; --H) {
-        std::vector<int> r = roots_at(H);
-        if ((int)r.size() < min_sub) continue;
-        bool ok = true;
-        for (int rt : r) {
-            std::vector<long long> lf(H + 1, 0), lb(H + 1, 0), nodes_at(H + 1, 0);
-            const std::vector<int> all = collect(rt);
-            // the subtree's node records staged in LDS beside a level's vectors (two copies of
-            // each supernode: forward and backward offsets), 16-B aligned after the vectors
-            const long long rec = 16 + 2LL * (long long)all.size() * (long long)sizeof(SubNode);
-            for (int v : all) {
-                lf[F.height[v]] += 24LL * KS * p[v];
-                long long slots = 0;
-                for (int sg = 0; sg < (p[v] + nb[v] + kSubSegRows - 1) / kSubSegRows; ++sg)
-                    slots += std::min(p[v], (sg + 1) * kSubSegRows);
-                lb[F.height[v]] += 24LL * KS * (p[v] + nb[v] + slots);
-                nodes_at[F.height[v]] += 1;
-                if (p[v] + nb[v] > kMaxItemRow) ok = false;
-            }
-            for (int h = 0; h <= H; ++h)
-                if (lf[h] > kSubLds || lb[h] > kSubLdsB || nodes_at[h] > kMaxItemRow || lf[h] + rec > kLdsMax ||
-                    lb[h] + rec > kLdsMax)
-                    ok = false;
-            if (!ok) break;
-        }
-        if (ok) { cut_height_ = H; break; }
+    {   // the cut height against the launch's aggregate LDS (solve_plan.hpp; the fused kernels'
+        // LDS attribute is 160 KiB, set below)
+        CutPlanIn pl;
+        pl.parent = &F.parent; pl.height = &F.height; pl.inc = &inc; pl.p = &p; pl.nb = &nb;
+        pl.max_height = F.max_height; pl.ks = KS; pl.min_sub = min_sub; pl.seg_rows = kSubSegRows;
+        pl.node_bytes = (long long)sizeof(SubNode);
+        cut_height_ = choose_cut_height(pl);
     }
     std::vector<char> fused(nn_, 0);
     {
@@ -1807,8 +1786,9 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     Y_.alloc(3 * KS * (size_t)n_);
     U_.alloc(std::max<long long>(KS * uo, 3));
     // (LDS figures above are per 3 columns; a 6-column solve needs twice as much; + the staged nodes)
+    // internal assert: choose_cut_height budgets exactly this aggregate
     if (std::max(sub_lds_bytes(KS, true), sub_lds_bytes(KS, false)) > 160 * 1024)
-        throw Error(ERR_STATE, "DirectSolver: fused subtree exceeds 160 KiB of LDS (cut-height budget)");
+        throw Error(ERR_STATE, "DirectSolver: internal error: fused subtrees exceed 160 KiB of LDS");
     if (std::max(sub_lds_bytes(KS, true), sub_lds_bytes(KS, false)) > 64 * 1024)
         for (const void* k : {(const void*)k_fwd_sub<256, 3, false>, (const void*)k_fwd_sub<512, 3, false>, (const void*)k_fwd_sub<1024, 3, false>,
                               (const void*)k_bwd_sub<256, 3, false>, (const void*)k_bwd_sub<512, 3, false>, (const void*)k_bwd_sub<1024, 3, false>,

@@ -25,6 +25,9 @@ namespace aa {
 
 ElasticSolver::~ElasticSolver() {
     drop_graph();
+    if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_join_) (void)hipEventDestroy(ev_join_);
+    if (side_) (void)hipStreamDestroy(side_);
     for (auto& kv : kstats_)
         for (auto e : kv.second.ev) (void)hipEventDestroy(e);
 }
@@ -437,6 +440,10 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     // solve (enqueue_iteration_z); AA_Z_PIPELINE=0 restores the sequential order
     pipe_z_ = st_.variant == AA_VARIANT_Z && st_.acceleration_type == 1;
     if (const char* e = std::getenv("AA_Z_PIPELINE")) pipe_z_ = pipe_z_ && e[0] != '0';
+    // the pipelined pass on a second stream (one GPU: a partitioned pass would put collectives
+    // on two streams); AA_CONCURRENT=0 keeps it in line
+    conc_ = pipe_z_ && !comm_;
+    if (const char* e = std::getenv("AA_CONCURRENT")) conc_ = conc_ && e[0] != '0';
     // Z variant + Anderson: the two-set layout whether pipelined or not (same sums, same bits)
     stamp("factor");
     solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_, pipe_z_ ? 2 : 1,
@@ -568,10 +575,19 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     if (pipe_z_) b2_.alloc(3 * (size_t)nf_); dx_.alloc(3 * (size_t)nf_);
     z_.alloc(Z_); u_.alloc(Z_); y_.alloc(3 * std::max<long long>(1, Yslots_)); du_.alloc(Z_);
     if (st_.variant == AA_VARIANT_Z) { dz_.alloc(Z_); lastz_.alloc(Z_); cz_.alloc(Z_); }
+    if (conc_) {
+        du2_.alloc(Z_); dz2_.alloc(Z_); dx2_.alloc(3 * (size_t)nf_);
+        ctrl_c_.alloc(1);
+        lzq2_.alloc(1);
+        if (!side_) AA_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+        if (!ev_fork_) AA_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+        if (!ev_join_) AA_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    }
     // residual block partials [a | b], padded to the largest rank's block count (zeros beyond
     // this rank's blocks), and their all-rank sums (the same buffer on one GPU)
     nbg_ = std::max(1, nbg_);
     red_ab_.alloc(2 * (size_t)nbg_); red_ab_.zero(s());
+    if (conc_) { red_c_.alloc(2 * (size_t)nbg_); red_c_.zero(s()); }
     pa_ = red_ab_.p; pb_ = red_ab_.p + nbg_;
     if (comm_) { red_gab_.alloc(2 * (size_t)nbg_); red_gab_.zero(s()); ga_ = red_gab_.p; gb_ = red_gab_.p + nbg_; }
     else { ga_ = pa_; gb_ = pb_; }
@@ -579,11 +595,13 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     lzq_.alloc(1);
     if (const char* q = std::getenv("AA_LOCAL_QUEUE")) use_queue_ = q[0] != '0';
     lq_ = make_local_queue(ctx_->device, lzq_.p);
+    if (conc_) lq2_ = make_local_queue(ctx_->device, lzq2_.p);
     if (const char* q = std::getenv("AA_LQ_STATS"); q && q[0] == '1') {
         lq_stats_.alloc(kLqStats);
         lq_stats_.zero(s());
         lq_.stats = lq_stats_.p;
     }
+    if (conc_) lq2_.stats = lq_.stats;
     hist_cap_ = std::max(1, st_.admm_iters);
     hist_prim_.alloc(hist_cap_); hist_comb_.alloc(hist_cap_); hist_rej_.alloc(hist_cap_);
     hist_clock_.alloc(hist_cap_ + 1);
@@ -723,6 +741,13 @@ void ElasticSolver::local_z_all(const double* xfull, const double* u, double* z,
     if (timed) ev_end("local_z");
 }
 
+// the element prox of every group on stream st with control block c (no partials, no slots)
+void ElasticSolver::local_z_on(const double* xfull, const double* u, double* z, int mode, hipStream_t st, Ctrl* c,
+                               const LocalQueue* q) {
+    for (auto& g : groups_)
+        launch_local_z(g.d, xfull, u, z, nullptr, nf_, st_.variant, mode, c, nullptr, 0, st, use_queue_ ? q : nullptr);
+}
+
 void ElasticSolver::prologue() {
     upload_pins();
     const bool accel = st_.acceleration_type == 1;
@@ -769,9 +794,10 @@ void ElasticSolver::prologue() {
         launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, nullptr, 0, s());
         solver_.solve(b_.p, xfull_.p, nullptr, 0, s());
         local_z_all(xfull_.p, u_.p, z_.p, nullptr, LZ_INIT, false);
-        launch_copy(dz_.p, z_.p, Z_, nullptr, 0, s());
-        launch_copy(dx_.p, xfull_.p, nx, nullptr, 0, s());
-        launch_copy(du_.p, u_.p, Z_, nullptr, 0, s());
+        // default_{z,x,u} of "iteration -1" (the parity buffers of the concurrent pass)
+        launch_copy(dz_at(-1), z_.p, Z_, nullptr, 0, s());
+        launch_copy(dx_at(-1), xfull_.p, nx, nullptr, 0, s());
+        launch_copy(du_at(-1), u_.p, Z_, nullptr, 0, s());
         // (Z variant: the accelerator's current iterate is z_ itself)
     }
 }
@@ -839,6 +865,13 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
     const long long nx = 3LL * nf_;
     Ctrl* c = ctrl_.p;
     const bool pipe = accel && pipe_z_;
+    // default_{u,z,x}: this iteration's (written below) and the previous one's (read by the
+    // reject restore, the previous iteration's combined-residual pass and its rollback)
+    double *duc = du_at(it), *dzc = dz_at(it), *dxc = dx_at(it);
+    double *dup = du_at(it - 1), *dzp = dz_at(it - 1), *dxp = dx_at(it - 1);
+    // concurrent pass (conc_): iteration k-1's combined residual on side_, joined at the end of
+    // this iteration; not in the instrumented (per-kernel-class timing) pass
+    const bool side = pipe && it > 0 && conc_ && !instrument_;
     ev_begin("grad");
     for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, accel ? 1 : 0, 0, c, s());
     ev_end("grad");
@@ -849,10 +882,18 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         ev_begin("solve");
         solver_.solve2(b_.p, xfull_.p, b2_.p, cxfull_.p, c, 0, s());
         ev_end("solve");
-        ev_begin("comb");
-        comb_finish_z(CTL_COMB_ZP);
-        launch_copy(xfull_.p, dx_.p, nx, c, 2, s());   // break at comb_{k-1}: x back to curr_x_{k-1}
-        ev_end("comb");
+        if (side) {
+            launch_ctrl_fork(c, ctrl_c_.p, s());
+            AA_HIP(hipEventRecord(ev_fork_, s()));
+            AA_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
+            comb_finish_z(CTL_COMB_ZP, side_, ctrl_c_.p, red_c_.p, red_c_.p + nbg_, &lq2_, dup, dzp);
+            AA_HIP(hipEventRecord(ev_join_, side_));
+        } else {
+            ev_begin("comb");
+            comb_finish_z(CTL_COMB_ZP, s(), c, pa_, pb_, &lq_, dup, dzp);
+            launch_copy(xfull_.p, dxp, nx, c, 2, s());   // break at comb_{k-1}: x back to curr_x_{k-1}
+            ev_end("comb");
+        }
     } else {
         ev_begin(pipe ? "solve1" : "solve");
         solver_.solve(b_.p, xfull_.p, c, 0, s());
@@ -872,9 +913,9 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
     launch_control(CTL_PRIM_CHECK_Z, c, ga_, nullptr, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
     if (accel) {   // reject branch (gated on the device; a no-op unless prim increased)
         ev_begin("reject");
-        launch_copy(u_.p, du_.p, Z_, c, 1, s());
-        launch_copy(xfull_.p, dx_.p, nx, c, 1, s());
-        launch_copy(z_.p, dz_.p, Z_, c, 1, s());
+        launch_copy(u_.p, dup, Z_, c, 1, s());
+        launch_copy(xfull_.p, dxp, nx, c, 1, s());
+        launch_copy(z_.p, dzp, Z_, c, 1, s());
         // accelerator.replace(curr_z): the accelerator's iterate is z_ (restored above)
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 0, 1, c, s());
         launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());
@@ -887,16 +928,16 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
     if (accel) {
         const int m = st_.anderson_m;
         ev_begin("copy");
-        launch_copy(dx_.p, xfull_.p, nx, c, 0, s());
-        launch_copy(du_.p, u_.p, Z_, c, 0, s());
+        launch_copy(dxc, xfull_.p, nx, c, 0, s());
+        launch_copy(duc, u_.p, Z_, c, 0, s());
         ev_end("copy");
         // default_z = update_z(curr_x, curr_u) (Solver.cpp:196-199); the same pass writes the
         // rhs slots of the combined-residual solve, w (w default_z + C - curr_u)
         // (Solver.cpp:220): curr_u is final for this iteration and the AA step does not touch it
         ev_begin("local_z");
-        local_z_all(xfull_.p, u_.p, dz_.p, y_.p, LZ_NORMAL, false);
+        local_z_all(xfull_.p, u_.p, dzc, y_.p, LZ_NORMAL, false);
         ev_end("local_z");
-        Seg2 G{dz_.p, Z_, nullptr, 0};
+        Seg2 G{dzc, Z_, nullptr, 0};
         Seg2 out{z_.p, Z_, nullptr, 0};
         Seg2 none{nullptr, 0, nullptr, 0};
         ev_begin("aa");
@@ -910,12 +951,17 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
             ev_begin("rhs");
             launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b2_.p, c, 0, s());
             ev_end("rhs");
+            if (side) {   // join: the pass's records, and a break at comb_{k-1} undoes this iteration
+                AA_HIP(hipStreamWaitEvent(s(), ev_join_, 0));
+                launch_ctrl_join(c, ctrl_c_.p, s());
+                launch_copy(xfull_.p, dxp, nx, c, 2, s());   // x back to curr_x_{k-1}
+            }
             return;
         }
         ev_begin("comb");
         launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 0, s());
         solver_.solve(b_.p, cxfull_.p, c, 0, s());
-        comb_finish_z(CTL_COMB_Z);
+        comb_finish_z(CTL_COMB_Z, s(), c, pa_, pb_, &lq_, duc, dzc);
         ev_end("comb");
         return;
     }
@@ -930,25 +976,30 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
 
 // comb pass after its solve: z_c = update_z(x_c, curr_u) into cz_, dual = W (z_c - default_z),
 // prim = D x_c - W z_c - C, comb = |prim|^2 + |dual|^2 and the break test (Solver.cpp:224-246).
-// Reads du_ (= curr_u of the iteration the pass belongs to) -- also when pipelined, where u_
-// already holds the next iteration's u.
-void ElasticSolver::comb_finish_z(int op) {
-    Ctrl* c = ctrl_.p;
-    local_z_all(cxfull_.p, du_.p, cz_.p, nullptr, LZ_NORMAL, false);
+// du / dz: curr_u and default_z of the iteration the pass belongs to (when pipelined, u_ already
+// holds the next iteration's u). On stream st with control block c and partials pa / pb: the
+// solver's own, or (concurrent pass) the side stream's copies, summed only there -- one GPU.
+void ElasticSolver::comb_finish_z(int op, hipStream_t st, Ctrl* c, double* pa, double* pb, const LocalQueue* q,
+                                  const double* du, const double* dz) {
+    local_z_on(cxfull_.p, du, cz_.p, LZ_NORMAL, st, c, q);
     int off = 0;
     for (auto& g : groups_) {
-        launch_prim_z(g.d, cxfull_.p, cz_.p, dz_.p, nf_, 0, c, pa_, pb_, off, s());
+        launch_prim_z(g.d, cxfull_.p, cz_.p, dz, nf_, 0, c, pa, pb, off, st);
         off += blocks_for(g.d.count);
     }
-    reduce_partials();
-    launch_control(op, c, ga_, gb_, nbg_, 1, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    if (st == s()) {
+        reduce_partials();
+        launch_control(op, c, ga_, gb_, nbg_, 1, hist_prim_.p, hist_comb_.p, hist_rej_.p, st);
+    } else {
+        launch_control(op, c, pa, pb, nbg_, 1, hist_prim_.p, hist_comb_.p, hist_rej_.p, st);
+    }
 }
 
 // the last iteration's combined-residual pass (pipelined Z variant)
-void ElasticSolver::enqueue_comb_tail_z() {
+void ElasticSolver::enqueue_comb_tail_z(int iters) {
     ev_begin("comb");
     solver_.solve(b2_.p, cxfull_.p, ctrl_.p, 0, s());
-    comb_finish_z(CTL_COMB_Z);
+    comb_finish_z(CTL_COMB_Z, s(), ctrl_.p, pa_, pb_, &lq_, du_at(iters - 1), dz_at(iters - 1));
     ev_end("comb");
 }
 
@@ -964,7 +1015,7 @@ void ElasticSolver::enqueue_iterations(int iters, bool accel) {
         if (eager_sync > 0 && cst == hipStreamCaptureStatusNone && (it + 1) % eager_sync == 0)
             AA_HIP(hipStreamSynchronize(s()));
     }
-    if (st_.variant != AA_VARIANT_UX && accel && pipe_z_ && iters > 0) enqueue_comb_tail_z();
+    if (st_.variant != AA_VARIANT_UX && accel && pipe_z_ && iters > 0) enqueue_comb_tail_z(iters);
 }
 
 void ElasticSolver::epilogue_enqueue(bool accel) {
@@ -1014,7 +1065,10 @@ void ElasticSolver::step() {
             comm_->allreduce_sum_host(&f, 1);
             if (f > 0 && ok) { drop_graph(); ok = false; }
         }
-        if (!ok) use_graph_ = graph = false;
+        if (!ok) {
+            use_graph_ = graph = false;
+            std::fprintf(stderr, "[aa_admm] step graph capture failed: launching eagerly\n");
+        }
     }
     prologue();
     if (graph) {

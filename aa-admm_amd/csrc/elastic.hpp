@@ -143,6 +143,20 @@ private:
     bool use_graph_ = true;
     bool pipe_z_ = false;   // Z variant + Anderson: comb solve batched with the next solve
     void drop_graph();
+    // Concurrent combined-residual pass (pipelined Z variant, one GPU; AA_CONCURRENT=0 turns it
+    // off): iteration k-1's pass runs on side_ beside iteration k, with its own control block,
+    // partials and work-queue counter; default_{u,z,x} alternate between two buffers by
+    // iteration parity so the pass reads k-1's while iteration k writes its own.
+    bool conc_ = false;
+    hipStream_t side_ = nullptr;
+    hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+    DevBuf<Ctrl> ctrl_c_;
+    DevBuf<int> lzq2_;
+    LocalQueue lq2_;
+    DevBuf<double> red_c_, du2_, dz2_, dx2_;
+    double* du_at(int it) { return conc_ && (it & 1) ? du2_.p : du_.p; }
+    double* dz_at(int it) { return conc_ && (it & 1) ? dz2_.p : dz_.p; }
+    double* dx_at(int it) { return conc_ && (it & 1) ? dx2_.p : dx_.p; }
 
     // kernel-class event timing (bench only)
     bool instrument_ = false;
@@ -155,13 +169,16 @@ private:
     void prologue();
     void enqueue_iteration_ux(bool accel);
     void enqueue_iteration_z(bool accel, int it);
-    void comb_finish_z(int op);
-    void enqueue_comb_tail_z();
+    void comb_finish_z(int op, hipStream_t st, Ctrl* c, double* pa, double* pb, const LocalQueue* q,
+                       const double* du, const double* dz);
+    void enqueue_comb_tail_z(int iters);
     void enqueue_iterations(int iters, bool accel);
     void epilogue_enqueue(bool accel);
     void fetch_results();
     int nb_elems() const { return red_blocks_; }
     void local_z_all(const double* xfull, const double* u, double* z, double* y, int mode, bool red);
+    void local_z_on(const double* xfull, const double* u, double* z, int mode, hipStream_t st, Ctrl* c,
+                    const LocalQueue* q);
 };
 
 }  // namespace aa

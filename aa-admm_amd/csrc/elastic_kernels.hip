@@ -1557,6 +1557,35 @@ void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b
 
 __global__ void k_stamp(Ctrl* ctrl) { ctrl->clock0 = (long long)wall_clock64(); }
 
+// Concurrent combined-residual pass (ElasticSolver::enqueue_iteration_z): the
+// pass of iteration k-1 runs on a second stream beside iteration k, on its own copy of the
+// control block. Fork: the copy is taken once everything before it on the main stream is done
+// (the prim / reject of k-1 it records, done, fail, the record counters).
+__global__ __launch_bounds__(256) void k_ctrl_fork(const Ctrl* __restrict__ ctrl, Ctrl* __restrict__ side) {
+    const int* a = reinterpret_cast<const int*>(ctrl);
+    int* b = reinterpret_cast<int*>(side);
+    for (int i = threadIdx.x; i < (int)(sizeof(Ctrl) / sizeof(int)); i += blockDim.x) b[i] = a[i];
+}
+
+// Join: the pass's records become the solver's; a break (comb < 1e-20 or the eps stop, the
+// side's done) ends the step as the sequential order would have -- before iteration k: done = 2
+// (the gated copy that follows restores x = curr_x of k-1), and what iteration k changed that
+// outlives the step is taken back (its reject count, a prox failure of its local steps).
+__global__ void k_ctrl_join(Ctrl* __restrict__ ctrl, const Ctrl* __restrict__ side) {
+    if (ctrl->done) return;   // the side pass was gated off as well
+    ctrl->nrec = side->nrec;
+    ctrl->iters_run = side->iters_run;
+    ctrl->comb = side->comb;
+    ctrl->eps_abs = side->eps_abs;
+    if (side->done) {
+        ctrl->done = 2;
+        ctrl->nrej = side->nrej;
+        ctrl->fail = side->fail;
+    } else {
+        ctrl->fail = ctrl->fail ? ctrl->fail : side->fail;
+    }
+}
+
 // WindForce::project (ExplicitForce.cpp:47-104; helper::triangle_norm :28-39), Wejchert-Haumann
 // normal force, one workgroup sweeping the triangle levels (see launch_wind); Eigen's operation
 // order (squaredNorm (a + b) + c, normalized = n / sqrt(squaredNorm), dot (a + b) + c), no FMA.
@@ -1596,6 +1625,16 @@ __global__ __launch_bounds__(1024) void k_wind(const int* __restrict__ tris3, co
 
 void launch_stamp(Ctrl* ctrl, hipStream_t s) {
     hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, s, ctrl);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_ctrl_fork(const Ctrl* ctrl, Ctrl* side, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctrl_fork, dim3(1), dim3(256), 0, s, ctrl, side);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_ctrl_join(Ctrl* ctrl, const Ctrl* side, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctrl_join, dim3(1), dim3(1), 0, s, ctrl, side);
     AA_CHECK_LAUNCH();
 }
 

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <exception>
 #include <functional>
 #include <omp.h>
 #include <numeric>
@@ -430,24 +431,26 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
     // partitioned: a rank whose own part fails (not positive definite) must not leave the others
     // waiting in the first top front's sum -- every rank reports its own-part outcome first and
     // all of them throw together (the top fronts are summed, so they fail or pass on all ranks)
-    auto agree = [&](const std::string& err) {
+    // the failure keeps its own type (aa::Error codes, std::bad_alloc) on the rank it happened on;
+    // only the other ranks throw the synthesized "another rank's part" error
+    auto agree = [&](const std::exception_ptr& err) {
         if (!part) {
-            if (!err.empty()) throw std::runtime_error(err);
+            if (err) std::rethrow_exception(err);
             return;
         }
-        double bad = err.empty() ? 0.0 : 1.0;
+        double bad = err ? 1.0 : 0.0;
         part->reduce_host(&bad, 1);
-        if (!err.empty()) throw std::runtime_error(err);
+        if (err) std::rethrow_exception(err);
         if (bad > 0) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite (on another rank's part)");
     };
     if (!dense) {   // host only: postorder, parallel inside the large fronts
         std::vector<int> pos(n, -1);
-        std::string err;
+        std::exception_ptr err;
         try {
             for (int s = 0; s < nn; ++s)
                 if (part ? mine(s) : true) factor_front(C, s, pos, true);
-        } catch (const std::exception& e) {
-            err = e.what();
+        } catch (...) {
+            err = std::current_exception();
         }
         agree(err);
         if (part)
@@ -463,7 +466,7 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
             if (tree.parent[s] >= 0) sub[tree.parent[s]] += sub[s];
         }
         const long long grain = std::max<long long>(256, n / 1024);
-        std::string err;
+        std::exception_ptr err;
         std::function<void(int)> rec = [&](int s) {
             for (int c : tree.children[s]) {
                 if (sub[c] > grain) {
@@ -478,13 +481,13 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
             if ((int)pos.size() < n) pos.assign(n, -1);
             bool failed;
 #pragma omp critical(aa_factor_err)
-            failed = !err.empty();
+            failed = (bool)err;
             if (failed) return;
             try {
                 factor_front(C, s, pos, false);
-            } catch (const std::exception& e) {
+            } catch (...) {
 #pragma omp critical(aa_factor_err)
-                if (err.empty()) err = e.what();
+                if (!err) err = std::current_exception();
             }
         };
         // partitioned: the own part's subtrees (roots: own supernodes whose parent is not own)

@@ -179,3 +179,37 @@ def compare(ref_steps, got_steps, tol_comb, tol_x, n_check=None):
     if not dx <= tol_x:
         fails.append(f"final x rel err {dx:.3e} (tol {tol_x:g})")
     return fails
+
+
+def check_full_golden(got, ref, reject_slack=0):
+    """A C4-recipe run against a reference fixture of make_golden.py --full / --bunny: per-step
+    residual curves relative to comb_0 (1e-6, L-BFGS prox path; prim 1e-5), reject flags (equal,
+    or at most reject_slack differing per step), positions and velocities on the sampled nodes
+    and their column sums (1e-6 relative). Returns a list of failures."""
+    fails = []
+    o = 0
+    for k, n in enumerate(ref["nrec"]):
+        h = got[k]
+        rc, rp, rr = ref["comb"][o:o + n], ref["prim"][o:o + n], ref["reject"][o:o + n]
+        o += n
+        if len(h["comb"]) != n:
+            fails.append(f"step {k}: {len(h['comb'])} records, want {n}")
+            continue
+        dc = np.abs(h["comb"] - rc).max() / rc[0]
+        if not dc <= 1e-6:
+            fails.append(f"step {k}: comb dev {dc:.3e}")
+        dp = np.abs(h["prim"] - rp).max() / rp[0]
+        if not dp <= 1e-5:
+            fails.append(f"step {k}: prim dev {dp:.3e}")
+        nrej = int((np.asarray(h["reject"]) != rr).sum())
+        if nrej > reject_slack:
+            fails.append(f"step {k}: {nrej} reject flags differ")
+        for key in ("x", "v"):
+            want = ref[key + "_sample"][k]
+            scale = np.abs(want).max()
+            hk = np.asarray(h[key]).reshape(-1, 3)
+            if not np.abs(hk[ref["sample"]] - want).max() <= 1e-6 * scale:
+                fails.append(f"step {k}: {key} samples")
+            if not np.allclose(hk.sum(0), ref[key + "_sum"][k], rtol=1e-6, atol=1e-6 * scale * len(hk)):
+                fails.append(f"step {k}: {key} column sums")
+    return fails

@@ -24,6 +24,12 @@ CASES = {
     # no Anderson, z order, linear tets
     "cant_z_noaa": (lambda: scenes.cantilever(10, 3, 3, scenes.LINEAR, iters=30, n_steps=2,
                                               variant=scenes.VARIANT_X, accel=0), 1e-9),
+    # at scale: the C4 recipe at the reference golden's size (64 000 tets, checked
+    # against tests/golden/full_drop40_z_nh_aa6.npz) and at full size (1 000 000 tets, against
+    # the single-GPU run) -- per-part fused subtrees, split-K tiles inside a part, the dense top
+    # split by rows, GPU-backend top fronts (AA_DENSE_MIN_FRONT default)
+    "drop40_ref": (lambda: scenes.tet_drop(40, 16, 20, iters=10, n_steps=3), 1e-6),
+    "block1m": (lambda: scenes.tet_drop(100, 40, 50, iters=40, n_steps=3), 1e-6),
 }
 
 # Geometry (ALM) cases: the same bars as tests/test_gpu_geom.py (comb relative to comb_0: 1e-8 over

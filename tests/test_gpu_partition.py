@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 from conftest import REPO
-from golden_io import compare, compare_geom
+from golden_io import GOLDEN, check_full_golden, compare, compare_geom
 from part_cases import CASES, GEOM_CASES
 
 pytestmark = pytest.mark.gpu
@@ -31,13 +31,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(case, nranks, out, transport="host", extra_env=None):
+def run_ranks(case, nranks, out, transport="host", extra_env=None, timeout=240):
     env = dict(os.environ, AA_CASE=case, AA_OUT=str(out), AA_TRANSPORT=transport, AA_DEVICE="0",
                OMP_NUM_THREADS="4", **(extra_env or {}))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
                         "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
                         os.path.join(REPO, "tests", "part_worker.py")],
-                       capture_output=True, text=True, timeout=240, env=env)
+                       capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     return [dict(np.load(out / f"rank{k}.npz")) for k in range(nranks)]
 
@@ -79,15 +79,75 @@ def test_partitioned_matches_single_gpu(case, nranks, top, minfront, tmp_path, p
     assert not fails, fails
 
 
-def test_rccl_transport_one_rank_is_identity(pkg, ctx):
+def _same_bits(ranks):
+    for r in ranks[1:]:
+        for k in ranks[0]:
+            if k not in ("n_elements",):
+                assert np.array_equal(r[k], ranks[0][k]), k
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_partitioned_drop40_matches_reference(nranks, tmp_path, pkg):
+    """The partitioned solver at a size where its design matters: the C4 recipe at
+    64 000 NeoHookean tets (make_tet_blocks(40,16,20), 3 steps x 10 iterations) on 2 and 4 ranks
+    against the REFERENCE's own run (tests/golden/full_drop40_z_nh_aa6.npz) at the single-GPU
+    test's bars (test_gpu_full_drop40_matches_reference): each part has its own fused subtrees and
+    split-K tile levels, the shared separators are one dense top split over the ranks by rows."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    from make_golden import scene_digest
+    from part_cases import CASES as C
+    ref = np.load(os.path.join(GOLDEN, "full_drop40_z_nh_aa6.npz"))
+    sc = C["drop40_ref"][0]()
+    assert np.array_equal(scene_digest(sc), ref["digest"]), "regenerated scene differs from the fixture's"
+    ranks = run_ranks("drop40_ref", nranks, tmp_path)
+    assert sum(int(r["n_elements"][0]) for r in ranks) == sc.n_elements()
+    _same_bits(ranks)
+    fails = check_full_golden(as_steps(ranks[0], len(ref["nrec"])), ref)
+    assert not fails, fails
+
+
+def test_partitioned_block1m_matches_single_gpu(tmp_path, pkg, ctx):
+    """BASELINE configs[3] at full size (1 000 000 NeoHookean tets) on 2 ranks against the
+    single-GPU solver, 3 steps x 40 iterations: residual curves within 1e-6 comb_0, final
+    positions 1e-6 relative, and the momentum invariant of the partitioned result itself (no pins:
+    mass-weighted mean velocity = g dt after the first step, 1e-9). The top fronts of the two-way
+    partition are large enough for the GPU backend (AA_DENSE_MIN_FRONT default), so the device
+    all-reduce of the partial top fronts runs."""
+    sc = CASES["block1m"][0]()
+    want, s = pkg.capi.run_scene(ctx, sc)
+    s.close()
+    ranks = run_ranks("block1m", 2, tmp_path, timeout=420)
+    assert sum(int(r["n_elements"][0]) for r in ranks) == sc.n_elements()
+    _same_bits(ranks)
+    got = as_steps(ranks[0], len(want))
+    assert [len(g["prim"]) for g in got] == [len(w["prim"]) for w in want]
+    for w in want:
+        w["x"] = w["x"].reshape(-1, 3)
+    fails = compare(want, got, 1e-6, 1e-6)
+    assert not fails, fails
+    m = sc.masses
+    v1 = got[0]["v"].reshape(-1, 3)
+    vbar = (m[:, None] * v1).sum(0) / m.sum()
+    g_dt = sc.gravity * sc.dt
+    assert abs(vbar[1] - g_dt) <= 1e-9 * abs(g_dt), vbar
+    assert abs(vbar[0]) <= 1e-9 * abs(g_dt) and abs(vbar[2]) <= 1e-9 * abs(g_dt), vbar
+
+
+@pytest.mark.parametrize("graph", ["0", "1"])
+def test_rccl_transport_one_rank_is_identity(graph, pkg, ctx, monkeypatch, capfd):
     """ncclCommInitRank / ncclAllReduce on the solver's stream with a one-rank communicator:
-    every reduction of the iteration runs through RCCL and the result is bit-identical."""
+    every reduction of the iteration runs through RCCL and the result is bit-identical -- launched
+    eagerly (the default) and with the all-reduces recorded into the step's hipGraph
+    (AA_RCCL_GRAPH=1)."""
+    monkeypatch.setenv("AA_RCCL_GRAPH", graph)
     capi = pkg.capi
     sc = CASES["drop_z"][0]()
     want, _ = capi.run_scene(ctx, sc)
     comm = capi.Comm.rccl(ctx, 0, 1, capi.Comm.unique_id())
     assert comm.info() == (0, 1)
+    capfd.readouterr()
     got, s = capi.run_scene(ctx, sc, comm=comm)
+    assert "capture failed" not in capfd.readouterr().err   # graph = 1: RCCL recorded and replayed
     for a, b in zip(want, got):
         assert np.array_equal(a["comb"], b["comb"]) and np.array_equal(a["x"], b["x"])
     s.close()

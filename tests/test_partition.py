@@ -32,6 +32,19 @@ def test_partitioned_solve_matches_unpartitioned(tmp_path):
         assert r.stdout.count(" OK") == 10 and r.stdout.count("SINGULAR_OK") == 2
 
 
+def test_fused_subtree_cut_checks_aggregate_lds(tmp_path):
+    """The fused-subtree cut height (csrc/solve_plan.hpp) is checked against the launch's own
+    LDS aggregate -- the widest level vector of any subtree plus the records of the largest one --
+    on a tree whose two subtrees each fit alone but not together (tests/cpp/cut_height.cpp)."""
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "cut_height")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "aa-admm_amd", "csrc"),
+                    os.path.join(REPO, "tests", "cpp", "cut_height.cpp"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 WORKER = r"""
 import importlib, os, sys
 import numpy as np

@@ -17,7 +17,7 @@
 #   prof CFG TAG [bench args]      rocprofv3 --kernel-trace --stats of a short eager run
 #   rehearse CFG P RANK [ENV=V,..] [bench args]   bench.py --rehearse P --rehearse-rank RANK
 #   eps TETS STEPS TAG             tools/elastic_eps_curves.py --gpu (per-step curves + npz)
-#   geps CFG N TAG                 tools/geom_eps_curve.py --gpu on a reduced geometry scene
+#   geps CFG N TAG                 tools/ref_geom_curve.py --gpu on a (reduced) geometry scene
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$(pwd); mkdir -p gpurun_out
 fatal() { case $1 in 0) ;; *) echo "fatal rc=$1 in [$2]; stopping"; exit $1;; esac; }

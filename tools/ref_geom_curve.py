@@ -29,6 +29,9 @@ ap.add_argument("--nx", type=int, default=0)
 ap.add_argument("--tag", default="r3_c3_ref_curve")
 ap.add_argument("--gpu", action="store_true", help="the GPU solver's curve of the same scene (libaa_admm.so)")
 ap.add_argument("--out", default=None, help="output path (default profiles/<tag>.json)")
+ap.add_argument("--perturb", type=float, default=0.0,
+                help="relative random perturbation of the start positions (seeded): how sensitive the curve's "
+                     "late tail is to rounding-level differences")
 a = ap.parse_args()
 gs = importlib.import_module("aa-admm_amd.geom_scenes")
 if a.config == "c3":
@@ -37,7 +40,9 @@ if a.config == "c3":
 else:
     n = a.nx or 707
     sc = gs.wire_grid(n, n, iters=a.iters, aa_m=20)
-eps = 2.0 * (1e-8 * sc.avg_edge_length() * sc.hard_cols()) ** 2
+eps = 2.0 * (1e-8 * sc.avg_edge_length() * sc.hard_cols()) ** 2   # before any perturbation
+if a.perturb:
+    sc.x0 = sc.x0 * (1.0 + a.perturb * np.random.default_rng(7).standard_normal(sc.x0.shape))
 if a.gpu:   # same scene, same cap, no early stop (the reference's stop is commented out too)
     pkg = importlib.import_module("aa-admm_amd")
     ctx = pkg.capi.Context(0)
@@ -60,7 +65,8 @@ else:
 comb = np.asarray(res["comb"])
 idx = sorted(set([0, 1, 2, 4, 9, 19, 49, 99, 199, 299, 499, 699, 999, 1499, 1999, len(comb) - 1]) & set(range(len(comb))))
 out = {"config": a.config, "scene": sc.name, "points": sc.n_points, "hard_cols": sc.hard_cols(), "anderson_m": sc.aa_m,
-       "accepted_iters": int(len(comb)), "eps_abs": eps, "comb0": float(comb[0]),
+       "accepted_iters": int(len(comb)), "eps_abs": eps, "perturb": a.perturb,
+       "first_iter_below_eps_abs": (int(np.nonzero(comb < eps)[0][0]) + 1 if (comb < eps).any() else None), "comb0": float(comb[0]),
        "min_comb": float(comb.min()), "min_comb_over_eps": float(comb.min() / eps),
        "reached_eps_abs": bool((comb < eps).any()),
        "first_iter_below": {f"{r:g}": (int(np.nonzero(comb <= r * comb[0])[0][0]) + 1 if (comb <= r * comb[0]).any() else None)
