@@ -882,12 +882,8 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         ev_begin("solve");
         solver_.solve2(b_.p, xfull_.p, b2_.p, cxfull_.p, c, 0, s());
         ev_end("solve");
-        if (side) {
-            launch_ctrl_fork(c, ctrl_c_.p, s());
-            AA_HIP(hipEventRecord(ev_fork_, s()));
-            AA_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
-            comb_finish_z(CTL_COMB_ZP, side_, ctrl_c_.p, red_c_.p, red_c_.p + nbg_, &lq2_, dup, dzp);
-            AA_HIP(hipEventRecord(ev_join_, side_));
+        if (side) {   // the pass's control block: k-1's prim / reject, before this iteration's
+            launch_ctrl_fork(c, ctrl_c_.p, s());   // check; its nrej / fail for a rollback
         } else {
             ev_begin("comb");
             comb_finish_z(CTL_COMB_ZP, s(), c, pa_, pb_, &lq_, dup, dzp);
@@ -937,6 +933,14 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         ev_begin("local_z");
         local_z_all(xfull_.p, u_.p, dzc, y_.p, LZ_NORMAL, false);
         ev_end("local_z");
+        if (side) {   // k-1's pass beside this iteration's Anderson step and comb rhs: its local
+            // step (one wave per SIMD) leaves room for their memory-bound waves (the two local
+            // steps cannot share a SIMD, so the fork comes after this iteration's)
+            AA_HIP(hipEventRecord(ev_fork_, s()));
+            AA_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
+            comb_finish_z(CTL_COMB_ZP, side_, ctrl_c_.p, red_c_.p, red_c_.p + nbg_, &lq2_, dup, dzp);
+            AA_HIP(hipEventRecord(ev_join_, side_));
+        }
         Seg2 G{dzc, Z_, nullptr, 0};
         Seg2 out{z_.p, Z_, nullptr, 0};
         Seg2 none{nullptr, 0, nullptr, 0};

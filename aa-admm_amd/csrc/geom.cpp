@@ -227,6 +227,9 @@ int build_wide(const std::vector<BvhNode>& N, int G, std::vector<BvhNode>& W) {
 
 GeomSolver::~GeomSolver() {
     drop_graph();
+    if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_join_) (void)hipEventDestroy(ev_join_);
+    if (side_) (void)hipStreamDestroy(side_);
     for (auto& kv : kstats_)
         for (auto e : kv.second.ev) (void)hipEventDestroy(e);
 }
@@ -641,6 +644,25 @@ void GeomSolver::factor_and_upload(const double* init_x3) {
     else redg_ = red_.p;
     ctrl_.alloc(1);
     clock0_.alloc(1);
+    // constraint groups on parallel branches (ALM loop only; opt-in, AA_GEOM_CONCURRENT=1): the
+    // closest-point group stays on the main stream (it dominates), the others run beside it.
+    // Measured slower (C5 396 -> 385, C3 1730 -> 1659 it/s): the short groups
+    // take CU slots from the closest-point walk, whose occupancy is what hides its latency.
+    conc_ = false;
+    if (const char* e = std::getenv("AA_GEOM_CONCURRENT")) conc_ = !plain_ && groups_.size() > 1 && e[0] == '1';
+    heavy_ = 0;
+    for (size_t gi = 0; gi < groups_.size(); ++gi) {
+        const GeoGroupDev& d = groups_[gi].d;
+        const bool cp = d.type == GEO_POINT_TO_REF || d.type == GEO_REF_SURFACE;
+        const GeoGroupDev& h = groups_[heavy_].d;
+        const bool hcp = h.type == GEO_POINT_TO_REF || h.type == GEO_REF_SURFACE;
+        if ((cp && !hcp) || (cp == hcp && (long long)d.count * d.K > (long long)h.count * h.K)) heavy_ = (int)gi;
+    }
+    if (conc_) {
+        if (!side_) AA_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+        if (!ev_fork_) AA_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+        if (!ev_join_) AA_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    }
     int khz = 0;
     AA_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx_->device));
     clock_khz_ = khz > 0 ? khz : 100000.0;
@@ -739,14 +761,31 @@ void GeomSolver::prologue(const double* init_x3, int max_iter, int m, int cap, d
     launch_geo_start(ctrl_.p, clock0_.p, s());
 }
 
+void GeomSolver::fork() {
+    AA_HIP(hipEventRecord(ev_fork_, s()));
+    AA_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
+}
+
+void GeomSolver::join() {
+    AA_HIP(hipEventRecord(ev_join_, side_));
+    AA_HIP(hipStreamWaitEvent(s(), ev_join_, 0));
+}
+
 // ADMM_u_update (+ the ALM residual partials): u_new = u + T(x_new) - z on every group with u
+// (each group's partials at its own block offset; with conc_, the groups beside the heaviest
+// on the side stream)
 void GeomSolver::enqueue_u_update(double* red, hipStream_t st) {
+    const bool br = conc_ && st == s() && !instrument_;
+    if (br) fork();
     int off = 0;
-    for (auto& g : groups_) {
+    for (size_t gi = 0; gi < groups_.size(); ++gi) {
+        auto& g = groups_[gi];
         if (!g.d.hard) continue;
-        launch_geo_u(g.d, new_x_.p, cur_x_.p, z_.p, cur_u_.p, new_u_.p, ctrl_.p, red, off, st);
+        launch_geo_u(g.d, new_x_.p, cur_x_.p, z_.p, cur_u_.p, new_u_.p, ctrl_.p, red, off,
+                     br && (int)gi != heavy_ ? side_ : st);
         off += geo_u_blocks(g.d.count);
     }
+    if (br) join();
 }
 
 // one pass of the while-loop body of GeometrySolver::solve_ADMM (Geometry/GeometrySolver.h:180-251)
@@ -820,7 +859,11 @@ void GeomSolver::enqueue_iteration(int m) {
     Ctrl* c = ctrl_.p;
     const long long nx = 3LL * n_;
     ev_mark("z");
-    for (auto& g : groups_) launch_geo_z(g.d, cur_x_.p, cur_u_.p, z_.p, y_.p, c, s());   // ADMM_z_update
+    const bool br = conc_ && !instrument_;
+    if (br) fork();
+    for (size_t gi = 0; gi < groups_.size(); ++gi)                                      // ADMM_z_update
+        launch_geo_z(groups_[gi].d, cur_x_.p, cur_u_.p, z_.p, y_.p, c, br && (int)gi != heavy_ ? side_ : s());
+    if (br) join();
     ev_mark("z");
     ev_mark("rhs");
     launch_geo_rhs(n_, slot_ptr_.p, slot_idx_.p, y_.p, rhs_fixed_.p, b_.p, c, s());     // ADMM_x_update rhs

@@ -148,6 +148,15 @@ private:
     void enqueue_iteration(int m);
     void enqueue_iteration_plain(int m);
     void enqueue_u_update(double* red, hipStream_t st);
+    // Constraint groups on parallel graph branches (AA_CONCURRENT=0 keeps one stream): each
+    // group's z / u kernels write only its own z, u, rhs slots and residual partials, so the
+    // groups other than the heaviest run on side_ beside it (joined before the next consumer)
+    bool conc_ = false;
+    int heavy_ = 0;   // the group kept on the main stream (the closest-point group, else the largest)
+    hipStream_t side_ = nullptr;
+    hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+    void fork();
+    void join();
     void fetch_results();
     double* solution_buf() { return plain_ ? cur_x_.p : new_x_.p; }
 };
