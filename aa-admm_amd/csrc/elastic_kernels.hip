@@ -329,6 +329,158 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     if (fail && ctrl) ctrl->fail = 1;
 }
 
+// k_local_z_hq with each element's L-BFGS split over a lane pair (dev::HyperLbfgs2, AA_LQ_SPLIT=1,
+// opt-in): a wave holds 32 elements, the state fits 256 registers, and a SIMD runs two waves -- the
+// one-wave kernel spends ~27 % of its cycles waiting on the refills' dependent loads with nothing
+// to hide them. Measured on C4 (profiles/r5_c4_local_step_split.json): 1.56x the VALU instructions
+// per element and 196 B of spills at 256 registers, 428 -> 800 us per launch; not the default. The queue hands out elements to pairs; every branch is pair-uniform
+// (both lanes hold the same decisions), so the DPP swaps always see their partner active. At a
+// finalize each lane writes its half of z and the slots of two of the four vertices.
+template <int NV>
+__global__ __launch_bounds__(kBlock, 2) void k_local_z_hq2(GroupDev g, const double* __restrict__ xfull,
+                                                           const double* __restrict__ u, double* __restrict__ z,
+                                                           double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
+                                                           int* __restrict__ queue, int refill,
+                                                           unsigned long long* __restrict__ stats) {
+    static_assert(NV == 4, "the lane-pair local step is for tets");
+    if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
+    constexpr int H = dev::kHalf;
+    unsigned trips = 0, refills = 0;
+    __shared__ unsigned hist[101];
+    if (stats) {
+        for (int i = threadIdx.x; i < 101; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63, h = lane & 1;
+    const unsigned long long evens = 0x5555555555555555ull;
+    dev::HyperLbfgs2 L;
+    double v[H], x[H];
+    double vol = 0;
+    int e = -1, fail = 0;
+    bool active = false, pending = false, exhausted = false;
+    // this lane's components of F = P x and Cp = P_pinned x_pin (the sums of gather_F, a = 0..3)
+    // and of u; component 5h + j (the pad j = 4 on h = 1 reads component 8 and is not used)
+    // one node at a time (not unrolled): the gathers' results would otherwise all be live at
+    // once beside the lanes' L-BFGS state, past the 256 registers of two waves per SIMD
+    auto gather_own = [&](double* Fo, double* Co, double* uo) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            Fo[j] = 0.0;
+            Co[j] = 0.0;
+            uo[j] = u ? u[g.zoff + (size_t)min(5 * h + j, 8) * g.count + e] : 0.0;
+        }
+#pragma unroll 1
+        for (int a = 0; a < NV; ++a) {
+            const int vi = g.idx[(size_t)a * g.count + e];
+            const double* xa = xfull + 3 * (size_t)vi;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int i = min(5 * h + j, 8), c = i / 3, r = i - 3 * c;
+                const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
+                const double xr = xa[r];
+                Fo[j] += gc * xr;
+                if (vi >= nf) Co[j] += gc * xr;
+            }
+        }
+    };
+    auto finalize = [&]() {
+#pragma unroll
+        for (int j = 0; j < H; ++j)
+            if (h == 0 || j < 4) z[g.zoff + (size_t)(5 * h + j) * g.count + e] = x[j];
+        if (y) {   // y_c = w (w z_c - w Cp_c - u_c) per own component, then the two vertices' slots
+            const double w = g.w[e];
+            double yo[H];
+            {
+                double co[H], uo[H];
+#pragma unroll
+                for (int j = 0; j < H; ++j) {
+                    co[j] = 0.0;
+                    uo[j] = u ? u[g.zoff + (size_t)min(5 * h + j, 8) * g.count + e] : 0.0;
+                }
+#pragma unroll 1
+                for (int a = 0; a < NV; ++a) {
+                    const int vi = g.idx[(size_t)a * g.count + e];
+                    if (vi < nf) continue;   // Cp: pinned nodes only
+                    const double* xa = xfull + 3 * (size_t)vi;
+#pragma unroll
+                    for (int j = 0; j < H; ++j) {
+                        const int i = min(5 * h + j, 8), c = i / 3, r = i - 3 * c;
+                        co[j] += g.G[(size_t)(c * NV + a) * g.count + e] * xa[r];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < H; ++j) yo[j] = w * (w * x[j] - w * co[j] - uo[j]);
+            }
+            double yc[9];
+            dev::pair_full(h, yo, yc);
+#pragma unroll 1
+            for (int b = 0; b < 2; ++b) {
+                const int a = 2 * h + b;
+                const int pos = g.spos[(size_t)a * g.count + e];
+                const double g0 = g.G[(size_t)(0 * NV + a) * g.count + e], g1 = g.G[(size_t)(1 * NV + a) * g.count + e],
+                             g2 = g.G[(size_t)(2 * NV + a) * g.count + e];
+                if (pos < 0) continue;   // pinned: no rhs row
+                double* o = y + 3 * (size_t)pos;
+                o[0] = g0 * yc[0] + g1 * yc[3] + g2 * yc[6];
+                o[1] = g0 * yc[1] + g1 * yc[4] + g2 * yc[7];
+                o[2] = g0 * yc[2] + g1 * yc[5] + g2 * yc[8];
+            }
+        }
+    };
+    for (;;) {
+        const bool need = !active && !exhausted;   // the same on both lanes of a pair
+        const unsigned long long mask = __ballot(need) & evens;
+        if (!__any(active || need)) break;
+        ++trips;
+        if (mask && (__popcll(mask) >= refill || !__any(active))) {
+            ++refills;
+            const int leader = __ffsll((long long)mask) - 1;
+            int b = 0;
+            if (lane == leader) b = atomicAdd(queue, __popcll(mask));
+            if (pending) {
+                finalize();
+                pending = false;
+            }
+            b = __shfl(b, leader, 64);
+            if (need) {
+                const int my = b + __popcll(mask & ((1ull << (lane & ~1)) - 1ull));
+                if (my >= g.count) {
+                    exhausted = true;
+                } else {
+                    e = my;
+                    double Fo[H], Co[H], uo[H];
+                    gather_own(Fo, Co, uo);
+                    const double w = g.w[e];
+#pragma unroll
+                    for (int j = 0; j < H; ++j) {
+                        v[j] = (h && j == 4) ? 0.0 : Fo[j] + uo[j] / w;
+                        x[j] = v[j];
+                    }
+                    vol = g.vol[e];
+                    L.begin();   // its start evaluation is this trip's
+                    active = true;
+                }
+            }
+        }
+        if (active && L.trip(h, g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail)) {
+            active = false;
+            pending = true;
+            if (stats && h == 0) atomicAdd(&hist[min(L.k_it, 100)], 1u);
+        }
+    }
+    if (stats) {
+        if (lane == 0) {
+            atomicAdd(stats + 101, (unsigned long long)trips);
+            atomicAdd(stats + 102, (unsigned long long)refills);
+            atomicAdd(stats + 103, 1ull);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 101; i += blockDim.x)
+            if (hist[i]) atomicAdd(stats + i, (unsigned long long)hist[i]);
+    }
+    if (fail && ctrl) ctrl->fail = 1;
+}
+
 // k_local_z_hq with a one-element lookahead per lane (AA_LQ_AHEAD=1; measured 6 % slower than
 // k_local_z_hq on C4). A refill of the plain queue is a chain of three dependent round trips -- the
 // returning queue atomic, the element's node ids, then the node positions -- paid while the wave's
@@ -1449,7 +1601,11 @@ LocalQueue make_local_queue(int device, int* counter) {
     const char* lh = std::getenv("AA_LQ_LDS");
     q.ahead = ah && ah[0] == '1';   // opt-in: measured slower on C4
     q.hist = (lh && lh[0] == '1') ? LQ_HIST_YLDS : LQ_HIST_REGS;   // opt-in: no faster on C4
-    const void* kq = q.ahead ? (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hqa<4, LQ_HIST_YLDS>
+    const char* sp = std::getenv("AA_LQ_SPLIT");
+    q.split = sp ? sp[0] == '1' : false;
+    if (q.split) q.ahead = false, q.hist = LQ_HIST_REGS;
+    const void* kq = q.split ? (const void*)k_local_z_hq2<4>
+                   : q.ahead ? (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hqa<4, LQ_HIST_YLDS>
                                                        : (const void*)k_local_z_hqa<4, LQ_HIST_REGS>)
                              : (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hq<4, LQ_HIST_YLDS>
                                                        : (const void*)k_local_z_hq<4, LQ_HIST_REGS>);
@@ -1459,6 +1615,7 @@ LocalQueue make_local_queue(int device, int* counter) {
     AA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kq, kBlock, lds));
     q.resident = std::max(1, cus * std::max(1, per));
     q.refill = r ? std::atoi(r) : 60;
+    if (q.split) q.refill = std::max(1, (q.refill + 1) / 2);   // in pairs (elements) per wave
     // lookahead stops once fewer elements than this are left (AA_LQ_MARGIN: in resident lanes)
     const char* mg = std::getenv("AA_LQ_MARGIN");
     q.margin = (int)(std::max(0.0, mg ? std::atof(mg) : 1.0) * q.resident * kBlock);
@@ -1474,7 +1631,11 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
         const int resident = std::max(1, queue->resident), refill = queue->refill;
         const dim3 grid(std::min(nb, resident));
         const size_t lds = queue->lds_bytes;
-        if (queue->ahead && queue->hist == LQ_HIST_YLDS)
+        if (queue->split) {   // two lanes per element: half the elements per block
+            const dim3 grid2(std::min(blocks_for(2LL * g.count), resident));
+            hipLaunchKernelGGL((k_local_z_hq2<4>), grid2, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode, ctrl,
+                               queue->counter, refill, queue->stats);
+        } else if (queue->ahead && queue->hist == LQ_HIST_YLDS)
             hipLaunchKernelGGL((k_local_z_hqa<4, LQ_HIST_YLDS>), grid, dim3(kBlock), lds, s, g, xfull, u, z, y, nf, mode,
                                ctrl, queue->counter, refill, queue->margin, queue->stats);
         else if (queue->ahead)

@@ -444,3 +444,20 @@ def test_gpu_c4_eps_regime_matches_reference(pkg, ctx):
         with pytest.raises(pkg.capi.AAError, match="line search"):
             s.step()
     s.close()
+
+
+@pytest.mark.parametrize("which", [n for n in case_names() if ("nh" in n or "stvk" in n or "beams" in n)] +
+                         ["full_drop40"])
+def test_gpu_lane_pair_local_step_matches_reference(which, pkg, ctx, monkeypatch):
+    """The NeoHookean / StVK local step with each element's L-BFGS split over a lane pair
+    (k_local_z_hq2, dev::HyperLbfgs2, AA_LQ_SPLIT=1: opt-in, measured 1.9x slower on C4 --
+    profiles/r5_c4_local_step_split.json) against the same reference fixtures and bars as the
+    one-lane kernel: the 9-term sums become two partial sums added, so results move by rounding
+    only. (Not run on the 64k-tet run-to-epsilon fixture: the reference's step-9 abort there is a
+    rounding accident of one element's line search, which the one-lane kernel reproduces and the
+    re-associated sums do not.)"""
+    monkeypatch.setenv("AA_LQ_SPLIT", "1")
+    if which == "full_drop40":
+        test_gpu_full_drop40_matches_reference(pkg, ctx)
+    else:
+        test_gpu_matches_reference_golden(which, pkg, ctx)
