@@ -442,6 +442,12 @@ def geom_run_to_eps(g, sc, eps, args):
            "median_ms": all_steps_median([r["eps_abs"]["ms"] if r["eps_abs"] else None for r in runs]),
            "median_ms_reached_only": round(statistics.median(hit_ms), 3) if hit_ms else None,
            "clock": "device wall_clock64 from the loop start (elapsed_time_)", "per_solve": runs}
+    if args.config == "c3" and sc.n_points == 101124:
+        out["reference_regime"] = (
+            "pinned (tests/golden/eps_pq317_ref.npz, test_gpu_c3_eps_regime_matches_reference): the reference run to "
+            "1500 iterations reaches eps_abs at 1332 unperturbed and at 1145 when started 1e-13 off "
+            "(profiles/r5_c3_ref_curve1500*.json): the curve branches at iteration ~1069 on rounding-level "
+            "differences; the GPU follows the 1145 branch to 1e-4 relative, and both agree to 9e-11 comb_0 before it")
     if not hit_ms:
         out["note"] = (f"not reached in {len(runs)}/{len(runs)} solves with cap {args.geom_eps_cap} accepted iterations; "
                        f"min comb / eps_abs = {min(r['min_comb_over_eps'] for r in runs):.3g}")
