@@ -444,6 +444,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     // on two streams); AA_CONCURRENT=0 keeps it in line
     conc_ = pipe_z_ && !comm_;
     if (const char* e = std::getenv("AA_CONCURRENT")) conc_ = conc_ && e[0] != '0';
+    conc_fork_ = std::getenv("AA_CONC_FORK") ? std::atoi(std::getenv("AA_CONC_FORK")) : 0;
     // Z variant + Anderson: the two-set layout whether pipelined or not (same sums, same bits)
     stamp("factor");
     solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_, pipe_z_ ? 2 : 1,
@@ -933,22 +934,28 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         ev_begin("local_z");
         local_z_all(xfull_.p, u_.p, dzc, y_.p, LZ_NORMAL, false);
         ev_end("local_z");
-        if (side) {   // k-1's pass beside this iteration's Anderson step and comb rhs: its local
-            // step (one wave per SIMD) leaves room for their memory-bound waves (the two local
-            // steps cannot share a SIMD, so the fork comes after this iteration's)
+        // k-1's pass beside this iteration's Anderson step and comb rhs: its local step (one
+        // wave per SIMD) leaves room for their memory-bound waves (the two local steps cannot
+        // share a SIMD, so the fork comes after this iteration's); conc_fork_ (AA_CONC_FORK,
+        // measured) moves the fork behind the Anderson reduce (1) or the mix (2)
+        auto fork_side = [&](int at) {
+            if (!side || at != conc_fork_) return;
             AA_HIP(hipEventRecord(ev_fork_, s()));
             AA_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
             comb_finish_z(CTL_COMB_ZP, side_, ctrl_c_.p, red_c_.p, red_c_.p + nbg_, &lq2_, dup, dzp);
             AA_HIP(hipEventRecord(ev_join_, side_));
-        }
+        };
+        fork_side(0);
         Seg2 G{dzc, Z_, nullptr, 0};
         Seg2 out{z_.p, Z_, nullptr, 0};
         Seg2 none{nullptr, 0, nullptr, 0};
         ev_begin("aa");
         launch_aa_reduce(G, z_.p, Z_, aa_dF_.p, aa_dG_.p, c, aa_red_.p, aa_blocks_, none, m, s());
         reduce_aa();
+        fork_side(1);
         launch_aa_solve(c, aag_, aa_blocks_, m, s());
         launch_aa_mix(G, z_.p, Z_, aa_dF_.p, aa_dG_.p, c, out, m, s());   // in place (out == cur)
+        fork_side(2);
         ev_end("aa");
         // combined residual "for drawing figures" (Solver.cpp:217-233): extra solve + update_z
         if (pipe) {   // its rhs now (the next iteration overwrites the slots); the rest next iteration

@@ -148,6 +148,7 @@ private:
     // partials and work-queue counter; default_{u,z,x} alternate between two buffers by
     // iteration parity so the pass reads k-1's while iteration k writes its own.
     bool conc_ = false;
+    int conc_fork_ = 0;   // where the side pass forks: after the local step (0), AA reduce (1), mix (2)
     hipStream_t side_ = nullptr;
     hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
     DevBuf<Ctrl> ctrl_c_;

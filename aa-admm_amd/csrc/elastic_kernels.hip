@@ -1398,7 +1398,13 @@ __device__ void cod_solve_block(int n, CodLds& S, const double* b, double* x) {
 }
 
 // 1024 threads: summing up to 2048 x NVAL block partials is latency-bound
-constexpr int kSolveBlock = 1024;
+// 256 threads (one wave per SIMD): the block then fits on a CU beside the NeoHookean local step's
+// one 402-register wave per SIMD, so the Anderson step of iteration k is not held back until the
+// concurrent combined-residual pass's local step retires (a 1024-thread block, 4 waves per SIMD,
+// needs a CU of its own). The block partials are still summed in kSolveChunks chunks per value
+// (the 1024-thread layout), so the sums -- and the coefficients -- are unchanged.
+constexpr int kSolveBlock = 256;
+constexpr int kSolveThreads1024 = 1024;
 template <int MM>
 __global__ __launch_bounds__(kSolveBlock) void k_aa_solve(Ctrl* ctrl, const double* red, int nb) {
     if (ctrl->done || !ctrl->aa_active || ctrl->aa_skip) return;
@@ -1408,15 +1414,15 @@ __global__ __launch_bounds__(kSolveBlock) void k_aa_solve(Ctrl* ctrl, const doub
         return;
     }
     constexpr int NVAL = 2 + 2 * MM;
-    constexpr int NCH = kSolveBlock / NVAL;     // block partials are split into NCH chunks per value
+    constexpr int NCH = kSolveThreads1024 / NVAL;   // block partials are split into NCH chunks per value
     __shared__ double tot[NVAL];
     __shared__ double part[NCH * NVAL];
     const int iter = ctrl->aa_iter;
     if (iter > 0) {
-        // thread (chunk c, value v) sums partials c, c+NCH, ... of value v: independent loads,
-        // fixed order -> deterministic
-        if (threadIdx.x < NCH * NVAL) {
-            const int v = threadIdx.x % NVAL, c = threadIdx.x / NVAL;
+        // item (chunk c, value v) sums partials c, c+NCH, ... of value v: independent loads,
+        // fixed order -> deterministic; a thread takes items w, w + blockDim, ...
+        for (int w = threadIdx.x; w < NCH * NVAL; w += blockDim.x) {
+            const int v = w % NVAL, c = w / NVAL;
             double s = 0;
 #pragma unroll 8
             for (int b = c; b < nb; b += NCH) s += red[(size_t)b * NVAL + v];
