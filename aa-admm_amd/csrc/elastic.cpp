@@ -444,7 +444,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     // on two streams); AA_CONCURRENT=0 keeps it in line
     conc_ = pipe_z_ && !comm_;
     if (const char* e = std::getenv("AA_CONCURRENT")) conc_ = conc_ && e[0] != '0';
-    conc_fork_ = std::getenv("AA_CONC_FORK") ? std::atoi(std::getenv("AA_CONC_FORK")) : 0;
+    conc_fork_ = std::getenv("AA_CONC_FORK") ? std::atoi(std::getenv("AA_CONC_FORK")) : 1;
     // Z variant + Anderson: the two-set layout whether pipelined or not (same sums, same bits)
     stamp("factor");
     solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_, pipe_z_ ? 2 : 1,
@@ -870,9 +870,12 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
     // reject restore, the previous iteration's combined-residual pass and its rollback)
     double *duc = du_at(it), *dzc = dz_at(it), *dxc = dx_at(it);
     double *dup = du_at(it - 1), *dzp = dz_at(it - 1), *dxp = dx_at(it - 1);
-    // concurrent pass (conc_): iteration k-1's combined residual on side_, joined at the end of
-    // this iteration; not in the instrumented (per-kernel-class timing) pass
-    const bool side = pipe && it > 0 && conc_ && !instrument_;
+    // concurrent pass (conc_): iteration k-1's combined residual on its own control block, forked
+    // and joined (the rollback of a break then happens once, at the join); on side_ beside this
+    // iteration's Anderson step -- in line on the solver's stream in the instrumented
+    // (per-kernel-class timing) pass
+    const bool side = pipe && it > 0 && conc_;
+    hipStream_t sst = instrument_ ? s() : side_;
     ev_begin("grad");
     for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, accel ? 1 : 0, 0, c, s());
     ev_end("grad");
@@ -936,14 +939,22 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         ev_end("local_z");
         // k-1's pass beside this iteration's Anderson step and comb rhs: its local step (one
         // wave per SIMD) leaves room for their memory-bound waves (the two local steps cannot
-        // share a SIMD, so the fork comes after this iteration's); conc_fork_ (AA_CONC_FORK,
-        // measured) moves the fork behind the Anderson reduce (1) or the mix (2)
+        // share a SIMD, so the fork comes after this iteration's local step). Where exactly
+        // (AA_CONC_FORK, same-box A/B on C4): after the local step (0) 412 / 412 it/s, after the
+        // Anderson reduce (1, default: the reduce then streams at full occupancy) 415 / 419,
+        // after the mix (2) 393 / 396, in line 399 / 400
+        // (the instrumented pass runs it in line before the Anderson step, outside its timing bracket)
         auto fork_side = [&](int at) {
-            if (!side || at != conc_fork_) return;
-            AA_HIP(hipEventRecord(ev_fork_, s()));
-            AA_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
-            comb_finish_z(CTL_COMB_ZP, side_, ctrl_c_.p, red_c_.p, red_c_.p + nbg_, &lq2_, dup, dzp);
-            AA_HIP(hipEventRecord(ev_join_, side_));
+            if (!side || at != (instrument_ ? 0 : conc_fork_)) return;
+            if (sst != s()) {
+                AA_HIP(hipEventRecord(ev_fork_, s()));
+                AA_HIP(hipStreamWaitEvent(sst, ev_fork_, 0));
+            }
+            if (sst == s()) ev_begin("comb");
+            comb_finish_z(CTL_COMB_ZP, sst, ctrl_c_.p, red_c_.p, red_c_.p + nbg_, &lq2_, dup, dzp);
+            if (sst == s()) ev_end("comb");
+            if (sst != s()) AA_HIP(hipEventRecord(ev_join_, sst));
+            join_wait_ = sst != s();
         };
         fork_side(0);
         Seg2 G{dzc, Z_, nullptr, 0};
@@ -963,9 +974,8 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
             launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b2_.p, c, 0, s());
             ev_end("rhs");
             if (side) {   // join: the pass's records, and a break at comb_{k-1} undoes this iteration
-                AA_HIP(hipStreamWaitEvent(s(), ev_join_, 0));
-                launch_ctrl_join(c, ctrl_c_.p, s());
-                launch_copy(xfull_.p, dxp, nx, c, 2, s());   // x back to curr_x_{k-1}
+                join_dx_ = dxp;
+                join_side();
             }
             return;
         }
@@ -1007,6 +1017,15 @@ void ElasticSolver::comb_finish_z(int op, hipStream_t st, Ctrl* c, double* pa, d
 }
 
 // the last iteration's combined-residual pass (pipelined Z variant)
+// the concurrent pass's join, at the end of the iteration that forked it: its records merged, a
+// break at its comb undoing that iteration (done = 2, x back to the pass's curr_x). Measured: a
+// join delayed to the next iteration's two-set solve (the pass also beside that iteration's
+// gradient and rhs) gains nothing (415.9 / 416.3 vs 414.9 / 417.0 it/s on C4)
+void ElasticSolver::join_side() {
+    if (join_wait_) AA_HIP(hipStreamWaitEvent(s(), ev_join_, 0));
+    launch_ctrl_join(ctrl_.p, ctrl_c_.p, xfull_.p, join_dx_, 3LL * nf_, s());
+}
+
 void ElasticSolver::enqueue_comb_tail_z(int iters) {
     ev_begin("comb");
     solver_.solve(b2_.p, cxfull_.p, ctrl_.p, 0, s());

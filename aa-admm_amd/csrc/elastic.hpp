@@ -148,7 +148,10 @@ private:
     // partials and work-queue counter; default_{u,z,x} alternate between two buffers by
     // iteration parity so the pass reads k-1's while iteration k writes its own.
     bool conc_ = false;
-    int conc_fork_ = 0;   // where the side pass forks: after the local step (0), AA reduce (1), mix (2)
+    int conc_fork_ = 1;   // where the side pass forks: after the local step (0), AA reduce (1), mix (2)
+    bool join_wait_ = false;
+    double* join_dx_ = nullptr;
+    void join_side();
     hipStream_t side_ = nullptr;
     hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
     DevBuf<Ctrl> ctrl_c_;

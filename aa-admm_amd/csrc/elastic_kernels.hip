@@ -1732,25 +1732,36 @@ __global__ __launch_bounds__(256) void k_ctrl_fork(const Ctrl* __restrict__ ctrl
     const int* a = reinterpret_cast<const int*>(ctrl);
     int* b = reinterpret_cast<int*>(side);
     for (int i = threadIdx.x; i < (int)(sizeof(Ctrl) / sizeof(int)); i += blockDim.x) b[i] = a[i];
+    __syncthreads();
+    if (threadIdx.x == 0) side->pad_ = ctrl->done;   // done at the fork: a join acts only on a pass that ran
 }
 
 // Join: the pass's records become the solver's; a break (comb < 1e-20 or the eps stop, the
-// side's done) ends the step as the sequential order would have -- before iteration k: done = 2
-// (the gated copy that follows restores x = curr_x of k-1), and what iteration k changed that
-// outlives the step is taken back (its reject count, a prox failure of its local steps).
-__global__ void k_ctrl_join(Ctrl* __restrict__ ctrl, const Ctrl* __restrict__ side) {
-    if (ctrl->done) return;   // the side pass was gated off as well
-    ctrl->nrec = side->nrec;
-    ctrl->iters_run = side->iters_run;
-    ctrl->comb = side->comb;
-    ctrl->eps_abs = side->eps_abs;
-    if (side->done) {
-        ctrl->done = 2;
-        ctrl->nrej = side->nrej;
-        ctrl->fail = side->fail;
-    } else {
-        ctrl->fail = ctrl->fail ? ctrl->fail : side->fail;
+// side's done) ends the step as the sequential order would have -- before the iteration(s)
+// enqueued since the fork: done = 2, x restored to curr_x of the pass's iteration (dx), and what
+// those iterations changed that outlives the step is taken back (their reject count, a prox
+// failure of their local steps). Every block decides from the side block alone (written before
+// this kernel, read-only here), so the restore happens exactly once, at the join that found the
+// break -- a later pass forked with done set is inert.
+__global__ __launch_bounds__(256) void k_ctrl_join(Ctrl* __restrict__ ctrl, const Ctrl* __restrict__ side,
+                                                   double* __restrict__ x, const double* __restrict__ dx, long long n) {
+    const bool ran = side->pad_ == 0, brk = ran && side->done != 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ran) {
+        ctrl->nrec = side->nrec;
+        ctrl->iters_run = side->iters_run;
+        ctrl->comb = side->comb;
+        ctrl->eps_abs = side->eps_abs;
+        if (brk) {
+            ctrl->done = 2;
+            ctrl->nrej = side->nrej;
+            ctrl->fail = side->fail;
+        } else {
+            ctrl->fail = ctrl->fail ? ctrl->fail : side->fail;
+        }
     }
+    if (!brk) return;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        x[i] = dx[i];
 }
 
 // WindForce::project (ExplicitForce.cpp:47-104; helper::triangle_norm :28-39), Wejchert-Haumann
@@ -1800,8 +1811,8 @@ void launch_ctrl_fork(const Ctrl* ctrl, Ctrl* side, hipStream_t s) {
     AA_CHECK_LAUNCH();
 }
 
-void launch_ctrl_join(Ctrl* ctrl, const Ctrl* side, hipStream_t s) {
-    hipLaunchKernelGGL(k_ctrl_join, dim3(1), dim3(1), 0, s, ctrl, side);
+void launch_ctrl_join(Ctrl* ctrl, const Ctrl* side, double* x, const double* dx, long long n, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctrl_join, dim3(std::max(1, grid_for(n))), dim3(256), 0, s, ctrl, side, x, dx, n);
     AA_CHECK_LAUNCH();
 }
 

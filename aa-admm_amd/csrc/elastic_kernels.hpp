@@ -119,9 +119,9 @@ enum CtlOp { CTL_PRIM_CHECK = 0, CTL_PRIM_FINAL = 1, CTL_COMB_UX = 2, CTL_PRIM_C
 void launch_control(int op, Ctrl* ctrl, const double* red_a, const double* red_b, int nblocks, int accel,
                     double* hist_prim, double* hist_comb, int* hist_rej, hipStream_t s);
 // concurrent combined-residual pass: side = *ctrl (fork); records merged back, a break taken
-// as done = 2 with iteration k's reject count / failure flag restored (join)
+// as done = 2 with x = dx and the later iterations' reject count / failure flag restored, once (join)
 void launch_ctrl_fork(const Ctrl* ctrl, Ctrl* side, hipStream_t s);
-void launch_ctrl_join(Ctrl* ctrl, const Ctrl* side, hipStream_t s);
+void launch_ctrl_join(Ctrl* ctrl, const Ctrl* side, double* x, const double* dx, long long n, hipStream_t s);
 // dst = src (gate: !done, and reject if gate_reject)
 void launch_copy(double* dst, const double* src, long long n, const Ctrl* ctrl, int gate_reject, hipStream_t s);
 // GB/s of a 16-B/lane streaming read of `bytes` (the measured HBM read ceiling; bench.py)

@@ -324,7 +324,14 @@ def test_gpu_run_to_eps(builder, pkg, ctx):
     full, s = capi.run_scene(ctx, sc)
     s.close()
     c0 = full[0]["comb"]
-    eps = max(1e-6, 2.0 * c0.min() / c0[0])   # reached in the first step
+    # reached in the first step: late (near the curve's minimum) and early (a quarter of the way:
+    # the stop then comes mid-step, with iterations enqueued after it -- the concurrent comb pass
+    # must roll x back exactly once)
+    for eps in (max(1e-6, 2.0 * c0.min() / c0[0]), c0[len(c0) // 4] / c0[0] * (1.0 + 1e-12)):
+        _run_to_eps_matches_capped(capi, ctx, sc, eps)
+
+
+def _run_to_eps_matches_capped(capi, ctx, sc, eps):
     a = capi.solver_from_scene(ctx, sc)
     a.initialize(capi.settings_from_scene(sc))
     a.set_iterations(sc.iters, eps)
