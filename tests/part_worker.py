@@ -56,4 +56,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:   # the rank's own traceback, where the test can read it (torchrun's
+        import traceback    # summary crowds it out of the captured stderr)
+        with open(os.path.join(os.environ.get("AA_OUT", "."), f"rank{os.environ.get('RANK', '0')}.err"), "w") as f:
+            traceback.print_exc(file=f)
+        raise

@@ -38,7 +38,9 @@ def run_ranks(case, nranks, out, transport="host", extra_env=None, timeout=240):
                         "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
                         os.path.join(REPO, "tests", "part_worker.py")],
                        capture_output=True, text=True, timeout=timeout, env=env)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    if r.returncode != 0:
+        errs = "".join(f"--- {f.name}:\n{f.read_text()[-3000:]}\n" for f in sorted(out.glob("rank*.err")))
+        assert False, errs + r.stdout[-1000:] + r.stderr[-2000:]
     return [dict(np.load(out / f"rank{k}.npz")) for k in range(nranks)]
 
 
