@@ -329,176 +329,6 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     if (fail && ctrl) ctrl->fail = 1;
 }
 
-// k_local_z_hq with the queue's element batches claimed and their node data PREFETCHED one batch
-// ahead (AA_LQ_PREFETCH). A plain refill is a chain of three dependent round trips -- the queue
-// atomic, the elements' node ids, the node positions -- paid by the whole wave (one wave per SIMD:
-// nothing hides it; ~27 % of the kernel's cycles wait on s_waitcnt). Here a wave claims batches of
-// 64 elements (lane l of a batch register holds element base + l): while it works on the current
-// batch, the next one is claimed (atomic), then its node ids and then its node positions are loaded
-// into registers, one step per trip, so they have landed long before the next refill. A refill then
-// hands the batch's elements to the idle lanes by cross-lane shuffles (no memory round trip) and
-// only issues the independent loads (G, u, w, vol) together with the finalizing lanes' loads: one
-// round trip. ~56 registers more (402 -> ~458, still one wave per SIMD). Each element's arithmetic
-// is k_local_z_hq's (F summed over the nodes in the same order), so the results are bit-identical.
-template <int NV>
-__global__ __launch_bounds__(kBlock) void k_local_z_hqp(GroupDev g, const double* __restrict__ xfull,
-                                                        const double* __restrict__ u, double* __restrict__ z,
-                                                        double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
-                                                        int* __restrict__ queue, int refill,
-                                                        unsigned long long* __restrict__ stats) {
-    static_assert(NV == 4, "the prefetching queue is for tets");
-    if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
-    constexpr int D = 3 * (NV - 1), B = 64;
-    unsigned trips = 0, refills = 0;
-    __shared__ unsigned hist[101];
-    if (stats) {
-        for (int i = threadIdx.x; i < 101; i += blockDim.x) hist[i] = 0;
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & 63;
-    dev::HyperLbfgs L;
-    double v[D], x[D];
-    double vol = 0;
-    int e = -1, fail = 0;
-    bool active = false, pending = false, exhausted = false;
-    // batch registers: lane l holds element (base + l)'s node ids and node positions
-    int ci[NV], ni[NV];
-    double cp[NV][3], np[NV][3];
-    auto load_ids = [&](int base, int* ids) {
-        const int el = base + lane;
-#pragma unroll
-        for (int a = 0; a < NV; ++a) ids[a] = el < g.count ? g.idx[(size_t)a * g.count + el] : 0;
-    };
-    auto load_pos = [&](const int* ids, double (*pos)[3]) {
-#pragma unroll
-        for (int a = 0; a < NV; ++a)
-#pragma unroll
-            for (int r = 0; r < 3; ++r) pos[a][r] = xfull[3 * (size_t)ids[a] + r];
-    };
-    // wave-uniform batch state: current batch base / consumed, next batch base / stage
-    // (0: claimed, ids to load; 1: ids loaded, positions to load; 2: ready)
-    int nraw = 0;
-    if (lane == 0) nraw = atomicAdd(queue, 2 * B);
-    int cb = __shfl(nraw, 0, 64), cpos = 0;
-    int nb = cb + B, nstage = 1;
-    load_ids(cb, ci);
-    load_ids(nb, ni);
-    load_pos(ci, cp);
-    auto finalize = [&]() {
-#pragma unroll
-        for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * g.count + e] = x[i];
-        if (y) {
-            double F[D], Cp[D], uu[D];
-            gather_F<NV>(g, e, xfull, nf, F, Cp);
-            load_u<D>(g, e, u, uu);
-            write_slots<NV>(g, e, nf, g.w[e], x, Cp, uu, y);
-        }
-    };
-    for (;;) {
-        // one prefetch step per trip for the next batch
-        if (nstage == 0) {
-            nb = __shfl(nraw, 0, 64);
-            load_ids(nb, ni);
-            nstage = 1;
-        } else if (nstage == 1) {
-            load_pos(ni, np);
-            nstage = 2;
-        }
-        const bool need = !active && !exhausted;
-        const unsigned long long mask = __ballot(need);
-        if (!__any(active || need)) break;
-        ++trips;
-        if (mask && (__popcll(mask) >= refill || !__any(active))) {
-            ++refills;
-            if (pending) {
-                finalize();
-                pending = false;
-            }
-            const int k = __popcll(mask), avail = B - cpos, from_next = nstage == 2 ? B : 0;
-            const int rank = __popcll(mask & ((1ull << lane) - 1ull));
-            const bool in_cur = rank < avail, in_next = !in_cur && rank - avail < from_next;
-            const int slot = in_cur ? cpos + rank : rank - avail;
-            // every lane takes part in the shuffles (idle lanes read slot 0, unused)
-            const int src = need && (in_cur || in_next) ? slot : 0;
-            double pos[NV][3];
-#pragma unroll
-            for (int a = 0; a < NV; ++a) {
-#pragma unroll
-                for (int r = 0; r < 3; ++r) {
-                    const double pc = __shfl(cp[a][r], src, 64), pn = __shfl(np[a][r], src, 64);
-                    pos[a][r] = in_cur ? pc : pn;
-                }
-            }
-            const int base = in_cur ? cb : nb;
-            const int take = min(k, avail + from_next);
-            if (take >= avail && from_next) {   // the current batch is used up: the next one becomes it
-#pragma unroll
-                for (int a = 0; a < NV; ++a) {
-                    ci[a] = ni[a];
-#pragma unroll
-                    for (int r = 0; r < 3; ++r) cp[a][r] = np[a][r];
-                }
-                cb = nb;
-                cpos = take - avail;
-                if (lane == 0) nraw = atomicAdd(queue, B);
-                nstage = 0;
-            } else {
-                cpos = min(B, cpos + take);
-            }
-            if (need && (in_cur || in_next)) {
-                const int my = base + slot;
-                if (my >= g.count) {
-                    exhausted = true;
-                } else {
-                    e = my;
-                    // F = P x (gather_F's sums, positions from the batch registers)
-                    double F[D];
-#pragma unroll
-                    for (int i = 0; i < D; ++i) F[i] = 0;
-#pragma unroll
-                    for (int a = 0; a < NV; ++a)
-#pragma unroll
-                        for (int c = 0; c < NV - 1; ++c) {
-                            const double gc = g.G[(size_t)(c * NV + a) * g.count + e];
-                            F[3 * c + 0] += gc * pos[a][0]; F[3 * c + 1] += gc * pos[a][1]; F[3 * c + 2] += gc * pos[a][2];
-                        }
-                    const double w = g.w[e];
-                    double uu[D];
-                    load_u<D>(g, e, u, uu);
-#pragma unroll
-                    for (int i = 0; i < D; ++i) {
-                        v[i] = F[i] + uu[i] / w;
-                        x[i] = v[i];
-                    }
-                    vol = g.vol[e];
-                    if (L.start(g.mat, g.mu, g.lambda, g.k, vol, v, x)) {
-                        finalize();
-                        if (stats) atomicAdd(&hist[0], 1u);
-                    } else {
-                        active = true;
-                    }
-                }
-            }
-        }
-        if (active && L.iterate(g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail)) {
-            active = false;
-            pending = true;
-            if (stats) atomicAdd(&hist[min(L.k_it, 100)], 1u);
-        }
-    }
-    if (stats) {
-        if (lane == 0) {
-            atomicAdd(stats + 101, (unsigned long long)trips);
-            atomicAdd(stats + 102, (unsigned long long)refills);
-            atomicAdd(stats + 103, 1ull);
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < 101; i += blockDim.x)
-            if (hist[i]) atomicAdd(stats + i, (unsigned long long)hist[i]);
-    }
-    if (fail && ctrl) ctrl->fail = 1;
-}
-
 // k_local_z_hq with each element's L-BFGS split over a lane pair (dev::HyperLbfgs2, AA_LQ_SPLIT=1,
 // opt-in): a wave holds 32 elements, the state fits 256 registers, and a SIMD runs two waves -- the
 // one-wave kernel spends ~27 % of its cycles waiting on the refills' dependent loads with nothing
@@ -1780,10 +1610,7 @@ LocalQueue make_local_queue(int device, int* counter) {
     const char* sp = std::getenv("AA_LQ_SPLIT");
     q.split = sp ? sp[0] == '1' : false;
     if (q.split) q.ahead = false, q.hist = LQ_HIST_REGS;
-    const char* pf = std::getenv("AA_LQ_PREFETCH");
-    q.prefetch = !q.split && !q.ahead && q.hist == LQ_HIST_REGS && pf && pf[0] == '1';
     const void* kq = q.split ? (const void*)k_local_z_hq2<4>
-                   : q.prefetch ? (const void*)k_local_z_hqp<4>
                    : q.ahead ? (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hqa<4, LQ_HIST_YLDS>
                                                        : (const void*)k_local_z_hqa<4, LQ_HIST_REGS>)
                              : (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hq<4, LQ_HIST_YLDS>
@@ -1810,10 +1637,7 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
         const int resident = std::max(1, queue->resident), refill = queue->refill;
         const dim3 grid(std::min(nb, resident));
         const size_t lds = queue->lds_bytes;
-        if (queue->prefetch) {
-            hipLaunchKernelGGL((k_local_z_hqp<4>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode, ctrl,
-                               queue->counter, refill, queue->stats);
-        } else if (queue->split) {   // two lanes per element: half the elements per block
+        if (queue->split) {   // two lanes per element: half the elements per block
             const dim3 grid2(std::min(blocks_for(2LL * g.count), resident));
             hipLaunchKernelGGL((k_local_z_hq2<4>), grid2, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode, ctrl,
                                queue->counter, refill, queue->stats);

@@ -77,7 +77,6 @@ struct LocalQueue {
     int resident = 0, refill = 60, margin = 0;
     bool ahead = false;  // AA_LQ_AHEAD=1: k_local_z_hqa (one-element lookahead per lane)
     bool split = false;  // AA_LQ_SPLIT=1: k_local_z_hq2 (each element's L-BFGS over a lane pair)
-    bool prefetch = false;   // AA_LQ_PREFETCH=1: k_local_z_hqp (batches claimed, node data prefetched)
     int hist = 0;        // LqHistory: where the L-BFGS history lives (AA_LQ_LDS=1: y half in LDS)
     size_t lds_bytes = 0;
     // optional diagnostics (AA_LQ_STATS=1): [0..100] elements by L-BFGS iterations (0 = the start
