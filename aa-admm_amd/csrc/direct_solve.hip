@@ -945,6 +945,10 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
     // optional phase clock (AA_SUB_TIMING): kernel start, then after every barrier
     long long* ck = clk ? clk + (size_t)blockIdx.x * clk_stride : nullptr;
     if (ck && tid == 0) ck[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    // kSubU: every update vector consumed inside the subtree lives in LDS (its slot planned by the
+    // host over the levels' lifetimes), so a front pull is one LDS read after its ELL offset and
+    // only the root's update vector goes to HBM. Same sums in the same order: bit-identical.
+    const bool ul = (T.flags & DirectSolver::kSubU) != 0;
     for (int l = 0; l < T.nlvl; ++l) {
         const SubLevel L = lvls[T.lvl0 + l];
         const SubNode* ln = sn + (L.n0 - T.node0);
@@ -952,7 +956,8 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             const int it = items[L.fa0 + i];
             const SubNode nd = ln[it >> 16];
             const int c = it & 0xffff;
-            front_row<NR>(nd, c, ell, B0, B1, U, lds + K * nd.lds + NR * c);
+            if (ul) front_row<NR>(nd, c, ell, B0, B1, lds, lds + K * nd.lds + NR * c);
+            else front_row<NR>(nd, c, ell, B0, B1, U, lds + K * nd.lds + NR * c);
         }
         __syncthreads();
         if (ck && tid == 0) ck[1 + 2 * l] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -964,7 +969,10 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
             const double* G = Gc + nd.goff + r;
             const int cmax = r < p ? r + 1 : p;
             double fr[NR];   // a boundary row's own front value, gathered before the factor stream
-            if (r >= p) front_row<NR, false>(nd, r, ell, B0, B1, U, fr);
+            if (r >= p) {
+                if (ul) front_row<NR, false>(nd, r, ell, B0, B1, lds, fr);
+                else front_row<NR, false>(nd, r, ell, B0, B1, U, fr);
+            }
             double a[NR];
             zero<NR>(a);
             if constexpr (NR == 3) dot_rows_chunk<NR, NT>(G, (size_t)R, 0, cmax, f, a);
@@ -973,6 +981,10 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
                 double* y = Y + NR * (size_t)(nd.beg + r);
 #pragma unroll
                 for (int k = 0; k < NR; ++k) y[k] = a[k];
+            } else if (nd.slot >= 0) {   // consumed by the parent, inside this subtree (kSubU)
+                double* u = lds + K * nd.slot + NR * (r - p);
+#pragma unroll
+                for (int k = 0; k < NR; ++k) u[k] = fr[k] - a[k];
             } else {
                 double* u = U + K * nd.uoff + NR * (size_t)(r - p);
 #pragma unroll
@@ -1005,7 +1017,8 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
                                                  const long long* __restrict__ items2,
                                                  const double* __restrict__ Gr, const int* __restrict__ bnd,
                                                  const double* __restrict__ Y, double* __restrict__ X0,
-                                                 double* __restrict__ X1, const Ctrl* ctrl, int gate_reject,
+                                                 double* __restrict__ X1, const int* __restrict__ xg,
+                                                 const Ctrl* ctrl, int gate_reject,
                                                  long long* clk, int clk_stride, int node_off) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1019,6 +1032,18 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
         constexpr int W8 = sizeof(SubNode) / 8;
         for (int i = tid; i < T.nnode * W8; i += BLOCK) dst[i] = src[i];
     }
+    // kSubX: the x rows a boundary can name -- the subtree's own columns (written below, level by
+    // level, top-down) and the root's boundary (solved above the cut, staged here once) -- in LDS,
+    // so [y_P ; -x_B] needs one LDS read after its boundary offset instead of a second HBM trip
+    const bool xl = (T.flags & DirectSolver::kSubX) != 0;
+    if (xl)
+        for (int a = tid; a < T.nxg; a += BLOCK) {
+            double v[NR];
+            ld_ext<NR>(X0, X1, (size_t)xg[T.xg_off + a], v);
+            double* d = lds + K * (T.xst + 3 * a);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) d[k] = v[k];
+        }
     __syncthreads();
     long long* ck = clk ? clk + (size_t)blockIdx.x * clk_stride : nullptr;
     if (ck && tid == 0) ck[0] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1030,7 +1055,20 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             const int it = items[L.bv0 + i];
             const SubNode nd = ln[it >> 16];
             const int r = it & 0xffff;
-            bwd_row<NR>(nd, r, bnd, Y, X0, X1, lds + K * nd.lds + NR * r);
+            if (xl) {
+                double* v = lds + K * nd.lds + NR * r;
+                if (r < nd.p) {
+                    const double* y = Y + NR * (size_t)(nd.beg + r);
+#pragma unroll
+                    for (int k = 0; k < NR; ++k) v[k] = y[k];
+                } else {
+                    const double* xs = lds + K * bnd[nd.bnd_off + r - nd.p];
+#pragma unroll
+                    for (int k = 0; k < NR; ++k) v[k] = -xs[k];
+                }
+            } else {
+                bwd_row<NR>(nd, r, bnd, Y, X0, X1, lds + K * nd.lds + NR * r);
+            }
         }
         __syncthreads();
         if (ck && tid == 0) ck[ph++] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1066,6 +1104,11 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
                 off += min(p, (seg + 1) * kSubSegRows);
             }
             st_ext<NR>(X0, X1, (size_t)(nd.beg + j), a);
+            if (xl && nd.xo >= 0) {
+                double* xs = lds + K * (nd.xo + 3 * j);
+#pragma unroll
+                for (int k = 0; k < NR; ++k) xs[k] = a[k];
+            }
         }
         __syncthreads();
         if (ck && tid == 0) ck[ph++] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1248,6 +1291,8 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         std::vector<SubTree> strees;
         std::vector<int> items;
         std::vector<long long> items2;
+        std::vector<int> fidx(nn_, -1), bidx(nn_, -1);   // forward / backward record of every fused supernode
+        std::vector<std::vector<int>> sub_all;      // supernodes of every subtree (root first)
         sub_lds_f_ = sub_lds_b_ = 0;
         if (cut_height_ >= 0) {
             for (int rt : roots_at(cut_height_)) {
@@ -1266,6 +1311,9 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                         SubNode nd{};
                         nd.p = p[v]; nd.nb = nb[v]; nd.beg = beg[v]; nd.bnd_off = bnd_off[v]; nd.ell_w = ell_w[v];
                         nd.lds = 0; nd.goff = goff[v]; nd.uoff = uoff[v]; nd.ell_off = ell_off[v]; nd.ldr = ldr[v];
+                        nd.slot = -1;   // forward copy: LDS update-vector slot (kSubU, set below)
+                        nd.xo = -1;
+                        fidx[v] = (int)snodes.size();
                         snodes.push_back(nd);
                     }
                     // forward: f_P offsets, assembly items, row items
@@ -1285,6 +1333,7 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                     const int n1 = (int)snodes.size();
                     for (size_t k = 0; k < lv.size(); ++k) {
                         SubNode nd = snodes[L.n0 + k];
+                        bidx[lv[k]] = (int)snodes.size();
                         nd.lds = lb / 8;
                         lb += 24 * (p[lv[k]] + nb[lv[k]]);
                         snodes.push_back(nd);
@@ -1318,9 +1367,12 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
                 T.nnode = (int)snodes.size() - T.node0;
                 sub_nodes_max_ = std::max(sub_nodes_max_, T.nnode);
                 strees.push_back(T);
+                sub_all.push_back(std::move(all));
             }
         }
         n_sub_ = (int)strees.size();
+        plan_sub_lds(F, kids, p, nb, beg, uoff, bnd_off, ell_w, ell_off, ell, bnd, fidx, bidx, sub_all, strees, snodes, KS,
+                     stats, s);
         if (stats) {
             double by = 0;
             int nsn = 0;
@@ -1829,10 +1881,110 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     AA_HIP(hipStreamSynchronize(s));
 }
 
-// dynamic LDS of a fused-subtree launch: the level vectors (K sets), then the staged node records
+// dynamic LDS of a fused-subtree launch: the level vectors (K sets), the LDS-resident update
+// vectors (forward) or x rows (backward), then the staged node records
 size_t DirectSolver::sub_lds_bytes(int K, bool fwd) const {
-    const size_t v = (size_t)K * (fwd ? sub_lds_f_ : sub_lds_b_);
+    const size_t v = (size_t)K * (fwd ? sub_lds_f_ + sub_lds_u_ : sub_lds_b_ + sub_lds_x_);
     return (v + 15) / 16 * 16 + (size_t)sub_nodes_max_ * sizeof(SubNode);
+}
+
+void DirectSolver::plan_sub_lds(const SupernodalFactor& F, const std::vector<std::vector<int>>& kids,
+                                const std::vector<int>& p, const std::vector<int>& nb, const std::vector<int>& beg,
+                                const std::vector<long long>& uoff, const std::vector<int>& bnd_off,
+                                const std::vector<int>& ell_w, const std::vector<long long>& ell_off,
+                                std::vector<long long>& ell, std::vector<int>& bnd, const std::vector<int>& fidx,
+                                const std::vector<int>& bidx, const std::vector<std::vector<int>>& sub_all, std::vector<SubTree>& strees,
+                                std::vector<SubNode>& snodes, int KS, bool stats, hipStream_t s) {
+    sub_lds_u_ = sub_lds_x_ = 0;
+    const char* eu = std::getenv("AA_SUB_LDS_U");
+    const char* ex = std::getenv("AA_SUB_LDS_X");
+    const bool want_u = !eu || eu[0] != '0', want_x = !ex || ex[0] != '0';
+    // vector bytes (KS sets) a launch may hold: 160 KiB less the staged records
+    const long long cap = (160LL * 1024 - (long long)sub_nodes_max_ * (long long)sizeof(SubNode)) / 16 * 16;
+    const int ubase = sub_lds_f_ / 8, xbase = sub_lds_b_ / 8;   // the regions follow the level vectors
+    std::vector<int> slot(nn_, -1), xg;
+    int nu = 0, nx = 0;
+    for (size_t t = 0; t < sub_all.size(); ++t) {
+        const std::vector<int>& all = sub_all[t];
+        SubTree& T = strees[t];
+        const int rt = all[0];
+        if (want_u) {
+            const int peak = plan_update_slots(all, kids, F.height, nb, slot);
+            if ((long long)KS * (sub_lds_f_ + 24LL * peak) <= cap) {
+                T.flags |= kSubU;
+                ++nu;
+                sub_lds_u_ = std::max(sub_lds_u_, 24 * peak);
+                for (int v : all) {
+                    snodes[fidx[v]].slot = slot[v] >= 0 ? ubase + 3 * slot[v] : -1;
+                    // v's pull lists name its children's update entries (all inside the subtree)
+                    const long long e1 = ell_off[v] + (long long)(p[v] + nb[v]) * ell_w[v];
+                    for (long long i = ell_off[v]; i < e1; ++i) {
+                        const long long e = ell[i];
+                        if (e < 0) continue;
+                        long long to = -1;
+                        for (int c : kids[v])
+                            if (e >= uoff[c] && e < uoff[c] + 3LL * nb[c]) { to = ubase + 3LL * slot[c] + (e - uoff[c]); break; }
+                        if (to < 0) throw Error(ERR_STATE, "DirectSolver: internal error: a pull outside its fused subtree");
+                        ell[i] = to;
+                    }
+                }
+            }
+        }
+        if (want_x) {
+            // the x rows a boundary inside the subtree can name: the columns of its inner supernodes
+            // (a boundary names ancestors only, so leaves' columns never) and the root's boundary
+            // (every entry leaving the subtree is one of them: fill-path property of the
+            // elimination tree; checked, else the subtree keeps HBM)
+            std::vector<std::pair<int, int>> inner;   // (first column, supernode), sorted
+            int rows = 0;
+            for (int v : all)
+                if (!kids[v].empty()) { inner.emplace_back(beg[v], v); rows += p[v]; }
+            std::sort(inner.begin(), inner.end());
+            const std::vector<int>& rb = F.bnd[rt];
+            const int nxg = (int)rb.size();
+            if ((long long)KS * (sub_lds_b_ + 24LL * (rows + nxg)) <= cap) {
+                std::vector<int> xo(inner.size());
+                for (size_t k = 0, r = 0; k < inner.size(); r += p[inner[k].second], ++k) xo[k] = xbase + 3 * (int)r;
+                std::vector<std::pair<int, int>> rw;
+                bool ok = true;
+                for (int v : all) {
+                    for (int a = 0; a < nb[v] && ok; ++a) {
+                        const int i = bnd[bnd_off[v] + a];
+                        auto in = std::upper_bound(inner.begin(), inner.end(), std::make_pair(i, INT32_MAX));
+                        int o = -1;
+                        if (in != inner.begin()) {
+                            --in;
+                            const int w = in->second;
+                            if (i < beg[w] + p[w]) o = xo[in - inner.begin()] + 3 * (i - beg[w]);
+                        }
+                        if (o < 0) {
+                            auto it = std::lower_bound(rb.begin(), rb.end(), i);
+                            if (it == rb.end() || *it != i) { ok = false; break; }
+                            o = xbase + 3 * (rows + (int)(it - rb.begin()));
+                        }
+                        rw.emplace_back(bnd_off[v] + a, o);
+                    }
+                    if (!ok) break;
+                }
+                if (ok) {
+                    for (const auto& q : rw) bnd[q.first] = q.second;
+                    for (size_t k = 0; k < inner.size(); ++k) snodes[bidx[inner[k].second]].xo = xo[k];
+                    T.flags |= kSubX;
+                    ++nx;
+                    T.xst = xbase + 3 * rows;
+                    T.nxg = nxg;
+                    T.xg_off = (int)xg.size();
+                    xg.insert(xg.end(), rb.begin(), rb.end());
+                    sub_lds_x_ = std::max(sub_lds_x_, 24 * (rows + nxg));
+                }
+            }
+        }
+    }
+    if (xg.empty()) xg.push_back(0);
+    sub_xg_.upload(xg, s);
+    if (stats)
+        std::fprintf(stderr, "[solve] fused subtrees in LDS: update vectors %d / %zu (%d B), x rows %d / %zu (%d B), per 3 columns\n",
+                     nu, sub_all.size(), sub_lds_u_, nx, sub_all.size(), sub_lds_x_);
 }
 
 void DirectSolver::solve(const double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
@@ -1909,7 +2061,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
     AA_HIP(hipStreamIsCapturing(s, &cst));
     const bool clk_on = sub_timing_ > 0 && cst == hipStreamCaptureStatusNone && n_sub_ > 0;
-    const int noff_f = (K * sub_lds_f_ + 15) / 16 * 16, noff_b = (K * sub_lds_b_ + 15) / 16 * 16;
+    const int noff_f = (K * (sub_lds_f_ + sub_lds_u_) + 15) / 16 * 16, noff_b = (K * (sub_lds_b_ + sub_lds_x_) + 15) / 16 * 16;
     // queue heads and dependency counters of the streamed runs start from zero every solve
     if (stream_) AA_HIP(hipMemsetAsync(sync_.p, 0, sizeof(int) * ((size_t)n_heads_ + 2 * (size_t)nn_), s));
 #define SUBF(BL) hipLaunchKernelGGL((nt_rows_ ? k_fwd_sub<BL, NR, true> : k_fwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, true), s, sub_trees_.p, \
@@ -1974,7 +2126,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
         if (L.bt_count) launch_btiles<NR>(L.btw, L.bt_count, L.bt_first, x0, x1, 0, ctrl, gate_reject, s);
     }
 #define SUBB(BL) hipLaunchKernelGGL((nt_rows_ ? k_bwd_sub<BL, NR, true> : k_bwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, false), s, sub_trees_.p, \
-                                    sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, \
+                                    sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, sub_xg_.p, \
                                     ctrl, gate_reject, clk_on ? sub_clk_.p + 64 * (size_t)n_sub_ : nullptr, 64, noff_b)
     if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }
 #undef SUBB

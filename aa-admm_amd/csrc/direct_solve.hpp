@@ -82,9 +82,18 @@ public:
     struct SubNode {   // a supernode inside a fused subtree; lds = its vector's offset in LDS,
         int p, nb, beg, bnd_off, ell_w, lds, slot, ldr;   // slot = its backward segment partials
         long long goff, uoff, ell_off;
+        int xo, pad;   // backward copy, kSubX: LDS offset of its x rows (-1: no boundary names them)
     };
     struct SubLevel { int n0, fa0, nfa, fr0, nfr, bv0, nbv, bc0, nbc, bs0, nbs, pad; };   // item ranges
-    struct SubTree { int lvl0, nlvl, node0, nnode; };   // nodes [node0, node0 + nnode) staged in LDS
+    // nodes [node0, node0 + nnode) staged in LDS. flags: kSubU = the children's update vectors
+    // stay in LDS (the forward records' slot = the LDS offset of their own, -1 = global U; the
+    // ELL pull lists of the subtree's supernodes hold LDS offsets); kSubX = the x rows a boundary
+    // inside the subtree can name stay in LDS -- the columns of its inner supernodes (backward
+    // record's xo) and the root's boundary (entry a at xst + 3a, staged from x[xg[xg_off + a]]);
+    // the subtree's boundary lists hold those LDS offsets.
+    // Offsets are in doubles of a 3-column solve (scaled by NR / 3 on the device, like U's).
+    static constexpr int kSubU = 1, kSubX = 2;
+    struct SubTree { int lvl0, nlvl, node0, nnode, flags, xst, nxg, xg_off; };
     // split-K backward of large supernodes: a tile (64 columns from c0, nr rows from r0) and the
     // per-column-block reduction of its nt tile partials (64 x 3 doubles each, from poff)
     // toff: the tile's block in the packed tile stream Gt_ (see build: every tile's factor entries
@@ -177,7 +186,18 @@ private:
     DevBuf<double> top_f_, top_x_;   // [set][3 * top_p_]: summed front, partial then summed x_top
     // fused bottom subtrees
     int n_sub_ = 0, sub_lds_f_ = 0, sub_lds_b_ = 0, cut_height_ = -1, sub_block_ = 256, sub_nodes_max_ = 0;
+    int sub_lds_u_ = 0, sub_lds_x_ = 0;   // LDS-resident update vectors / x rows (bytes per 3 columns)
+    DevBuf<int> sub_xg_;                  // per kSubX subtree: its root's boundary (global x rows)
     size_t sub_lds_bytes(int K, bool fwd) const;
+    // kSubU / kSubX per subtree where the extra LDS fits beside the level vectors and records;
+    // rewrites those subtrees' ELL pull lists and boundary lists to LDS offsets (build only)
+    void plan_sub_lds(const SupernodalFactor& F, const std::vector<std::vector<int>>& kids, const std::vector<int>& p,
+                      const std::vector<int>& nb, const std::vector<int>& beg, const std::vector<long long>& uoff,
+                      const std::vector<int>& bnd_off, const std::vector<int>& ell_w,
+                      const std::vector<long long>& ell_off, std::vector<long long>& ell, std::vector<int>& bnd,
+                      const std::vector<int>& fidx, const std::vector<int>& bidx,
+                      const std::vector<std::vector<int>>& sub_all,
+                      std::vector<SubTree>& strees, std::vector<SubNode>& snodes, int KS, bool stats, hipStream_t s);
     int wave_p_ = kWaveP, wave_r_ = kWaveR;   // row-task / split-K thresholds (AA_SOLVE_WAVEP / _WAVER)
     DevBuf<SubNode> sub_nodes_;
     DevBuf<SubLevel> sub_levels_;

@@ -76,4 +76,46 @@ inline int choose_cut_height(const CutPlanIn& a) {
     return -1;
 }
 
+// LDS slots (in rows) for the update vectors a fused subtree keeps on chip (kSubU). `all` is the
+// subtree's supernodes, root first; the root's update vector leaves the subtree (slot -1). The
+// forward kernel runs a level in two phases -- (1) the front gathers of the level's supernodes,
+// (2) their rows, whose boundary rows gather their own front values again and then write the
+// supernode's update vector -- so a child's slot is live from its own level until its parent's
+// level has finished both phases: slots of level h are taken first-fit, and the children of
+// level h are released after them. Returns the peak row count (the LDS region's size).
+inline int plan_update_slots(const std::vector<int>& all, const std::vector<std::vector<int>>& kids,
+                             const std::vector<int>& height, const std::vector<int>& nb, std::vector<int>& slot) {
+    if (all.empty()) return 0;
+    const int root = all[0];
+    int H = 0;
+    for (int v : all) H = std::max(H, height[v]);
+    std::vector<std::vector<int>> at(H + 1);
+    for (int v : all) at[height[v]].push_back(v);
+    std::vector<std::pair<int, int>> used;   // (first row, rows), sorted by first row
+    int peak = 0;
+    for (int h = 0; h <= H; ++h) {
+        std::sort(at[h].begin(), at[h].end());
+        for (int v : at[h]) {
+            slot[v] = -1;
+            if (v == root || nb[v] == 0) continue;
+            int pos = 0;
+            size_t i = 0;
+            for (; i < used.size(); ++i) {
+                if (used[i].first - pos >= nb[v]) break;
+                pos = used[i].first + used[i].second;
+            }
+            used.insert(used.begin() + (long)i, {pos, nb[v]});
+            slot[v] = pos;
+            peak = std::max(peak, pos + nb[v]);
+        }
+        for (int v : at[h])
+            for (int c : kids[v]) {
+                if (slot[c] < 0) continue;
+                for (size_t i = 0; i < used.size(); ++i)
+                    if (used[i].first == slot[c]) { used.erase(used.begin() + (long)i); break; }
+            }
+    }
+    return peak;
+}
+
 }  // namespace aa

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import os
+import re
 
 from golden_io import GOLDEN, case_names, compare, load_case, scenes
 
@@ -240,6 +241,31 @@ def test_gpu_packed_tiles_and_nt_loads_bit_identical(pkg, ctx, monkeypatch, knob
     for x, y in zip(ref, got):
         for k in ("prim", "comb", "reject", "x", "v"):
             assert np.array_equal(np.asarray(x[k]), np.asarray(y[k])), (name, k)
+
+
+@pytest.mark.parametrize("pipe", ["0", "1"])
+def test_gpu_fused_subtrees_lds_vectors_bit_identical(pkg, ctx, monkeypatch, capfd, pipe):
+    """The fused subtrees keep their children's update vectors (forward) and the x rows their
+    boundaries name (backward) in LDS (DirectSolver kSubU / kSubX) instead of passing them
+    through HBM (AA_SUB_LDS_U=0 / AA_SUB_LDS_X=0): the same products and sums in the same order,
+    so bit-identical trajectories -- one-set (AA_Z_PIPELINE=0) and two-set solves alike."""
+    sc = scenes.tet_drop(40, 16, 20, iters=12, n_steps=2)
+    monkeypatch.setenv("AA_Z_PIPELINE", pipe)
+    monkeypatch.setenv("AA_SOLVE_MIN_SUBTREES", "32")   # 64 k tets: tall subtrees (none at 256)
+    monkeypatch.setenv("AA_SOLVE_STATS", "1")
+    monkeypatch.setenv("AA_SUB_LDS_U", "0")
+    monkeypatch.setenv("AA_SUB_LDS_X", "0")
+    off, _ = pkg.capi.run_scene(ctx, sc)
+    capfd.readouterr()
+    monkeypatch.delenv("AA_SUB_LDS_U")
+    monkeypatch.delenv("AA_SUB_LDS_X")
+    on, _ = pkg.capi.run_scene(ctx, sc)
+    err = capfd.readouterr().err
+    m = re.search(r"fused subtrees in LDS: update vectors (\d+) / (\d+) .* x rows (\d+) / (\d+)", err)
+    assert m and int(m.group(1)) > 0 and int(m.group(3)) > 0, err[-2000:]
+    for a, b in zip(off, on):
+        for k in ("prim", "comb", "reject", "x", "v"):
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
 
 
 @pytest.mark.parametrize("ahead", ["0", "1"])

@@ -4,6 +4,7 @@ judged relative to comb_0 -- 1e-8 over the first 40 accepted iterations and 1e-6
 curve (Anderson trajectories amplify rounding differences; the oracle meets the same bounds
 against the reference); solutions 1e-8 relative; closest points 1e-13 absolute."""
 import os
+import re
 import sys
 
 import numpy as np
@@ -318,6 +319,29 @@ def test_gpu_c5_eps_regime_matches_reference(pkg, ctx):
     assert abs(c.min() / want.min() - 1.0) <= 0.1, (c.min(), want.min())
     assert c.min() > float(ref["eps_abs"]) and want.min() > float(ref["eps_abs"])
     g.close()
+
+
+@pytest.mark.parametrize("min_sub", ["64", "16"])
+def test_gpu_geom_fused_subtrees_lds_vectors_bit_identical(pkg, ctx, monkeypatch, capfd, min_sub):
+    """The geometry solver's fused subtrees with their update vectors and boundary x rows in LDS
+    (DirectSolver kSubU / kSubX) against HBM (AA_SUB_LDS_U=0 / AA_SUB_LDS_X=0): bit-identical
+    ALM trajectories; few subtrees make them tall (many levels, most update vectors inside)."""
+    sc = pkg.geom_scenes.pq_heightfield(160, 150, iters=60, aa_m=10, noise=0.3)
+    monkeypatch.setenv("AA_SOLVE_MIN_SUBTREES", min_sub)
+    monkeypatch.setenv("AA_SOLVE_STATS", "1")
+    runs = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("AA_SUB_LDS_U", on)
+        monkeypatch.setenv("AA_SUB_LDS_X", on)
+        capfd.readouterr()
+        h, g = pkg.capi.run_geom(ctx, sc)
+        err = capfd.readouterr().err
+        runs.append((h, g.runtime().rejects))
+        g.close()
+    m = re.search(r"fused subtrees in LDS: update vectors (\d+) / (\d+) .* x rows (\d+) / (\d+)", err)
+    assert m and int(m.group(1)) > 0 and int(m.group(3)) > 0, err[-2000:]
+    (a, ra), (b, rb) = runs
+    assert np.array_equal(a["comb"], b["comb"]) and np.array_equal(a["x"], b["x"]) and ra == rb
 
 
 @pytest.mark.parametrize("builder", [

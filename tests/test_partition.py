@@ -45,6 +45,19 @@ def test_fused_subtree_cut_checks_aggregate_lds(tmp_path):
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+def test_fused_subtree_update_slots_never_overlap_live(tmp_path):
+    """The LDS slots of the fused subtrees' update vectors (solve_plan.hpp plan_update_slots):
+    on 300 random trees, no slot written in a level overlaps one still to be read
+    (tests/cpp/update_slots.cpp replays the forward kernel's two-phase schedule)."""
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "update_slots")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "aa-admm_amd", "csrc"),
+                    os.path.join(REPO, "tests", "cpp", "update_slots.cpp"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 WORKER = r"""
 import importlib, os, sys
 import numpy as np
