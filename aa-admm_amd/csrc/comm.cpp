@@ -116,13 +116,26 @@ public:
     void allreduce_sum_host(double* buf, size_t n) override {
         if (n == 0) return;
         if (fn_(buf, (long long)n, user_) != 0) throw Error(ERR_DEVICE, "host all-reduce callback failed");
+        if (verify_) check_same(buf, n);
     }
     bool capturable() const override { return false; }
 
 private:
+    // AA_COMM_VERIFY=1 (tests): every rank must hold the same bits after a sum -- a 64-bit FNV-1a
+    // hash of the result, its halves summed over the ranks, must equal size x this rank's
+    void check_same(const double* buf, size_t n) {
+        unsigned long long h = 1469598103934665603ull;
+        const unsigned char* b = reinterpret_cast<const unsigned char*>(buf);
+        for (size_t i = 0; i < n * sizeof(double); ++i) { h ^= b[i]; h *= 1099511628211ull; }
+        double v[2] = {(double)(h >> 32), (double)(h & 0xffffffffull)}, mine[2] = {v[0], v[1]};
+        if (fn_(v, 2, user_) != 0) throw Error(ERR_DEVICE, "host all-reduce callback failed");
+        if (v[0] != size_ * mine[0] || v[1] != size_ * mine[1])
+            throw Error(ERR_DEVICE, "host all-reduce: the ranks hold different sums (" + std::to_string(n) + " values)");
+    }
     HostAllreduceFn fn_;
     void* user_;
     std::vector<double> buf_;
+    bool verify_ = std::getenv("AA_COMM_VERIFY") && std::getenv("AA_COMM_VERIFY")[0] == '1';
 };
 
 // Rehearsal transport: ONE rank of a P-way partition on its own GPU, every other rank absent.

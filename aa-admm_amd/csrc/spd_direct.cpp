@@ -433,7 +433,7 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
     // all of them throw together (the top fronts are summed, so they fail or pass on all ranks)
     // the failure keeps its own type (aa::Error codes, std::bad_alloc) on the rank it happened on;
     // only the other ranks throw the synthesized "another rank's part" error
-    auto agree = [&](const std::exception_ptr& err) {
+    auto agree = [&](const std::exception_ptr& err, const char* where = "part") {
         if (!part) {
             if (err) std::rethrow_exception(err);
             return;
@@ -441,7 +441,24 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
         double bad = err ? 1.0 : 0.0;
         part->reduce_host(&bad, 1);
         if (err) std::rethrow_exception(err);
-        if (bad > 0) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite (on another rank's part)");
+        if (bad > 0)
+            throw std::runtime_error(std::string("multifrontal_cholesky: matrix not positive definite (on another rank's ") +
+                                     where + ")");
+    };
+    // the shared top fronts, one at a time in postorder: every rank factors the same summed front,
+    // so an outcome that differs between ranks is a defect -- each front's outcome is agreed, so
+    // all ranks stop together and the others name it instead of failing in a later collective
+    auto factor_top = [&](std::vector<int>& pos) {
+        for (int s = 0; s < nn; ++s) {
+            if (tree.part[s] != -1) continue;
+            std::exception_ptr err;
+            try {
+                factor_front(C, s, pos, true);
+            } catch (...) {
+                err = std::current_exception();
+            }
+            agree(err, "copy of a top front");
+        }
     };
     if (!dense) {   // host only: postorder, parallel inside the large fronts
         std::vector<int> pos(n, -1);
@@ -453,9 +470,7 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
             err = std::current_exception();
         }
         agree(err);
-        if (part)
-            for (int s = 0; s < nn; ++s)
-                if (tree.part[s] == -1) factor_front(C, s, pos, true);
+        if (part) factor_top(pos);
     } else {
         // tree-parallel: independent subtrees are OpenMP tasks (a front waits for its children),
         // each host front is factored by one thread; the large fronts near the root go to the
@@ -509,8 +524,7 @@ SupernodalFactor multifrontal_cholesky(const CsrMatrix& A, const NdTree& tree, D
         agree(err);
         if (part) {
             std::vector<int> pos(n, -1);
-            for (int s = 0; s < nn; ++s)
-                if (tree.part[s] == -1) factor_front(C, s, pos, true);
+            factor_top(pos);
         }
     }
     for (int s = 0; s < nn; ++s) {
