@@ -178,7 +178,10 @@ public:
         int info[2] = {0, 0};
         AA_HIP(hipMemcpyAsync(info, info_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s_));
         AA_HIP(hipStreamSynchronize(s_));
-        if (info[0] != 0) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite");
+        if (info[0] != 0)
+            throw std::runtime_error("multifrontal_cholesky: matrix not positive definite (GPU front " + std::to_string(s) +
+                                     ", order " + std::to_string(f) + ", pivot " + std::to_string(info[0]) + " of " +
+                                     std::to_string(p) + ", " + std::to_string(kids.size()) + " children)");
         if (info[1] != 0) throw std::runtime_error("multifrontal_cholesky: singular diagonal block");
         // ---- outputs in the host layouts
         auto fetch = [&](std::vector<double>& out, const double* src, int ld, int rows, int cols, int lower) {

@@ -371,7 +371,10 @@ void factor_front(FrontCtx& C, int s, std::vector<int>& pos, bool inner_parallel
     for (int k = 0; k < p; ++k) {
         double* ck = &Fc[(size_t)k * f];
         const double d = ck[k];
-        if (!(d > 0.0)) throw std::runtime_error("multifrontal_cholesky: matrix not positive definite");
+        if (!(d > 0.0))
+            throw std::runtime_error("multifrontal_cholesky: matrix not positive definite (host front " + std::to_string(s) +
+                                     ", order " + std::to_string(f) + ", pivot " + std::to_string(k) + " of " +
+                                     std::to_string(p) + ", d = " + std::to_string(d) + ")");
         const double dk = std::sqrt(d);
         ck[k] = dk;
         const double inv = 1.0 / dk;
