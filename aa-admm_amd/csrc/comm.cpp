@@ -106,11 +106,11 @@ public:
     HostComm(HostAllreduceFn fn, void* user, int rank, int size) : fn_(fn), user_(user) { rank_ = rank; size_ = size; }
     void allreduce_sum(const double* src, double* dst, size_t n, hipStream_t s) override {
         if (n == 0) return;
-        buf_.resize(n);
-        AA_HIP(hipMemcpyAsync(buf_.data(), src, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        double* b = buf_.get(n);   // pinned: the copies are stream-ordered DMA (common.hpp PinnedBuf)
+        AA_HIP(hipMemcpyAsync(b, src, n * sizeof(double), hipMemcpyDeviceToHost, s));
         AA_HIP(hipStreamSynchronize(s));
-        allreduce_sum_host(buf_.data(), n);
-        AA_HIP(hipMemcpyAsync(dst, buf_.data(), n * sizeof(double), hipMemcpyHostToDevice, s));
+        allreduce_sum_host(b, n);
+        AA_HIP(hipMemcpyAsync(dst, b, n * sizeof(double), hipMemcpyHostToDevice, s));
         AA_HIP(hipStreamSynchronize(s));
     }
     void allreduce_sum_host(double* buf, size_t n) override {
@@ -134,7 +134,7 @@ private:
     }
     HostAllreduceFn fn_;
     void* user_;
-    std::vector<double> buf_;
+    PinnedBuf<double> buf_;
     bool verify_ = std::getenv("AA_COMM_VERIFY") && std::getenv("AA_COMM_VERIFY")[0] == '1';
 };
 

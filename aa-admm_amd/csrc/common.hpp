@@ -60,6 +60,30 @@ struct DevBuf {
     size_t bytes() const { return n * sizeof(T); }
 };
 
+// Pinned (page-locked) host staging buffer that only grows. Host <-> device copies of setup data
+// and of the host-staged all-reduce go through it, so they are plain DMA in stream order: the
+// 4-rank partition test saw a top front's last column stale after a pageable hipMemcpyAsync +
+// hipStreamSynchronize on one of four processes sharing the GPU (round 5).
+template <typename T>
+struct PinnedBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    T* get(size_t count) {
+        if (count > n) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            n = 0;
+            AA_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), count * sizeof(T), hipHostMallocDefault));
+            n = count;
+        }
+        return p;
+    }
+};
+
 // Records what `enqueue` puts on stream s into an instantiated graph. Returns false -- with the
 // stream out of capture mode and nothing recorded kept -- when any part fails (e.g. a collective
 // the communication library cannot capture); the caller then launches eagerly.

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <map>
 #include <set>
+#include <cstring>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -122,9 +123,14 @@ public:
         if (na > 0) {
             int* di = ii_.get(2 * (size_t)na);
             double* dv = dv_.get(na);
-            AA_HIP(hipMemcpyAsync(di, ai.data(), na * sizeof(int), hipMemcpyHostToDevice, s_));
-            AA_HIP(hipMemcpyAsync(di + na, aj.data(), na * sizeof(int), hipMemcpyHostToDevice, s_));
-            AA_HIP(hipMemcpyAsync(dv, av.data(), na * sizeof(double), hipMemcpyHostToDevice, s_));
+            // host data through pinned staging (common.hpp PinnedBuf): stream-ordered DMA
+            int* hi = hint_.get(2 * (size_t)na);
+            double* hv = hdbl_.get(na);
+            std::memcpy(hi, ai.data(), na * sizeof(int));
+            std::memcpy(hi + na, aj.data(), na * sizeof(int));
+            std::memcpy(hv, av.data(), na * sizeof(double));
+            AA_HIP(hipMemcpyAsync(di, hi, 2 * (size_t)na * sizeof(int), hipMemcpyHostToDevice, s_));
+            AA_HIP(hipMemcpyAsync(dv, hv, na * sizeof(double), hipMemcpyHostToDevice, s_));
             hipLaunchKernelGGL(k_scatter_coo, dim3(blocks_for(na)), dim3(kBlock), 0, s_, F, f, di, di + na, dv, na);
             AA_CHECK_LAUNCH();
             AA_HIP(hipStreamSynchronize(s_));   // the host vectors are the caller's
@@ -132,13 +138,17 @@ public:
         for (const Child& c : kids) {
             if (c.m == 0) continue;
             int* dmap = map_.get(c.m);
-            AA_HIP(hipMemcpyAsync(dmap, c.map, c.m * sizeof(int), hipMemcpyHostToDevice, s_));
+            int* hm = hint_.get(c.m);
+            std::memcpy(hm, c.map, c.m * sizeof(int));
+            AA_HIP(hipMemcpyAsync(dmap, hm, c.m * sizeof(int), hipMemcpyHostToDevice, s_));
             const double* Usrc;
             int rowmajor;
             std::unique_ptr<DevBuf<double>> own;
             if (c.U) {
                 double* du = up_.get((size_t)c.m * c.m);
-                AA_HIP(hipMemcpyAsync(du, c.U->data(), (size_t)c.m * c.m * sizeof(double), hipMemcpyHostToDevice, s_));
+                double* hu = hdbl_.get((size_t)c.m * c.m);
+                std::memcpy(hu, c.U->data(), (size_t)c.m * c.m * sizeof(double));
+                AA_HIP(hipMemcpyAsync(du, hu, (size_t)c.m * c.m * sizeof(double), hipMemcpyHostToDevice, s_));
                 Usrc = du;
                 rowmajor = 1;
             } else {
@@ -175,9 +185,10 @@ public:
             rb_check(rocblas_dtrmm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_none,
                                    rocblas_diagonal_non_unit, nb, p, &one, L, p, F + p, f, Md, nb), "rocblas_dtrmm");
         }
-        int info[2] = {0, 0};
-        AA_HIP(hipMemcpyAsync(info, info_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s_));
+        int* hinfo = hint_.get(2);
+        AA_HIP(hipMemcpyAsync(hinfo, info_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s_));
         AA_HIP(hipStreamSynchronize(s_));
+        const int info[2] = {hinfo[0], hinfo[1]};
         if (info[0] != 0)
             throw std::runtime_error("multifrontal_cholesky: matrix not positive definite (GPU front " + std::to_string(s) +
                                      ", order " + std::to_string(f) + ", pivot " + std::to_string(info[0]) + " of " +
@@ -191,8 +202,10 @@ public:
             const dim3 blk(32, 8), grd((cols + 31) / 32, (rows + 31) / 32);
             hipLaunchKernelGGL(k_to_rowmajor, grd, blk, 0, s_, t, src, ld, rows, cols, lower);
             AA_CHECK_LAUNCH();
-            AA_HIP(hipMemcpyAsync(out.data(), t, out.size() * sizeof(double), hipMemcpyDeviceToHost, s_));
+            double* h = hdbl_.get(out.size());
+            AA_HIP(hipMemcpyAsync(h, t, out.size() * sizeof(double), hipMemcpyDeviceToHost, s_));
             AA_HIP(hipStreamSynchronize(s_));
+            std::memcpy(out.data(), h, out.size() * sizeof(double));
         };
         fetch(Linv, L, p, p, p, 1);
         fetch(LBP, F + p, f, nb, p, 0);
@@ -223,6 +236,8 @@ private:
     DevBuf<int> info_;
     Grow<double> F_, L_, M_, T_, dv_, up_;
     Grow<int> ii_, map_;
+    PinnedBuf<double> hdbl_;   // host staging (pinned) for the copies above
+    PinnedBuf<int> hint_;
 };
 
 }  // namespace
