@@ -72,6 +72,7 @@ public:
     }
     ~RcclComm() override {
         if (comm_) (void)rccl().comm_destroy(comm_);
+        if (hs_) (void)hipStreamDestroy(hs_);
     }
     void allreduce_sum(const double* src, double* dst, size_t n, hipStream_t s) override {
         if (n == 0) return;
@@ -79,16 +80,20 @@ public:
     }
     void allreduce_sum_host(double* buf, size_t n) override {
         if (n == 0) return;
-        double* d = nullptr;
-        AA_HIP(hipMalloc(&d, n * sizeof(double)));
-        hipError_t e = hipMemcpy(d, buf, n * sizeof(double), hipMemcpyHostToDevice);
-        if (e == hipSuccess) {
-            const ncclResult_t rc = rccl().all_reduce(d, d, n, ncclDouble, ncclSum, comm_, nullptr);
-            if (rc != ncclSuccess) { (void)hipFree(d); nccl_check(rc, "ncclAllReduce"); }
-            e = hipMemcpy(buf, d, n * sizeof(double), hipMemcpyDeviceToHost);
-        }
-        (void)hipFree(d);
-        AA_HIP(e);
+        // through pinned staging (common.hpp PinnedBuf), copies and the sum ordered on one stream;
+        // every device sum this rank enqueued before (the solver's stream is non-blocking) has
+        // finished first, so the ranks' collectives reach the communicator in program order
+        AA_HIP(hipDeviceSynchronize());
+        double* h = stage_.get(n);
+        std::memcpy(h, buf, n * sizeof(double));
+        if (dstage_.n < n) dstage_.alloc(n);
+        double* d = dstage_.p;
+        if (!hs_) AA_HIP(hipStreamCreateWithFlags(&hs_, hipStreamNonBlocking));
+        AA_HIP(hipMemcpyAsync(d, h, n * sizeof(double), hipMemcpyHostToDevice, hs_));
+        nccl_check(rccl().all_reduce(d, d, n, ncclDouble, ncclSum, comm_, hs_), "ncclAllReduce");
+        AA_HIP(hipMemcpyAsync(h, d, n * sizeof(double), hipMemcpyDeviceToHost, hs_));
+        AA_HIP(hipStreamSynchronize(hs_));
+        std::memcpy(buf, h, n * sizeof(double));
     }
     // Eager by default: a partitioned step with RCCL launches its kernels and all-reduces
     // without a hipGraph (the device-side control still needs no host sync, and at P ranks the
@@ -99,6 +104,9 @@ public:
 
 private:
     ncclComm_t comm_ = nullptr;
+    PinnedBuf<double> stage_;
+    DevBuf<double> dstage_;
+    hipStream_t hs_ = nullptr;
 };
 
 class HostComm final : public Comm {
