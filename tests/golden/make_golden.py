@@ -210,6 +210,26 @@ def full_bunny40(tmp):
     print("full_bunny40_z_nh_aa6", [len(s["prim"]) for s in steps])
 
 
+def full_c4(tmp):
+    """BASELINE configs[3] at full size (make_tet_blocks(100,40,50) = 1 000 000 NeoHookean tets,
+    211 191 nodes, z-AA m=6): ONE time step of 10 iterations of the reference itself (its setup
+    factors the 633 k-dof system with Eigen's SimplicialLDLT: about three hours here), the
+    per-iteration residuals and positions / velocities on 512 sampled nodes plus their column sums."""
+    sc = scenes.tet_drop(100, 40, 50, iters=10, n_steps=1)
+    steps = run_ref(sc, tmp)
+    rng = np.random.default_rng(6)
+    sample = np.sort(rng.choice(sc.n_nodes, 512, replace=False)).astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "full_c4_block_z_nh_aa6.npz"), digest=scene_digest(sc), sample=sample,
+                        nrec=np.array([len(s["prim"]) for s in steps]),
+                        prim=np.concatenate([s["prim"] for s in steps]), comb=np.concatenate([s["comb"] for s in steps]),
+                        reject=np.concatenate([s["reject"] for s in steps]),
+                        x_sample=np.stack([s["x"][sample] for s in steps]),
+                        v_sample=np.stack([s["v"][sample] for s in steps]),
+                        x_sum=np.stack([s["x"].sum(0) for s in steps]), v_sum=np.stack([s["v"].sum(0) for s in steps]),
+                        step_ms=np.array([s["step_ms"] for s in steps]))
+    print("full_c4_block_z_nh_aa6", [len(s["prim"]) for s in steps])
+
+
 def residual_files(tmp):
     """The reference's own Solver::save() output (Solver.hpp:130-155: result/residual-<m>.txt,
     written by every step()) for one (u,x)-variant and one z-variant scene, kept verbatim as data
@@ -235,6 +255,10 @@ def main(only=None):
     if only == ["--full"]:
         with tempfile.TemporaryDirectory() as tmp:
             full_drop40(tmp)
+        return
+    if only == ["--full-c4"]:
+        with tempfile.TemporaryDirectory() as tmp:
+            full_c4(tmp)
         return
     if only == ["--bunny"]:
         with tempfile.TemporaryDirectory() as tmp:

@@ -335,6 +335,28 @@ def test_gpu_full_drop40_matches_reference(pkg, ctx):
     assert not fails, fails
 
 
+def test_gpu_full_c4_matches_reference(pkg, ctx):
+    """BASELINE configs[3] at full size against the reference itself: make_tet_blocks(100,40,50) =
+    1 000 000 NeoHookean tets, 211 191 nodes, z-AA m=6, one time step of 10 iterations
+    (tests/golden/full_c4_block_z_nh_aa6.npz, make_golden.py --full-c4: the reference's own
+    SimplicialLDLT setup takes hours on the CPU, so the fixture holds one step). The bars of the
+    64k-tet golden: the residual curve relative to comb_0 (1e-6, L-BFGS prox path), equal reject
+    flags, positions / velocities on 512 sampled nodes and their column sums (1e-6 relative)."""
+    import sys
+    from golden_io import check_full_golden
+    path = os.path.join(GOLDEN, "full_c4_block_z_nh_aa6.npz")
+    if not os.path.exists(path):
+        pytest.skip("full-size C4 reference fixture not generated")
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import scene_digest
+    ref = np.load(path)
+    sc = scenes.tet_drop(100, 40, 50, iters=10, n_steps=1)
+    assert np.array_equal(scene_digest(sc), ref["digest"]), "regenerated scene differs from the fixture's"
+    got, _ = pkg.capi.run_scene(ctx, sc)
+    fails = check_full_golden(got, ref)
+    assert not fails, fails
+
+
 @pytest.mark.parametrize("builder", [
     lambda: scenes.tet_drop(12, 4, 6, iters=120, n_steps=2),                       # Z, pipelined comb
     lambda: scenes.cloth(24, 24, iters=120, n_steps=2),                            # UX, fused comb record
