@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <map>
 #include <set>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -165,9 +166,44 @@ public:
             AA_HIP(hipStreamSynchronize(s_));   // before the staging buffers / held matrix are reused
         }
         if (reduce_front) reduce_front(F, (size_t)f * f);   // partitioned top: the ranks' partial fronts summed
+        // Kept-copy check (default on; AA_FRONT_CHECK=0 off): the assembled front is kept (one
+        // device copy); if its Cholesky fails, the copy is factored again and the outcome reported --
+        // a second failure is the matrix's (thrown with the diagnostics), a success means the first
+        // attempt was at fault and the run goes on with the second. Added for an intermittent
+        // not-positive-definite report seen only with several processes sharing one GPU.
+        double* Fk = nullptr;
+        if (check_) {
+            Fk = K_.get((size_t)f * f);
+            AA_HIP(hipMemcpyAsync(Fk, F, (size_t)f * f * sizeof(double), hipMemcpyDeviceToDevice, s_));
+        }
         // ---- partial factorization
         const double one = 1.0, mone = -1.0;
         rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
+        if (check_) {
+            int* hc = hint_.get(1);
+            AA_HIP(hipMemcpyAsync(hc, info_.p, sizeof(int), hipMemcpyDeviceToHost, s_));
+            AA_HIP(hipStreamSynchronize(s_));
+            if (hc[0] != 0) {
+                const int first = hc[0];
+                double* hf = hdbl_.get((size_t)f * f);
+                AA_HIP(hipMemcpyAsync(hf, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToHost, s_));
+                AA_HIP(hipStreamSynchronize(s_));
+                size_t nonfinite = 0;
+                double dmin = 1e300, dmax = 0;
+                for (size_t q = 0; q < (size_t)f * f; ++q) nonfinite += !std::isfinite(hf[q]);
+                for (int q = 0; q < f; ++q) { dmin = std::min(dmin, hf[(size_t)q * f + q]); dmax = std::max(dmax, hf[(size_t)q * f + q]); }
+                AA_HIP(hipMemcpyAsync(F, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToDevice, s_));
+                rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
+                AA_HIP(hipMemcpyAsync(hc, info_.p, sizeof(int), hipMemcpyDeviceToHost, s_));
+                AA_HIP(hipStreamSynchronize(s_));
+                char msg[320];
+                std::snprintf(msg, sizeof msg, "[front-check] front %d order %d p %d: potrf info %d; kept copy: %zu non-finite, "
+                              "diag [%.3e, %.3e]; potrf again on the copy: info %d", s, f, p, first, nonfinite, dmin, dmax, hc[0]);
+                std::fprintf(stderr, "%s\n", msg);
+                if (hc[0] != 0) throw std::runtime_error(std::string("multifrontal_cholesky: matrix not positive definite ") + msg);
+                // the copy factored: the first attempt was at fault, go on with this one
+            }
+        }
         if (nb > 0) {
             rb_check(rocblas_dtrsm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
                                    rocblas_diagonal_non_unit, nb, p, &one, F, f, F + p, f), "rocblas_dtrsm");
@@ -238,6 +274,8 @@ private:
     Grow<int> ii_, map_;
     PinnedBuf<double> hdbl_;   // host staging (pinned) for the copies above
     PinnedBuf<int> hint_;
+    Grow<double> K_;           // AA_FRONT_CHECK: the assembled front, kept
+    bool check_ = !(std::getenv("AA_FRONT_CHECK") && std::getenv("AA_FRONT_CHECK")[0] == '0');
 };
 
 }  // namespace

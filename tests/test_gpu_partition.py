@@ -32,7 +32,7 @@ def _free_port():
 
 
 def run_ranks(case, nranks, out, transport="host", extra_env=None, timeout=240):
-    env = dict(os.environ, AA_CASE=case, AA_OUT=str(out), AA_TRANSPORT=transport, AA_DEVICE="0", AA_COMM_VERIFY="1",
+    env = dict(os.environ, AA_CASE=case, AA_OUT=str(out), AA_TRANSPORT=transport, AA_DEVICE="0", AA_COMM_VERIFY="1", AA_FRONT_CHECK="1",
                OMP_NUM_THREADS="4", **(extra_env or {}))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
                         "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
