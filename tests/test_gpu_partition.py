@@ -38,6 +38,13 @@ def run_ranks(case, nranks, out, transport="host", extra_env=None, timeout=240):
                         "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
                         os.path.join(REPO, "tests", "part_worker.py")],
                        capture_output=True, text=True, timeout=timeout, env=env)
+    # a GPU front whose first Cholesky failed and whose kept copy factored (dense_gpu.hip, DESIGN
+    # §5) is reported on stderr: kept in gpurun_out/ for the diagnosis, the run itself is valid
+    notes = [ln for ln in (r.stderr or "").splitlines() if "[front-check]" in ln]
+    if notes:
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", "front_check.log"), "a") as fh:
+            fh.write(f"{case} P={nranks}: " + " | ".join(notes) + "\n")
     if r.returncode != 0:
         errs = "".join(f"--- {f.name}:\n{f.read_text()[-3000:]}\n" for f in sorted(out.glob("rank*.err")))
         assert False, errs + r.stdout[-1000:] + r.stderr[-2000:]
