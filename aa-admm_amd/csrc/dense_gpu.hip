@@ -22,6 +22,7 @@
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 #include <string>
 
 #include "common.hpp"
@@ -89,12 +90,11 @@ public:
     explicit RocFrontBackend(hipStream_t s) : s_(s) {
         AA_HIP(hipStreamGetDevice(s_, &dev_));
         AA_HIP(hipSetDevice(dev_));
-        rb_check(rocblas_create_handle(&h_), "rocblas_create_handle");
-        rb_check(rocblas_set_stream(h_, s_), "rocblas_set_stream");
+
         info_.alloc(2);
     }
     ~RocFrontBackend() override {
-        if (h_) (void)rocblas_destroy_handle(h_);
+        for (auto& kv : handles_) (void)rocblas_destroy_handle(kv.second);
     }
     bool holds(int s) const override {
         std::lock_guard<std::mutex> g(mu_);
@@ -110,6 +110,14 @@ public:
                 std::vector<double>& M, std::vector<double>* U) override {
         std::lock_guard<std::mutex> g(mu_);
         AA_HIP(hipSetDevice(dev_));
+        // one rocBLAS handle per calling thread (rocBLAS handles are per-thread objects; the
+        // OpenMP workers of the tree-parallel factorization take turns here), and nothing of a
+        // previous call still in flight on the device when this one starts or ends: with several
+        // processes sharing the GPU the partition tests found fronts factored from stale data
+        //  -- these are the two assumptions the backend no longer relies on
+        rocblas_handle h_ = handle();
+        AA_HIP(hipDeviceSynchronize());
+        struct DevSync { ~DevSync() { (void)hipDeviceSynchronize(); } } dev_sync;
         const auto t0 = std::chrono::steady_clock::now();
         struct Tally {   // time inside the backend (AA_SETUP_TIMES)
             RocFrontBackend* b;
@@ -266,7 +274,18 @@ public:
 private:
     hipStream_t s_;
     int dev_ = 0;
-    rocblas_handle h_ = nullptr;
+    std::map<std::thread::id, rocblas_handle> handles_;
+    rocblas_handle handle() {   // (under mu_)
+        auto it = handles_.find(std::this_thread::get_id());
+        if (it != handles_.end()) return it->second;
+        rocblas_handle h = nullptr;
+        rb_check(rocblas_create_handle(&h), "rocblas_create_handle");
+        rb_check(rocblas_set_stream(h, s_), "rocblas_set_stream");
+        // deterministic rocBLAS kernels: every rank must factor the shared top bit-identically
+        rb_check(rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed), "rocblas_set_atomics_mode");
+        handles_[std::this_thread::get_id()] = h;
+        return h;
+    }
     mutable std::mutex mu_;
     std::map<int, std::unique_ptr<DevBuf<double>>> held_;
     DevBuf<int> info_;
