@@ -623,7 +623,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
         // same grid on every rank (the largest rank's) so the partial layouts line up
         aa_blocks_ = aa_reduce_blocks(st_.variant == AA_VARIANT_UX ? zmax + 3LL * nf_ : zmax);
         (void)dim;
-        const int mm = m <= 8 ? 8 : (m <= 16 ? 16 : 32);
+        const int mm = aa_window_bucket(m);
         aa_red_.alloc((size_t)aa_blocks_ * (2 + 2 * mm)); aa_red_.zero(s());
         if (comm_) { aa_red_g_.alloc(aa_red_.n); aa_red_g_.zero(s()); aag_ = aa_red_g_.p; }
         else aag_ = aa_red_.p;

@@ -1856,7 +1856,13 @@ int aa_reduce_blocks(long long dim) {   // more partials only pay off on large v
     return grid_for(dim) < cap ? grid_for(dim) : cap;
 }
 
-static int mm_bucket(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : 32); }
+// m <= 12 (C3's m = 10) has its own bucket: k_aa_reduce<12> 125 VGPRs / k_aa_mix<12> 110 against
+// 157 / 135 at 16 -- 4 waves per SIMD instead of 3 (AA_AA_MM12=0: the 16 bucket, for the A/B)
+int aa_window_bucket(int m) {
+    static const bool b12 = !(std::getenv("AA_AA_MM12") && std::getenv("AA_AA_MM12")[0] == '0');
+    return m <= 8 ? 8 : (b12 && m <= 12 ? 12 : (m <= 16 ? 16 : 32));
+}
+static int mm_bucket(int m) { return aa_window_bucket(m); }
 
 static bool aa_cols() {
     static const bool on = !(std::getenv("AA_AA_COLS") && std::getenv("AA_AA_COLS")[0] == '0');
@@ -1869,6 +1875,7 @@ void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, doub
 #define AA_RED_ARGS G, cur, eff, dF, dG, ctrl, red, copy_to, comb_a, comb_b, comb_nb, hist_prim, hist_comb, hist_rej, mask
     switch (mm_bucket(m)) {
         case 8: hipLaunchKernelGGL(k_aa_reduce<8>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
+        case 12: hipLaunchKernelGGL(k_aa_reduce<12>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
         case 16: hipLaunchKernelGGL(k_aa_reduce<16>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS); break;
         default:   // m > 16: column-parallel (AA_AA_COLS=0: the row-parallel kernel)
             if (aa_cols()) hipLaunchKernelGGL(k_aa_reduce_cols<32>, dim3(nblocks), dim3(kBlock), 0, s, AA_RED_ARGS);
@@ -1882,6 +1889,7 @@ void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, doub
 void launch_aa_solve(Ctrl* ctrl, const double* red, int nblocks, int m, hipStream_t s) {
     switch (mm_bucket(m)) {
         case 8: hipLaunchKernelGGL(k_aa_solve<8>, dim3(1), dim3(kSolveBlock), 0, s, ctrl, red, nblocks); break;
+        case 12: hipLaunchKernelGGL(k_aa_solve<12>, dim3(1), dim3(kSolveBlock), 0, s, ctrl, red, nblocks); break;
         case 16: hipLaunchKernelGGL(k_aa_solve<16>, dim3(1), dim3(kSolveBlock), 0, s, ctrl, red, nblocks); break;
         default: hipLaunchKernelGGL(k_aa_solve<32>, dim3(1), dim3(kSolveBlock), 0, s, ctrl, red, nblocks); break;
     }
@@ -1893,6 +1901,7 @@ void launch_aa_mix(Seg2 G, double* cur, long long eff, double* dF, double* dG, C
     const long long dim = G.na + G.nb;
     switch (mm_bucket(m)) {
         case 8: hipLaunchKernelGGL(k_aa_mix<8>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
+        case 12: hipLaunchKernelGGL(k_aa_mix<12>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
         case 16: hipLaunchKernelGGL(k_aa_mix<16>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
         default: hipLaunchKernelGGL(k_aa_mix<32>, dim3(grid_for(dim)), dim3(kBlock), 0, s, G, cur, eff, dF, dG, ctrl, out); break;
     }

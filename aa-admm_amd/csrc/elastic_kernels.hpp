@@ -146,7 +146,9 @@ void launch_wind(const int* tris3, const int* tri_ord, const int* lvl_ptr, int n
 // G: the fixed-point map output (2 segments); cur: the stored current iterate (current_u_);
 // dF/dG: history (column-major, eff x m / dim x m); copy_to: optional copy of G (the
 // "default" iterate kept for the reject test); out: where the accelerated iterate goes.
-// m: window (selects the register-resident accumulator bucket 8/16/32).
+// m: window (selects the register-resident accumulator bucket 8/12/16/32, aa_window_bucket;
+// the block partials hold 2 + 2 aa_window_bucket(m) values).
+int aa_window_bucket(int m);
 int aa_reduce_blocks(long long dim);
 // comb_a/comb_b given: the UX combined residual, break test and record are fused in front
 void launch_aa_reduce(Seg2 G, const double* cur, long long eff, double* dF, double* dG, Ctrl* ctrl, double* red,

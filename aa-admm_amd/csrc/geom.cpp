@@ -699,7 +699,7 @@ void GeomSolver::prepare_m(int m) {
         aa_dF_.alloc((size_t)m * (plain_ ? std::max<long long>(1, Zh_) : dim)); aa_dF_.zero(s());
         aa_dG_.alloc((size_t)m * dim); aa_dG_.zero(s());
         aa_blocks_ = aa_reduce_blocks(zh_max_ + 3LL * n_);   // the same grid on every rank
-        const int mm = m <= 8 ? 8 : (m <= 16 ? 16 : 32);
+        const int mm = aa_window_bucket(m);
         aa_red_.alloc((size_t)aa_blocks_ * (2 + 2 * mm)); aa_red_.zero(s());
         if (comm_) { aa_red_g_.alloc(aa_red_.n); aa_red_g_.zero(s()); aag_ = aa_red_g_.p; }
         else aag_ = aa_red_.p;
