@@ -73,6 +73,24 @@ __global__ void k_to_rowmajor(double* __restrict__ dst, const double* __restrict
     }
 }
 
+// number of non-finite entries of the column-major rows x cols block at a (leading dimension ld),
+// added into *out (one atomic per workgroup)
+__global__ void k_count_nonfinite(const double* __restrict__ a, int ld, int rows, int cols, int* out) {
+    __shared__ int sc[kBlock / 64];
+    int c = 0;
+    const long long n = (long long)rows * cols;
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
+        c += !isfinite(a[(k / rows) * ld + k % rows]);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sc[w];
+        if (t) atomicAdd(out, t);
+    }
+}
+
 template <class T>
 struct Grow {   // device buffer that only grows
     DevBuf<T> b;
@@ -87,11 +105,12 @@ public:
     // dev_: the stream's device. factor() runs on OpenMP worker threads whose HIP current device
     // is 0 unless set, so every entry point selects dev_ first: buffers, the handle and the
     // stream must all live on the solver's GPU (ranks 1..P-1 of a partitioned run).
-    explicit RocFrontBackend(hipStream_t s) : s_(s) {
+    explicit RocFrontBackend(hipStream_t s, bool test_hooks = true) : s_(s) {
+        if (!test_hooks) poison_ = 0;
         AA_HIP(hipStreamGetDevice(s_, &dev_));
         AA_HIP(hipSetDevice(dev_));
 
-        info_.alloc(2);
+        info_.alloc(3);   // potrf info, trtri info, non-finite output count
     }
     ~RocFrontBackend() override {
         for (auto& kv : handles_) (void)rocblas_destroy_handle(kv.second);
@@ -174,64 +193,78 @@ public:
             AA_HIP(hipStreamSynchronize(s_));   // before the staging buffers / held matrix are reused
         }
         if (reduce_front) reduce_front(F, (size_t)f * f);   // partitioned top: the ranks' partial fronts summed
-        // Kept-copy check (default on; AA_FRONT_CHECK=0 off): the assembled front is kept (one
-        // device copy); if its Cholesky fails, the copy is factored again and the outcome reported --
-        // a second failure is the matrix's (thrown with the diagnostics), a success means the first
-        // attempt was at fault and the run goes on with the second. Added for an intermittent
-        // not-positive-definite report seen only with several processes sharing one GPU.
-        double* Fk = nullptr;
+        double* Fk = nullptr;   // the kept copy (below)
         if (check_) {
             Fk = K_.get((size_t)f * f);
             AA_HIP(hipMemcpyAsync(Fk, F, (size_t)f * f * sizeof(double), hipMemcpyDeviceToDevice, s_));
         }
-        // ---- partial factorization
+        // ---- partial factorization: potrf, trsm, syrk, trtri, trmm; returns the potrf / trtri infos
+        // and (check_) the number of non-finite entries in F (L11, L21, Schur complement), L11^-1 and M
         const double one = 1.0, mone = -1.0;
-        rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
-        if (check_) {
-            int* hc = hint_.get(1);
-            AA_HIP(hipMemcpyAsync(hc, info_.p, sizeof(int), hipMemcpyDeviceToHost, s_));
-            AA_HIP(hipStreamSynchronize(s_));
-            if (hc[0] != 0) {
-                const int first = hc[0];
-                double* hf = hdbl_.get((size_t)f * f);
-                AA_HIP(hipMemcpyAsync(hf, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToHost, s_));
-                AA_HIP(hipStreamSynchronize(s_));
-                size_t nonfinite = 0;
-                double dmin = 1e300, dmax = 0;
-                for (size_t q = 0; q < (size_t)f * f; ++q) nonfinite += !std::isfinite(hf[q]);
-                for (int q = 0; q < f; ++q) { dmin = std::min(dmin, hf[(size_t)q * f + q]); dmax = std::max(dmax, hf[(size_t)q * f + q]); }
-                AA_HIP(hipMemcpyAsync(F, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToDevice, s_));
-                rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
-                AA_HIP(hipMemcpyAsync(hc, info_.p, sizeof(int), hipMemcpyDeviceToHost, s_));
-                AA_HIP(hipStreamSynchronize(s_));
-                char msg[320];
-                std::snprintf(msg, sizeof msg, "[front-check] front %d order %d p %d: potrf info %d; kept copy: %zu non-finite, "
-                              "diag [%.3e, %.3e]; potrf again on the copy: info %d", s, f, p, first, nonfinite, dmin, dmax, hc[0]);
-                std::fprintf(stderr, "%s\n", msg);
-                if (hc[0] != 0) throw std::runtime_error(std::string("multifrontal_cholesky: matrix not positive definite ") + msg);
-                // the copy factored: the first attempt was at fault, go on with this one
-            }
-        }
-        if (nb > 0) {
-            rb_check(rocblas_dtrsm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
-                                   rocblas_diagonal_non_unit, nb, p, &one, F, f, F + p, f), "rocblas_dtrsm");
-            rb_check(rocblas_dsyrk(h_, rocblas_fill_lower, rocblas_operation_none, nb, p, &mone, F + p, f, &one,
-                                   F + (size_t)p * f + p, f), "rocblas_dsyrk");
-        }
         double* L = L_.get((size_t)p * p);
-        AA_HIP(hipMemcpy2DAsync(L, p * sizeof(double), F, f * sizeof(double), p * sizeof(double), p,
-                                hipMemcpyDeviceToDevice, s_));
-        rb_check(rocsolver_dtrtri(h_, rocblas_fill_lower, rocblas_diagonal_non_unit, p, L, p, info_.p + 1),
-                 "rocsolver_dtrtri");
-        double* Md = nullptr;
-        if (nb > 0) {
-            Md = M_.get((size_t)nb * p);
-            rb_check(rocblas_dtrmm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_none,
-                                   rocblas_diagonal_non_unit, nb, p, &one, L, p, F + p, f, Md, nb), "rocblas_dtrmm");
+        double* Md = nb > 0 ? M_.get((size_t)nb * p) : nullptr;
+        auto attempt = [&](int* out) {
+            AA_HIP(hipMemsetAsync(info_.p, 0, 3 * sizeof(int), s_));
+            rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
+            if (nb > 0) {
+                rb_check(rocblas_dtrsm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                                       rocblas_diagonal_non_unit, nb, p, &one, F, f, F + p, f), "rocblas_dtrsm");
+                rb_check(rocblas_dsyrk(h_, rocblas_fill_lower, rocblas_operation_none, nb, p, &mone, F + p, f, &one,
+                                       F + (size_t)p * f + p, f), "rocblas_dsyrk");
+            }
+            AA_HIP(hipMemcpy2DAsync(L, p * sizeof(double), F, f * sizeof(double), p * sizeof(double), p,
+                                    hipMemcpyDeviceToDevice, s_));
+            rb_check(rocsolver_dtrtri(h_, rocblas_fill_lower, rocblas_diagonal_non_unit, p, L, p, info_.p + 1),
+                     "rocsolver_dtrtri");
+            if (nb > 0)
+                rb_check(rocblas_dtrmm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_none,
+                                       rocblas_diagonal_non_unit, nb, p, &one, L, p, F + p, f, Md, nb), "rocblas_dtrmm");
+            if (check_) {
+                const auto cnt = [&](const double* a, int ld, int rows, int cols) {
+                    if ((long long)rows * cols == 0) return;
+                    const long long n = (long long)rows * cols;
+                    hipLaunchKernelGGL(k_count_nonfinite, dim3((unsigned)std::min<long long>((n + kBlock - 1) / kBlock, 1024)),
+                                       dim3(kBlock), 0, s_, a, ld, rows, cols, info_.p + 2);
+                    AA_CHECK_LAUNCH();
+                };
+                cnt(F, f, f, f);
+                cnt(L, p, p, p);
+                if (nb > 0) cnt(Md, nb, nb, p);
+            }
+            AA_HIP(hipMemcpyAsync(out, info_.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s_));
+            AA_HIP(hipStreamSynchronize(s_));
+        };
+        if (check_ && poison_ > 0 && --poison_ == 0) {   // test hook: this front's first attempt starts from a NaN
+            AA_HIP(hipMemsetAsync(F, 0xff, sizeof(double), s_));
         }
-        int* hinfo = hint_.get(2);
-        AA_HIP(hipMemcpyAsync(hinfo, info_.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s_));
-        AA_HIP(hipStreamSynchronize(s_));
+        int* hinfo = hint_.get(3);
+        attempt(hinfo);
+        // Kept-copy check (default on; AA_FRONT_CHECK=0 off): the assembled front is kept (one
+        // device copy); if its Cholesky fails or any output entry is not finite, the copy is factored
+        // again and the outcome reported -- a second failure is the matrix's (thrown with the
+        // diagnostics), a success means the first attempt was at fault and the run goes on with the
+        // second. Added for intermittent not-positive-definite reports and non-finite factors seen
+        // only with several processes sharing one GPU; an SPD front never yields either.
+        if (check_ && (hinfo[0] != 0 || hinfo[2] != 0)) {
+            const int first = hinfo[0], bad = hinfo[2];
+            double* hf = hdbl_.get((size_t)f * f);
+            AA_HIP(hipMemcpyAsync(hf, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToHost, s_));
+            AA_HIP(hipStreamSynchronize(s_));
+            size_t nonfinite = 0;
+            double dmin = 1e300, dmax = 0;
+            for (size_t q = 0; q < (size_t)f * f; ++q) nonfinite += !std::isfinite(hf[q]);
+            for (int q = 0; q < f; ++q) { dmin = std::min(dmin, hf[(size_t)q * f + q]); dmax = std::max(dmax, hf[(size_t)q * f + q]); }
+            AA_HIP(hipMemcpyAsync(F, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToDevice, s_));
+            attempt(hinfo);
+            char msg[400];
+            std::snprintf(msg, sizeof msg, "[front-check] front %d order %d p %d: potrf info %d, %d non-finite outputs; kept copy: "
+                          "%zu non-finite, diag [%.3e, %.3e]; again on the copy: potrf info %d, %d non-finite outputs",
+                          s, f, p, first, bad, nonfinite, dmin, dmax, hinfo[0], hinfo[2]);
+            std::fprintf(stderr, "%s\n", msg);
+            if (hinfo[0] != 0) throw std::runtime_error(std::string("multifrontal_cholesky: matrix not positive definite ") + msg);
+            if (hinfo[2] != 0) throw std::runtime_error(std::string("multifrontal_cholesky: non-finite factor ") + msg);
+            // the copy factored: the first attempt was at fault, go on with this one
+        }
         const int info[2] = {hinfo[0], hinfo[1]};
         if (info[0] != 0)
             throw std::runtime_error("multifrontal_cholesky: matrix not positive definite (GPU front " + std::to_string(s) +
@@ -295,6 +328,9 @@ private:
     PinnedBuf<int> hint_;
     Grow<double> K_;           // AA_FRONT_CHECK: the assembled front, kept
     bool check_ = !(std::getenv("AA_FRONT_CHECK") && std::getenv("AA_FRONT_CHECK")[0] == '0');
+    // AA_FRONT_CHECK_POISON=k (tests): the k-th front this backend factors gets a NaN in its first
+    // attempt (after the copy is kept) -- the retry must give the unpoisoned run's bits
+    int poison_ = std::getenv("AA_FRONT_CHECK_POISON") ? std::atoi(std::getenv("AA_FRONT_CHECK_POISON")) : 0;
 };
 
 }  // namespace
@@ -317,7 +353,7 @@ double warm_gpu_front_backend(hipStream_t s) {
     const auto t0 = std::chrono::steady_clock::now();
     {   // a diagonally dominant front of the smallest GPU order with a boundary block: potrf, trsm,
         // syrk, trtri, trmm and the assembly / layout kernels, as every GPU front of a factor runs
-        RocFrontBackend b(s);
+        RocFrontBackend b(s, false);
         const int p = b.min_front, f = p + 64;
         std::vector<int> ai, aj;
         std::vector<double> av;

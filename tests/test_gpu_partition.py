@@ -164,6 +164,26 @@ def test_rccl_transport_one_rank_is_identity(graph, pkg, ctx, monkeypatch, capfd
     comm.close()
 
 
+def test_front_check_retry_is_bit_identical(pkg, ctx, monkeypatch, capfd):
+    """The GPU front backend's kept-copy retry (dense_gpu.hip): a front whose first
+    factorization yields a non-finite entry (here injected: AA_FRONT_CHECK_POISON=1 puts a NaN into
+    the first GPU front's first attempt) is factored again from the kept copy, reported on stderr,
+    and the run's results are the unpoisoned run's bits (rocBLAS atomics off: deterministic)."""
+    monkeypatch.setenv("AA_DENSE_MIN_FRONT", "64")
+    sc = CASES["drop_z"][0]()
+    want, s = pkg.capi.run_scene(ctx, sc)
+    s.close()
+    capfd.readouterr()
+    monkeypatch.setenv("AA_FRONT_CHECK_POISON", "1")
+    got, s = pkg.capi.run_scene(ctx, sc)
+    s.close()
+    err = capfd.readouterr().err
+    notes = [ln for ln in err.splitlines() if "[front-check]" in ln]
+    assert len(notes) == 1 and "again on the copy: potrf info 0, 0 non-finite outputs" in notes[0], notes
+    for a, b in zip(want, got):
+        assert np.array_equal(a["comb"], b["comb"]) and np.array_equal(a["x"], b["x"])
+
+
 @pytest.mark.parametrize("case,nranks,minfront", [("pq", 2, 0), ("pq", 4, 0), ("pq", 3, 0), ("pq", 3, 64), ("wire", 2, 0),
                                                   ("pq_noaa", 2, 0)])
 def test_partitioned_geometry_matches_single_gpu(case, nranks, minfront, tmp_path, pkg, ctx):
