@@ -237,15 +237,78 @@ public:
         if (check_ && poison_ > 0 && --poison_ == 0) {   // test hook: this front's first attempt starts from a NaN
             AA_HIP(hipMemsetAsync(F, 0xff, sizeof(double), s_));
         }
+        // Product check (check_): with a fixed pseudo-random r, the factored front must reproduce the
+        // kept copy -- Fk r = [L11 0; L21 I] [I 0; 0 S] [L11 0; L21 I]^T r (S the Schur complement) --
+        // and L11^-1 (L11 r1) = r1, M r1 = L21 (L11^-1 r1); O(f^2) matrix-vector products against the
+        // O(f^3) factorization. Returns the largest relative deviation (a transient that leaves wrong
+        // but finite numbers shows up as O(1); rounding as < 1e-10).
+        auto verify = [&]() -> double {
+            if (!check_) return 0.0;
+            double* v = V_.get(6 * (size_t)f);
+            double *r = v, *y = v + f, *t = v + 2 * (size_t)f, *y2 = v + 3 * (size_t)f, *a = v + 4 * (size_t)f, *b = v + 5 * (size_t)f;
+            double* hr = hdbl_.get(8 * (size_t)f);
+            unsigned long long z = 0x9e3779b97f4a7c15ull;
+            for (int i = 0; i < f; ++i) { z = z * 6364136223846793005ull + 1442695040888963407ull; hr[i] = (double)(z >> 11) * 0x1.0p-53 - 0.5; }
+            AA_HIP(hipMemcpyAsync(r, hr, (size_t)f * sizeof(double), hipMemcpyHostToDevice, s_));
+            const double zero = 0.0;
+            rb_check(rocblas_dsymv(h_, rocblas_fill_lower, f, &one, Fk, f, r, 1, &zero, y, 1), "rocblas_dsymv");
+            // t = L11^T r1 + L21^T r2
+            AA_HIP(hipMemcpyAsync(t, r, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s_));
+            rb_check(rocblas_dtrmv(h_, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit, p, F, f, t, 1), "rocblas_dtrmv");
+            if (nb > 0) rb_check(rocblas_dgemv(h_, rocblas_operation_transpose, nb, p, &one, F + p, f, r + p, 1, &one, t, 1), "rocblas_dgemv");
+            // y2 = [L11 t; L21 t + S r2]
+            AA_HIP(hipMemcpyAsync(y2, t, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s_));
+            rb_check(rocblas_dtrmv(h_, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit, p, F, f, y2, 1), "rocblas_dtrmv");
+            if (nb > 0) {
+                rb_check(rocblas_dsymv(h_, rocblas_fill_lower, nb, &one, F + (size_t)p * f + p, f, r + p, 1, &zero, y2 + p, 1), "rocblas_dsymv");
+                rb_check(rocblas_dgemv(h_, rocblas_operation_none, nb, p, &one, F + p, f, t, 1, &one, y2 + p, 1), "rocblas_dgemv");
+            }
+            // a = L11^-1 (L11 r1); b = L11^-1 r1, then M r1 vs L21 b (in t[.. nb], y2 reused below)
+            AA_HIP(hipMemcpyAsync(a, r, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s_));
+            rb_check(rocblas_dtrmv(h_, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit, p, F, f, a, 1), "rocblas_dtrmv");
+            rb_check(rocblas_dtrmv(h_, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit, p, L, p, a, 1), "rocblas_dtrmv");
+            AA_HIP(hipMemcpyAsync(b, r, (size_t)p * sizeof(double), hipMemcpyDeviceToDevice, s_));
+            rb_check(rocblas_dtrmv(h_, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit, p, L, p, b, 1), "rocblas_dtrmv");
+            double* hm = hr + f;   // host copies: y, y2, a; then the M check
+            AA_HIP(hipMemcpyAsync(hm, y, 2 * (size_t)f * sizeof(double), hipMemcpyDeviceToHost, s_));   // y (and t: unused)
+            AA_HIP(hipMemcpyAsync(hm + 2 * (size_t)f, y2, (size_t)f * sizeof(double), hipMemcpyDeviceToHost, s_));
+            AA_HIP(hipMemcpyAsync(hm + 3 * (size_t)f, a, (size_t)p * sizeof(double), hipMemcpyDeviceToHost, s_));
+            double dev = 0;
+            auto rel = [](const double* u, const double* w, int n) {
+                double d = 0, m = 0;
+                for (int i = 0; i < n; ++i) { d = std::max(d, std::fabs(u[i] - w[i])); m = std::max(m, std::fabs(u[i])); }
+                return m > 0 ? d / m : d;
+            };
+            if (nb > 0) {   // M r1 (into y) and L21 b (into y2 + p)
+                rb_check(rocblas_dgemv(h_, rocblas_operation_none, nb, p, &one, Md, nb, r, 1, &zero, y, 1), "rocblas_dgemv");
+                rb_check(rocblas_dgemv(h_, rocblas_operation_none, nb, p, &one, F + p, f, b, 1, &zero, t, 1), "rocblas_dgemv");
+            }
+            AA_HIP(hipStreamSynchronize(s_));
+            const double* hy = hm;
+            const double* hy2 = hm + 2 * (size_t)f;
+            const double* ha = hm + 3 * (size_t)f;
+            dev = std::max(dev, rel(hy, hy2, f));
+            dev = std::max(dev, rel(hr, ha, p));
+            if (nb > 0) {
+                double* hq = hm + 4 * (size_t)f;   // (hdbl_ holds 8 f >= 5 f + 2 nb)
+                AA_HIP(hipMemcpyAsync(hq, y, (size_t)nb * sizeof(double), hipMemcpyDeviceToHost, s_));
+                AA_HIP(hipMemcpyAsync(hq + nb, t, (size_t)nb * sizeof(double), hipMemcpyDeviceToHost, s_));
+                AA_HIP(hipStreamSynchronize(s_));
+                dev = std::max(dev, rel(hq + nb, hq, nb));
+            }
+            return std::isfinite(dev) ? dev : 1e300;
+        };
         int* hinfo = hint_.get(3);
         attempt(hinfo);
+        double dev1 = (hinfo[0] == 0 && hinfo[2] == 0) ? verify() : 0.0;
+        if (dev1 < 1e300) max_dev = std::max(max_dev, dev1);
         // Kept-copy check (default on; AA_FRONT_CHECK=0 off): the assembled front is kept (one
         // device copy); if its Cholesky fails or any output entry is not finite, the copy is factored
         // again and the outcome reported -- a second failure is the matrix's (thrown with the
         // diagnostics), a success means the first attempt was at fault and the run goes on with the
         // second. Added for intermittent not-positive-definite reports and non-finite factors seen
         // only with several processes sharing one GPU; an SPD front never yields either.
-        if (check_ && (hinfo[0] != 0 || hinfo[2] != 0)) {
+        if (check_ && (hinfo[0] != 0 || hinfo[2] != 0 || dev1 > kVerifyTol)) {
             const int first = hinfo[0], bad = hinfo[2];
             double* hf = hdbl_.get((size_t)f * f);
             AA_HIP(hipMemcpyAsync(hf, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToHost, s_));
@@ -256,10 +319,12 @@ public:
             for (int q = 0; q < f; ++q) { dmin = std::min(dmin, hf[(size_t)q * f + q]); dmax = std::max(dmax, hf[(size_t)q * f + q]); }
             AA_HIP(hipMemcpyAsync(F, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToDevice, s_));
             attempt(hinfo);
-            char msg[400];
-            std::snprintf(msg, sizeof msg, "[front-check] front %d order %d p %d: potrf info %d, %d non-finite outputs; kept copy: "
-                          "%zu non-finite, diag [%.3e, %.3e]; again on the copy: potrf info %d, %d non-finite outputs",
-                          s, f, p, first, bad, nonfinite, dmin, dmax, hinfo[0], hinfo[2]);
+            const double dev2 = (hinfo[0] == 0 && hinfo[2] == 0) ? verify() : 0.0;
+            char msg[480];
+            std::snprintf(msg, sizeof msg, "[front-check] front %d order %d p %d: potrf info %d, %d non-finite outputs, "
+                          "product deviation %.2e; kept copy: %zu non-finite, diag [%.3e, %.3e]; again on the copy: potrf "
+                          "info %d, %d non-finite outputs, product deviation %.2e",
+                          s, f, p, first, bad, dev1, nonfinite, dmin, dmax, hinfo[0], hinfo[2], dev2);
             std::fprintf(stderr, "%s\n", msg);
             if (hinfo[0] != 0) throw std::runtime_error(std::string("multifrontal_cholesky: matrix not positive definite ") + msg);
             if (hinfo[2] != 0) throw std::runtime_error(std::string("multifrontal_cholesky: non-finite factor ") + msg);
@@ -303,6 +368,7 @@ public:
 
     double busy_ms = 0;
     int fronts = 0;
+    double max_dev = 0;   // largest first-attempt product deviation (AA_SETUP_TIMES)
 
 private:
     hipStream_t s_;
@@ -327,6 +393,11 @@ private:
     PinnedBuf<double> hdbl_;   // host staging (pinned) for the copies above
     PinnedBuf<int> hint_;
     Grow<double> K_;           // AA_FRONT_CHECK: the assembled front, kept
+    Grow<double> V_;           // AA_FRONT_CHECK: the product check's vectors
+    // a deviation above this is a wrong factorization, not rounding (the check's products of an
+    // SPD front deviate by ~1e-15 .. 1e-12 relative); a second deviation is reported, not thrown:
+    // the run goes on with the retried factor
+    static constexpr double kVerifyTol = 1e-8;
     bool check_ = !(std::getenv("AA_FRONT_CHECK") && std::getenv("AA_FRONT_CHECK")[0] == '0');
     // AA_FRONT_CHECK_POISON=k (tests): the k-th front this backend factors gets a NaN in its first
     // attempt (after the copy is kept) -- the retry must give the unpoisoned run's bits
@@ -385,9 +456,10 @@ SupernodalFactor factor_on_device(const CsrMatrix& A, const NdTree& tree, hipStr
     SupernodalFactor F = multifrontal_cholesky(A, tree, b.get(), part);
     if (const char* t = std::getenv("AA_SETUP_TIMES"); t && t[0] == '1') {
         const auto* rb = static_cast<const RocFrontBackend*>(b.get());
-        std::fprintf(stderr, "[setup]   factor %.1f ms: %d fronts on the GPU (%.1f ms inside the backend), %.1f GFLOP\n",
+        std::fprintf(stderr, "[setup]   factor %.1f ms: %d fronts on the GPU (%.1f ms inside the backend, product check "
+                     "deviation <= %.1e), %.1f GFLOP\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), rb->fronts,
-                     rb->busy_ms, F.flops * 1e-9);
+                     rb->busy_ms, rb->max_dev, F.flops * 1e-9);
     }
     return F;
 }
