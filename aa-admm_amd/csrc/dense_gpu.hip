@@ -91,6 +91,11 @@ __global__ void k_count_nonfinite(const double* __restrict__ a, int ld, int rows
     }
 }
 
+__global__ void k_copy_front(double* __restrict__ dst, const double* __restrict__ src, long long n) {
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
+        dst[k] = src[k];
+}
+
 template <class T>
 struct Grow {   // device buffer that only grows
     DevBuf<T> b;
@@ -234,6 +239,17 @@ public:
             AA_HIP(hipMemcpyAsync(out, info_.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s_));
             AA_HIP(hipStreamSynchronize(s_));
         };
+        if (check_ && reduce_front) {
+            // a partitioned top front: its sum arrived by a host->device copy. Both root-front
+            // transients seen (§5: the last pivot of the shared root failing, the kept copy -- taken
+            // from the same memory by a copy -- factoring cleanly) fit the factorization's kernels
+            // reading lines that predate that copy; the front is rewritten from the kept copy by a
+            // kernel on this stream, so the factorization reads what a kernel wrote
+            const long long n = (long long)f * f;
+            hipLaunchKernelGGL(k_copy_front, dim3((unsigned)std::min<long long>((n + kBlock - 1) / kBlock, 2048)), dim3(kBlock),
+                               0, s_, F, Fk, n);
+            AA_CHECK_LAUNCH();
+        }
         if (check_ && poison_ > 0 && --poison_ == 0) {   // test hook: this front's first attempt starts from a NaN
             AA_HIP(hipMemsetAsync(F, 0xff, sizeof(double), s_));
         }
