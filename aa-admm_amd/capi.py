@@ -29,7 +29,7 @@ EXPORTS = [
     "aa_elastic_get_times", "aa_elastic_set_iterations", "aa_elastic_set_x",
     "aa_elastic_runtime", "aa_elastic_bench_iterations", "aa_elastic_kernel_stats", "aa_elastic_local_stats",
     "aa_elastic_setup_phases",
-    "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_create_solo", "aa_comm_destroy", "aa_comm_info",
+    "aa_runtime_libraries", "aa_comm_unique_id", "aa_comm_create_rccl", "aa_comm_create_host", "aa_comm_create_solo", "aa_comm_destroy", "aa_comm_info",
     "aa_comm_allreduce_host", "aa_elastic_set_comm", "aa_geom_set_comm",
     "aa_geom_create", "aa_geom_create_kind", "aa_geom_destroy", "aa_geom_add_ref_surface", "aa_geom_add_constraints", "aa_geom_add_laplacian",
     "aa_geom_add_closeness", "aa_geom_add_laplacians", "aa_geom_add_closenesses", "aa_geom_setup", "aa_geom_solve", "aa_geom_set_stop", "aa_geom_get_solution", "aa_geom_get_history",
@@ -86,6 +86,62 @@ def lib() -> C.CDLL:
         L.aa_version.restype = C.c_char_p
         _LIB = L
     return _LIB
+
+
+RUNTIME_LIBS = ("amdhip64", "hsa-runtime64", "rocblas", "rocsolver", "rccl")
+
+
+def runtime_libraries() -> dict:
+    """{name: path} of the HIP / HSA / rocBLAS / rocSOLVER / RCCL objects this process has bound
+    (aa_runtime_libraries, dladdr; loads librccl, needs no GPU)."""
+    n = C.c_longlong()
+    buf = C.create_string_buffer(4096)
+    _chk(lib().aa_runtime_libraries(buf, C.c_longlong(len(buf)), C.byref(n)))
+    out = {}
+    for ln in buf.value.decode().splitlines():
+        k, _, v = ln.partition("=")
+        out[k] = v
+    return out
+
+
+def expected_runtime_dir() -> str:
+    """The ROCm lib directory `ldd libaa_admm.so` resolves libamdhip64 to (the build's RUNPATH)."""
+    import subprocess
+    r = subprocess.run(["ldd", LIB_PATH], capture_output=True, text=True, check=True)
+    for ln in r.stdout.splitlines():
+        if "libamdhip64" in ln and "=>" in ln:
+            return os.path.dirname(os.path.realpath(ln.split("=>")[1].split("(")[0].strip()))
+    raise RuntimeError(f"ldd {LIB_PATH}: libamdhip64 not found")
+
+
+def mapped_runtime_objects() -> dict:
+    """{name: sorted real paths} of every mapped copy of the RUNTIME_LIBS (/proc/self/maps)."""
+    out = {k: set() for k in RUNTIME_LIBS}
+    with open("/proc/self/maps") as f:
+        for ln in f:
+            parts = ln.split()
+            if len(parts) < 6 or not parts[5].startswith("/"):
+                continue
+            base = os.path.basename(parts[5])
+            for k in RUNTIME_LIBS:
+                if base.startswith("lib" + k + ".so"):
+                    out[k].add(os.path.realpath(parts[5]))
+    return {k: sorted(v) for k, v in out.items()}
+
+
+def check_runtime() -> dict:
+    """Fail unless every runtime object bound by this process (and every mapped copy of one) lives in
+    the ROCm directory the library was linked against -- e.g. not a framework's bundled ROCm loaded
+    before libaa_admm.so. Returns {"expected": dir, "bound": {...}, "mapped": {...}}."""
+    want = expected_runtime_dir()
+    bound = {k: os.path.realpath(v) if v else "" for k, v in runtime_libraries().items()}
+    mapped = mapped_runtime_objects()
+    bad = [f"{k} bound to {v or '(not loaded)'}" for k, v in bound.items() if os.path.dirname(v) != want]
+    bad += [f"{k} mapped from {p}" for k, ps in mapped.items() for p in ps if os.path.dirname(p) != want]
+    if bad:
+        raise RuntimeError(f"libaa_admm.so was built against {want}, but this process uses: " + "; ".join(bad)
+                           + " (load the library before any framework that bundles its own ROCm runtime)")
+    return {"expected": want, "bound": bound, "mapped": mapped}
 
 
 class AAError(RuntimeError):

@@ -1,5 +1,6 @@
 // extern "C" boundary (include/aa_admm.h). Every entry point catches and maps exceptions to
 // status codes; the message is kept per thread for aa_last_error().
+#include <algorithm>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -244,6 +245,18 @@ int aa_elastic_get_times(aa_elastic h, double* time_ms, int cap, int* n) {
 
 int aa_elastic_runtime(aa_elastic h, aa_runtime* out) {
     return guarded([&] { NEED(h && out, "null argument"); *out = h->s->runtime(); });
+}
+
+int aa_runtime_libraries(char* buf, long long cap, long long* len) {
+    return guarded([&] {
+        std::string s = aa::runtime_libraries();
+        if (len) *len = (long long)s.size();
+        if (buf && cap > 0) {
+            size_t k = std::min((size_t)(cap - 1), s.size());
+            std::memcpy(buf, s.data(), k);
+            buf[k] = 0;
+        }
+    });
 }
 
 int aa_comm_unique_id(unsigned char id[128]) {

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <utility>
 
 #include "common.hpp"
 
@@ -24,15 +25,36 @@ struct Rccl {
     decltype(&ncclGetErrorString) error_string = nullptr;
 };
 
+// Directory of the shared object that defines `addr` ("" if unknown).
+std::string object_dir(const void* addr) {
+    Dl_info info;
+    if (!addr || !dladdr(addr, &info) || !info.dli_fname) return "";
+    std::string f = info.dli_fname;
+    size_t k = f.rfind('/');
+    return k == std::string::npos ? std::string() : f.substr(0, k);
+}
+
+std::string object_path(const void* addr) {
+    Dl_info info;
+    if (!addr || !dladdr(addr, &info) || !info.dli_fname) return "";
+    return info.dli_fname;
+}
+
+std::string hip_runtime_dir() { return object_dir(reinterpret_cast<const void*>(&hipGetDeviceCount)); }
+
 const Rccl& rccl() {
     static Rccl r;
     static std::once_flag once;
     static std::string err;
     std::call_once(once, [] {
+        // RCCL from the directory of the HIP runtime this library is bound to, so a process never
+        // pairs one ROCm release's HIP with another's RCCL; the loader's search only as a fallback
         void* h = nullptr;
-        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-            h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+        std::string dir = hip_runtime_dir();
+        if (!dir.empty()) h = dlopen((dir + "/librccl.so.1").c_str(), RTLD_NOW | RTLD_GLOBAL);
+        for (const char* name : {"librccl.so.1", "librccl.so"}) {
             if (h) break;
+            h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
         }
         if (!h) { err = std::string("cannot load librccl: ") + dlerror(); return; }
         r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
@@ -166,6 +188,17 @@ public:
 };
 
 }  // namespace
+
+std::string runtime_libraries() {
+    try { (void)rccl(); } catch (const Error&) {}   // loads librccl (no device call); absent = empty path
+    auto sym = [](const char* name) -> const void* { return dlsym(RTLD_DEFAULT, name); };
+    const std::pair<const char*, const char*> probes[] = {
+        {"amdhip64", "hipMalloc"}, {"hsa-runtime64", "hsa_init"}, {"rocblas", "rocblas_create_handle"},
+        {"rocsolver", "rocsolver_dpotrf"}, {"rccl", "ncclAllReduce"}};
+    std::string out;
+    for (const auto& p : probes) out += std::string(p.first) + "=" + object_path(sym(p.second)) + "\n";
+    return out;
+}
 
 std::unique_ptr<Comm> make_solo_comm(int rank, int size) { return std::unique_ptr<Comm>(new SoloComm(rank, size)); }
 

@@ -18,6 +18,7 @@
 
 #include <cstddef>
 #include <memory>
+#include <string>
 #include <vector>
 
 namespace aa {
@@ -41,6 +42,8 @@ protected:
 };
 
 void rccl_unique_id(unsigned char out[128]);
+// "name=path\n" of the HIP, HSA, rocBLAS, rocSOLVER and RCCL objects this process has bound (dladdr)
+std::string runtime_libraries();
 std::unique_ptr<Comm> make_rccl_comm(const unsigned char id[128], int rank, int size);
 std::unique_ptr<Comm> make_host_comm(HostAllreduceFn fn, void* user, int rank, int size);
 std::unique_ptr<Comm> make_solo_comm(int rank, int size);   // timing rehearsal of one rank (comm.cpp)

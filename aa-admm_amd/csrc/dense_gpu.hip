@@ -91,11 +91,6 @@ __global__ void k_count_nonfinite(const double* __restrict__ a, int ld, int rows
     }
 }
 
-__global__ void k_copy_front(double* __restrict__ dst, const double* __restrict__ src, long long n) {
-    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
-        dst[k] = src[k];
-}
-
 template <class T>
 struct Grow {   // device buffer that only grows
     DevBuf<T> b;
@@ -135,13 +130,9 @@ public:
         std::lock_guard<std::mutex> g(mu_);
         AA_HIP(hipSetDevice(dev_));
         // one rocBLAS handle per calling thread (rocBLAS handles are per-thread objects; the
-        // OpenMP workers of the tree-parallel factorization take turns here), and nothing of a
-        // previous call still in flight on the device when this one starts or ends: with several
-        // processes sharing the GPU the partition tests found fronts factored from stale data
-        //  -- these are the two assumptions the backend no longer relies on
+        // OpenMP workers of the tree-parallel factorization take turns here); everything below is
+        // ordered on s_
         rocblas_handle h_ = handle();
-        AA_HIP(hipDeviceSynchronize());
-        struct DevSync { ~DevSync() { (void)hipDeviceSynchronize(); } } dev_sync;
         const auto t0 = std::chrono::steady_clock::now();
         struct Tally {   // time inside the backend (AA_SETUP_TIMES)
             RocFrontBackend* b;
@@ -239,17 +230,6 @@ public:
             AA_HIP(hipMemcpyAsync(out, info_.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s_));
             AA_HIP(hipStreamSynchronize(s_));
         };
-        if (check_ && reduce_front) {
-            // a partitioned top front: its sum arrived by a host->device copy. Both root-front
-            // transients seen (§5: the last pivot of the shared root failing, the kept copy -- taken
-            // from the same memory by a copy -- factoring cleanly) fit the factorization's kernels
-            // reading lines that predate that copy; the front is rewritten from the kept copy by a
-            // kernel on this stream, so the factorization reads what a kernel wrote
-            const long long n = (long long)f * f;
-            hipLaunchKernelGGL(k_copy_front, dim3((unsigned)std::min<long long>((n + kBlock - 1) / kBlock, 2048)), dim3(kBlock),
-                               0, s_, F, Fk, n);
-            AA_CHECK_LAUNCH();
-        }
         if (check_ && poison_ > 0 && --poison_ == 0) {   // test hook: this front's first attempt starts from a NaN
             AA_HIP(hipMemsetAsync(F, 0xff, sizeof(double), s_));
         }
@@ -318,14 +298,17 @@ public:
         attempt(hinfo);
         double dev1 = (hinfo[0] == 0 && hinfo[2] == 0) ? verify() : 0.0;
         if (dev1 < 1e300) max_dev = std::max(max_dev, dev1);
-        // Kept-copy check (default on; AA_FRONT_CHECK=0 off): the assembled front is kept (one
-        // device copy); if its Cholesky fails or any output entry is not finite, the copy is factored
-        // again and the outcome reported -- a second failure is the matrix's (thrown with the
-        // diagnostics), a success means the first attempt was at fault and the run goes on with the
-        // second. Added for intermittent not-positive-definite reports and non-finite factors seen
-        // only with several processes sharing one GPU; an SPD front never yields either.
+        // Front check (default on; AA_FRONT_CHECK=0 off): the assembled front is kept (one device
+        // copy) and every output is checked -- potrf info, non-finite entries, the product check.
+        // An SPD front fails none of them, so a failure is an ERROR: the kept copy's diagnostics
+        // (and, with AA_FRONT_DUMP=<dir>, the kept copy and the first attempt's outputs, for a replay)
+        // and, if the kept copy factors cleanly, the statement that the first attempt was at fault.
+        // AA_FRONT_RETRY=1 (opt-in, and the poison test) goes on with the second factorization
+        // instead, reported on stderr. History: the wrong factorizations of round 5 came
+        // from rank processes bound to another ROCm build's HIP / rocBLAS / rocSOLVER.
         if (check_ && (hinfo[0] != 0 || hinfo[2] != 0 || dev1 > kVerifyTol)) {
             const int first = hinfo[0], bad = hinfo[2];
+            if (const char* d = std::getenv("AA_FRONT_DUMP")) dump(d, s, f, p, nb, Fk, F, L, Md);
             double* hf = hdbl_.get((size_t)f * f);
             AA_HIP(hipMemcpyAsync(hf, Fk, (size_t)f * f * sizeof(double), hipMemcpyDeviceToHost, s_));
             AA_HIP(hipStreamSynchronize(s_));
@@ -342,9 +325,13 @@ public:
                           "info %d, %d non-finite outputs, product deviation %.2e",
                           s, f, p, first, bad, dev1, nonfinite, dmin, dmax, hinfo[0], hinfo[2], dev2);
             std::fprintf(stderr, "%s\n", msg);
-            if (hinfo[0] != 0) throw std::runtime_error(std::string("multifrontal_cholesky: matrix not positive definite ") + msg);
-            if (hinfo[2] != 0) throw std::runtime_error(std::string("multifrontal_cholesky: non-finite factor ") + msg);
-            // the copy factored: the first attempt was at fault, go on with this one
+            ++retries;
+            if (hinfo[0] != 0) throw Error(ERR_NUMERIC, std::string("multifrontal_cholesky: matrix not positive definite ") + msg);
+            if (hinfo[2] != 0) throw Error(ERR_NUMERIC, std::string("multifrontal_cholesky: non-finite factor ") + msg);
+            if (dev2 > kVerifyTol) throw Error(ERR_NUMERIC, std::string("multifrontal_cholesky: factor fails the product check ") + msg);
+            if (!retry_)
+                throw Error(ERR_NUMERIC, std::string("multifrontal_cholesky: GPU front factored wrongly on the first attempt "
+                                                     "(the kept copy factors cleanly; AA_FRONT_RETRY=1 continues with it) ") + msg);
         }
         const int info[2] = {hinfo[0], hinfo[1]};
         if (info[0] != 0)
@@ -384,9 +371,31 @@ public:
 
     double busy_ms = 0;
     int fronts = 0;
+    int retries = 0;      // fronts whose first attempt failed a check (an error unless AA_FRONT_RETRY=1)
     double max_dev = 0;   // largest first-attempt product deviation (AA_SETUP_TIMES)
 
 private:
+    // AA_FRONT_DUMP: the kept front and the first attempt's outputs of front s, column-major
+    // doubles, for a replay in one process (tools/front_replay.py)
+    void dump(const char* dir, int s, int f, int p, int nb, const double* Fk, const double* F, const double* L,
+              const double* Md) {
+        auto put = [&](const char* what, const double* src, size_t n) {
+            std::vector<double> h(n);
+            AA_HIP(hipMemcpyAsync(h.data(), src, n * sizeof(double), hipMemcpyDeviceToHost, s_));
+            AA_HIP(hipStreamSynchronize(s_));
+            const std::string path = std::string(dir) + "/front" + std::to_string(s) + "_f" + std::to_string(f) + "_p" +
+                                     std::to_string(p) + "_" + what + ".bin";
+            if (FILE* fo = std::fopen(path.c_str(), "wb")) {
+                std::fwrite(h.data(), sizeof(double), n, fo);
+                std::fclose(fo);
+            }
+        };
+        put("kept", Fk, (size_t)f * f);
+        put("first_F", F, (size_t)f * f);
+        put("first_Linv", L, (size_t)p * p);
+        if (nb > 0) put("first_M", Md, (size_t)nb * p);
+    }
+
     hipStream_t s_;
     int dev_ = 0;
     std::map<std::thread::id, rocblas_handle> handles_;
@@ -411,9 +420,9 @@ private:
     Grow<double> K_;           // AA_FRONT_CHECK: the assembled front, kept
     Grow<double> V_;           // AA_FRONT_CHECK: the product check's vectors
     // a deviation above this is a wrong factorization, not rounding (the check's products of an
-    // SPD front deviate by ~1e-15 .. 1e-12 relative); a second deviation is reported, not thrown:
-    // the run goes on with the retried factor
+    // SPD front deviate by ~1e-15 .. 1e-12 relative)
     static constexpr double kVerifyTol = 1e-8;
+    bool retry_ = std::getenv("AA_FRONT_RETRY") && std::getenv("AA_FRONT_RETRY")[0] == '1';
     bool check_ = !(std::getenv("AA_FRONT_CHECK") && std::getenv("AA_FRONT_CHECK")[0] == '0');
     // AA_FRONT_CHECK_POISON=k (tests): the k-th front this backend factors gets a NaN in its first
     // attempt (after the copy is kept) -- the retry must give the unpoisoned run's bits
@@ -473,9 +482,9 @@ SupernodalFactor factor_on_device(const CsrMatrix& A, const NdTree& tree, hipStr
     if (const char* t = std::getenv("AA_SETUP_TIMES"); t && t[0] == '1') {
         const auto* rb = static_cast<const RocFrontBackend*>(b.get());
         std::fprintf(stderr, "[setup]   factor %.1f ms: %d fronts on the GPU (%.1f ms inside the backend, product check "
-                     "deviation <= %.1e), %.1f GFLOP\n",
+                     "deviation <= %.1e, %d retried), %.1f GFLOP\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), rb->fronts,
-                     rb->busy_ms, rb->max_dev, F.flops * 1e-9);
+                     rb->busy_ms, rb->max_dev, rb->retries, F.flops * 1e-9);
     }
     return F;
 }

@@ -10,7 +10,8 @@ triangles, (u,x)-Anderson m=6 (configs[1]); c3 / c5: the Geometry ALM configs.
 A bench "step" is one Solver::step() time step; `value` = ADMM iterations executed / max-over-
 ranks wall time. Synthetic input (generated mesh, no datasets).
 
-Multi-GPU: one process per GPU (torchrun). Elastic configs partition ONE mesh over the ranks
+Multi-GPU: one process per GPU (torch.distributed.run as the launcher only: the ranks never import
+torch, see aa-admm_amd/rdzv.py). Elastic configs partition ONE mesh over the ranks
 (--partition rccl, the default for N>1: nested-dissection parts, separator rows of the global
 solve and all residual/Anderson partials all-reduced on RCCL over xGMI; strong scaling);
 --partition none runs independent replicas (weak scaling).
@@ -107,32 +108,28 @@ def launch_ranks(n):
 
 
 def dist_setup(n_gpus):
+    """(world, rank, local rank, group, runtime report). A rank process never imports torch
+    (torch.distributed.run is only the launcher): libaa_admm.so is loaded and checked against the
+    ROCm runtime it was built for BEFORE the rendezvous (aa-admm_amd/dist.py rank_setup), which is
+    a torch-free socket group (aa-admm_amd/rdzv.py) -- RCCL id broadcast, barriers, timing max."""
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != n_gpus:
         raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} "
                          "(the launcher and the flag must agree)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # plumbing only: host barrier + max-reduce of timings
-        dist.init_process_group("gloo")
-    return world, rank, local, dist
+    pkg = importlib.import_module("aa-admm_amd")
+    group, report = pkg.dist.rank_setup()
+    return world, rank, local, group, report
 
 
-def allreduce(dist, val, op):
-    if dist is None:
-        return val
-    import torch
-    t = torch.tensor([val], dtype=torch.float64)
-    dist.all_reduce(t, op=op)
-    return float(t.item())
+def allreduce(group, val, op):
+    return group.allreduce_scalar(val, op)
 
 
-def barrier(dist, ctx):
+def barrier(group, ctx):
     ctx.synchronize()
-    if dist is not None:
-        dist.barrier()
+    group.barrier()
     ctx.synchronize()
 
 
@@ -215,7 +212,7 @@ def cpu_baseline(sc):
                       f"{wall:.1f} s"}
 
 
-def make_comm(pkg, ctx, args, world, rank):
+def make_comm(pkg, ctx, args, world, rank, group):
     """Communicator of a mesh-partitioned run (None for replicas)."""
     part = args.partition if args.partition != "auto" else ("rccl" if world > 1 else "none")
     comm = None
@@ -224,13 +221,13 @@ def make_comm(pkg, ctx, args, world, rank):
                 f"solo rehearsal: rank {args.rehearse_rank} of {args.rehearse}, collectives replaced")
     if part == "rccl":
         try:
-            comm = pkg.dist.rccl_comm(ctx, rank, world)
+            comm = pkg.dist.rccl_comm(ctx, group)
         except Exception as e:   # transport only: the compute stays on the GPUs either way
             print(f"[bench] RCCL communicator failed ({e}); using the host-staged transport", file=sys.stderr)
             part = "host (rccl init failed)"
-            comm = pkg.dist.host_comm(rank, world)
+            comm = pkg.dist.host_comm(group)
     elif part == "host":
-        comm = pkg.dist.host_comm(rank, world)
+        comm = pkg.dist.host_comm(group)
     return comm, part
 
 
@@ -273,7 +270,7 @@ def geom_cpu_baseline(args):
 MALL_BYTES = 256e6   # MI355X Infinity Cache: working sets below it are flagged cache-resident
 
 
-def geom_line(args, world, rank, local, dist):
+def geom_line(args, world, rank, local, group):
     """configs[2] / configs[4]: one bench step = one solve_ADMM of `iters` accepted ALM iterations
     (inputs resident on the device after setup); value = accepted iterations / wall time.
     Returns the JSON line (rank 0) or None."""
@@ -281,7 +278,7 @@ def geom_line(args, world, rank, local, dist):
     capi = pkg.capi
     ctx = capi.Context(0 if args.same_device else local)
     sc, desc = geom_scene(args)
-    comm, part = make_comm(pkg, ctx, args, world, rank)
+    comm, part = make_comm(pkg, ctx, args, world, rank, group)
     lib_first_use_ms = ctx.warm_dense()   # one-time rocBLAS / rocSOLVER load, outside setup_ms
     t0 = time.time()
     bind_phases = {}
@@ -307,7 +304,7 @@ def geom_line(args, world, rank, local, dist):
                        "warmup_solves_ms": round(warm_ms, 1), "warmup_solves": max(1, args.warmup) - 1,
                        "library_first_use_ms": round(lib_first_use_ms, 1)}
     print(f"[bench] {args.config} setup {setup_ms / 1e3:.2f} s ({setup_breakdown})", file=sys.stderr, flush=True)
-    barrier(dist, ctx)
+    barrier(group, ctx)
     t0 = time.perf_counter()
     acc, xupd, tte, tte_rel = 0, 0, [], []
     for _ in range(args.steps):
@@ -323,11 +320,11 @@ def geom_line(args, world, rank, local, dist):
             hr = np.nonzero(h["comb"] <= r * h["comb"][0])[0] if len(h["comb"]) else []
             rel[str(r)] = {"iters": int(hr[0]) + 1, "ms": round(float(h["time_s"][hr[0]] * 1e3), 3)} if len(hr) else None
         tte_rel.append(rel)
-    barrier(dist, ctx)
+    barrier(group, ctx)
     elapsed = time.perf_counter() - t0
-    elapsed_max = allreduce(dist, elapsed, _max_op(dist))
+    elapsed_max = allreduce(group, elapsed, "max")
     # replicas: independent copies (weak scaling); partitioned: one problem (strong scaling)
-    acc_all = float(acc) if comm is not None else allreduce(dist, float(acc), _sum_op(dist))
+    acc_all = float(acc) if comm is not None else allreduce(group, float(acc), "sum")
     geps = geom_run_to_eps(g, sc, eps, args) if args.geom_eps_solves > 0 else None
     value = acc_all / elapsed_max
     roof, cpu, line = None, None, None
@@ -454,12 +451,12 @@ def geom_run_to_eps(g, sc, eps, args):
     return out
 
 
-def main_geom(args, world, rank, local, dist):
-    line = geom_line(args, world, rank, local, dist)
+def main_geom(args, world, rank, local, group, report):
+    line = geom_line(args, world, rank, local, group)
     if line is not None:
+        line["runtime_libs"] = report["bound"]
         print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
+    group.close()
 
 
 def elastic_scene(args, iters=None, n_steps=1):
@@ -607,28 +604,33 @@ def main():
         sys.exit(launch_ranks(args.gpus))
     if args.rehearse > 1:   # a timing rehearsal is not a bench line: no baselines, no eps leg
         args.no_cpu_baseline, args.no_secondary, args.eps_steps, args.geom_eps_solves = True, True, 0, 0
-    world, rank, local, dist = dist_setup(args.gpus)
+    world, rank, local, group, report = dist_setup(args.gpus)
     if args.launch_check:
+        # every rank's bound runtime objects and mapped copies, after the RCCL load (ncclGetUniqueId
+        # itself needs a GPU: without one only the library load is exercised)
+        pkg = importlib.import_module("aa-admm_amd")
+        try:
+            pkg.capi.Comm.unique_id()
+        except pkg.capi.AAError:
+            pass
+        report = pkg.capi.check_runtime()
         part = args.partition if args.partition != "auto" else ("rccl" if world > 1 else "none")
-        all_ranks = [None] * world
-        if dist is not None:
-            dist.all_gather_object(all_ranks, {"rank": rank, "local_rank": local})
-        else:
-            all_ranks = [{"rank": 0, "local_rank": 0}]
+        all_ranks = group.all_gather_json({"rank": rank, "local_rank": local, "torch_imported": "torch" in sys.modules,
+                                           "runtime_bound": report["bound"], "runtime_mapped": report["mapped"]})
         if rank == 0:
             print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": all_ranks,
+                              "runtime_expected": report["expected"],
                               "parallelism": f"mesh-partitioned{world} ({part})" if part != "none" else f"replicas{world}"}))
-        if dist is not None:
-            dist.destroy_process_group()
+        group.close()
         return
     if args.config in ("c3", "c5"):
-        return main_geom(args, world, rank, local, dist)
+        return main_geom(args, world, rank, local, group, report)
     pkg = importlib.import_module("aa-admm_amd")
     capi = pkg.capi
 
     ctx = capi.Context(0 if args.same_device else local)
     sc, desc = elastic_scene(args)
-    comm, part = make_comm(pkg, ctx, args, world, rank)
+    comm, part = make_comm(pkg, ctx, args, world, rank, group)
     solver = capi.solver_from_scene(ctx, sc, comm)
     if args.lq_stats:
         os.environ["AA_LQ_STATS"] = "1"
@@ -651,7 +653,7 @@ def main():
     if args.lq_stats:
         solver.local_stats(reset=True)
 
-    barrier(dist, ctx)
+    barrier(group, ctx)
     t0 = time.perf_counter()
     iters_run, tte, rejects = 0, [], 0
     for _ in range(args.steps):
@@ -661,12 +663,12 @@ def main():
         h = solver.history()
         rejects += int(np.sum(h["reject"]))
         tte.append(eps_stats(h["comb"], solver.times(), EPS_ELASTIC))
-    barrier(dist, ctx)
+    barrier(group, ctx)
     elapsed = time.perf_counter() - t0
-    elapsed_max = allreduce(dist, elapsed, _max_op(dist))
+    elapsed_max = allreduce(group, elapsed, "max")
     # replicas: every rank ran its own copy of the scene (weak scaling); partitioned: all ranks
     # ran ONE scene together (strong scaling), its iterations count once
-    iters_all = float(iters_run) if comm is not None else allreduce(dist, float(iters_run), _sum_op(dist))
+    iters_all = float(iters_run) if comm is not None else allreduce(group, float(iters_run), "sum")
     value = iters_all / elapsed_max
 
     lq = None
@@ -740,7 +742,7 @@ def main():
         a3 = argparse.Namespace(**{**vars(args), "config": "c3", "iters": 100, "nx": 112,
                                    "partition": "none" if world > 1 else args.partition})
         try:
-            secondary = geom_line(a3, world, rank, local, dist)
+            secondary = geom_line(a3, world, rank, local, group)
         except Exception as e:   # report, never lose the primary line
             secondary = {"config": "c3", "error": str(e)[:300]}
 
@@ -796,17 +798,9 @@ def main():
             line["local_step_queue"] = lq
         if secondary is not None:
             line["secondary"] = secondary
+        line["runtime_libs"] = report["bound"]
         print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
-
-
-def _max_op(dist):
-    return None if dist is None else dist.ReduceOp.MAX
-
-
-def _sum_op(dist):
-    return None if dist is None else dist.ReduceOp.SUM
+    group.close()
 
 
 if __name__ == "__main__":

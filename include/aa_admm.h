@@ -159,6 +159,12 @@ int aa_elastic_runtime(aa_elastic h, aa_runtime* out);                   /* runt
 typedef struct aa_comm_s* aa_comm;
 /* Host transport callback: in-place SUM of n doubles over all ranks; return 0 on success. */
 typedef int (*aa_host_allreduce_fn)(double* buf, long long n, void* user);
+/* Which ROCm runtime this process is bound to (no reference counterpart): "name=path\n" for the
+ * objects defining hipMalloc, hsa_init, rocblas_create_handle, rocsolver_dpotrf and ncclAllReduce
+ * (librccl is loaded from the HIP runtime's directory first). Needs no GPU. A process that loaded
+ * another ROCm build's libamdhip64 before this library (e.g. a framework's bundled runtime) shows
+ * it here; the multi-rank launchers check it. Copies at most cap-1 bytes; *len = full length. */
+int aa_runtime_libraries(char* buf, long long cap, long long* len);
 /* ncclGetUniqueId: called on rank 0, the 128 bytes are broadcast by the caller. */
 int aa_comm_unique_id(unsigned char id[128]);
 /* RCCL communicator over xGMI on ctx's GPU (ncclCommInitRank; collective over all ranks). */

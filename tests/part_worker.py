@@ -5,11 +5,11 @@ runs the time steps; rank r writes its per-step history and final state to OUT/r
     AA_CASE=<name> AA_TRANSPORT=host|rccl AA_OUT=<dir> python -m torch.distributed.run ... part_worker.py
 """
 import importlib
+import json
 import os
 import sys
 
 import numpy as np
-import torch.distributed as dist
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -19,16 +19,20 @@ from part_cases import CASES, GEOM_CASES  # noqa: E402
 
 
 def main():
+    # no torch in a rank process: the library is loaded and its ROCm runtime checked first
+    # (aa-admm_amd/dist.py rank_setup), the rendezvous is aa-admm_amd/rdzv.py
     pkg = importlib.import_module("aa-admm_amd")
-    dist.init_process_group("gloo")
-    rank, size = dist.get_rank(), dist.get_world_size()
+    group, report = pkg.dist.rank_setup()
+    rank, size = group.rank, group.size
+    with open(os.path.join(os.environ["AA_OUT"], f"rank{rank}.runtime.json"), "w") as f:
+        json.dump(report, f)
     case = os.environ["AA_CASE"]
     device = int(os.environ.get("AA_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     ctx = pkg.capi.Context(device)
     if os.environ.get("AA_TRANSPORT", "host") == "rccl":
-        comm = pkg.dist.rccl_comm(ctx, rank, size)
+        comm = pkg.dist.rccl_comm(ctx, group)
     else:
-        comm = pkg.dist.host_comm(rank, size)
+        comm = pkg.dist.host_comm(group)
     if case.startswith("geom:"):
         sc = GEOM_CASES[case[5:]]()
         h, g = pkg.capi.run_geom(ctx, sc, comm=comm)
@@ -37,7 +41,7 @@ def main():
         g.close()
         comm.close()
         ctx.close()
-        dist.destroy_process_group()
+        group.close()
         return
     sc = CASES[case][0]()
     steps, s = pkg.capi.run_scene(ctx, sc, comm=comm)
@@ -52,7 +56,7 @@ def main():
     s.close()
     comm.close()
     ctx.close()
-    dist.destroy_process_group()
+    group.close()
 
 
 if __name__ == "__main__":

@@ -1,6 +1,7 @@
 """bench.py's multi-rank launcher: `bench.py --gpus N` run without an outside
 torch.distributed.run must start N ranks itself (as a child process, before any HIP call) so the
 driver's 1/2/4/8-GPU line reports N ranks, and a WORLD_SIZE that disagrees with --gpus must fail.
+Each rank reports the ROCm runtime it is bound to: never torch's bundled one.
 The CPU test stops at --launch-check (no GPU); the GPU test runs a real 2-rank partitioned step
 (host transport, both ranks on GPU 0)."""
 import json
@@ -36,6 +37,14 @@ def test_bench_gpus2_launches_two_ranks():
     assert [q["rank"] for q in line["ranks"]] == [0, 1]
     assert [q["local_rank"] for q in line["ranks"]] == [0, 1]
     assert line["parallelism"] == "mesh-partitioned2 (rccl)"
+    # each rank: no torch in the process, every runtime object (incl. the dlopened RCCL) from the
+    # directory libaa_admm.so was linked against
+    for q in line["ranks"]:
+        assert q["torch_imported"] is False
+        for name, path in q["runtime_bound"].items():
+            assert os.path.dirname(path) == line["runtime_expected"], (q["rank"], name, path)
+        for name, paths in q["runtime_mapped"].items():
+            assert paths and all(os.path.dirname(p) == line["runtime_expected"] for p in paths), (name, paths)
 
 
 def test_bench_single_gpu_default_is_one_rank():

@@ -10,6 +10,7 @@ which must give bit-identical results to the plain solver.
 Tolerances as the single-GPU parity tests (residual curves relative to comb_0: 1e-9 closed-
 form, 1e-6 L-BFGS; final x the same relative bars); the partition only reorders sums. All
 ranks must agree bit for bit (their decisions come from identical all-reduced values)."""
+import json
 import os
 import socket
 import subprocess
@@ -32,19 +33,27 @@ def _free_port():
 
 
 def run_ranks(case, nranks, out, transport="host", extra_env=None, timeout=240):
-    env = dict(os.environ, AA_CASE=case, AA_OUT=str(out), AA_TRANSPORT=transport, AA_DEVICE="0", AA_COMM_VERIFY="1", AA_FRONT_CHECK="1",
+    env = dict(os.environ, AA_CASE=case, AA_OUT=str(out), AA_TRANSPORT=transport, AA_DEVICE="0", AA_COMM_VERIFY="1",
                OMP_NUM_THREADS="4", **(extra_env or {}))
+    env.pop("AA_FRONT_RETRY", None)   # a wrong first factorization fails the run (dense_gpu.hip front check)
+    dump = os.path.join(REPO, "gpurun_out", "front_dump")
+    os.makedirs(dump, exist_ok=True)
+    env["AA_FRONT_DUMP"] = dump
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
                         "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
                         os.path.join(REPO, "tests", "part_worker.py")],
                        capture_output=True, text=True, timeout=timeout, env=env)
-    # a GPU front whose first Cholesky failed and whose kept copy factored (dense_gpu.hip, DESIGN
-    # §5) is reported on stderr: kept in gpurun_out/ for the diagnosis, the run itself is valid
+    # any GPU front that failed a check is a failed run (the backend throws; its line and the dump
+    # of the kept copy and first attempt stay in gpurun_out/ for tools/front_replay.py)
     notes = [ln for ln in (r.stderr or "").splitlines() if "[front-check]" in ln]
     if notes:
-        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
         with open(os.path.join(REPO, "gpurun_out", "front_check.log"), "a") as fh:
             fh.write(f"{case} P={nranks}: " + " | ".join(notes) + "\n")
+    assert not notes, notes
+    # every rank bound the ROCm runtime the library was built for (part_worker.py: rank_setup)
+    for k in range(nranks):
+        rep = json.load(open(out / f"rank{k}.runtime.json"))
+        assert all(os.path.dirname(v) == rep["expected"] for v in rep["bound"].values()), rep
     if r.returncode != 0:
         errs = "".join(f"--- {f.name}:\n{f.read_text()[-3000:]}\n" for f in sorted(out.glob("rank*.err")))
         assert False, errs + r.stdout[-1000:] + r.stderr[-2000:]
@@ -164,16 +173,40 @@ def test_rccl_transport_one_rank_is_identity(graph, pkg, ctx, monkeypatch, capfd
     comm.close()
 
 
+def test_front_check_failure_is_an_error_with_a_replayable_dump(pkg, ctx, monkeypatch, capfd, tmp_path):
+    """The GPU front check (dense_gpu.hip) is an assertion: a front whose first
+    factorization yields a wrong output (here injected: AA_FRONT_CHECK_POISON=1 puts a NaN into the
+    first GPU front's first attempt) fails initialize with AA_ERR_NUMERIC -- no silent retry -- and
+    AA_FRONT_DUMP writes the kept copy and the first attempt's outputs, which tools/front_replay.py
+    replays on the host: it names the outputs that differ from a CPU factor of the kept copy."""
+    monkeypatch.setenv("AA_DENSE_MIN_FRONT", "64")
+    monkeypatch.delenv("AA_FRONT_RETRY", raising=False)
+    monkeypatch.setenv("AA_FRONT_CHECK_POISON", "1")
+    monkeypatch.setenv("AA_FRONT_DUMP", str(tmp_path))
+    sc = CASES["drop_z"][0]()
+    with pytest.raises(pkg.capi.AAError) as ei:
+        pkg.capi.run_scene(ctx, sc)
+    assert ei.value.code == -4 and "factored wrongly on the first attempt" in str(ei.value), str(ei.value)
+    notes = [ln for ln in capfd.readouterr().err.splitlines() if "[front-check]" in ln]
+    assert len(notes) == 1, notes
+    kept = sorted(tmp_path.glob("front*_kept.bin"))
+    assert len(kept) == 1
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import front_replay
+    rep = front_replay.replay(str(kept[0]))
+    assert rep["kept_factors"] and "first_F" in rep["differ"], rep
+
+
 def test_front_check_retry_is_bit_identical(pkg, ctx, monkeypatch, capfd):
-    """The GPU front backend's kept-copy retry (dense_gpu.hip): a front whose first
-    factorization yields a non-finite entry (here injected: AA_FRONT_CHECK_POISON=1 puts a NaN into
-    the first GPU front's first attempt) is factored again from the kept copy, reported on stderr,
-    and the run's results are the unpoisoned run's bits (rocBLAS atomics off: deterministic)."""
+    """The opt-in kept-copy retry (AA_FRONT_RETRY=1): the poisoned front is factored again from the
+    kept copy, reported on stderr, and the run's results are the unpoisoned run's bits (rocBLAS
+    atomics off: deterministic)."""
     monkeypatch.setenv("AA_DENSE_MIN_FRONT", "64")
     sc = CASES["drop_z"][0]()
     want, s = pkg.capi.run_scene(ctx, sc)
     s.close()
     assert "[front-check]" not in capfd.readouterr().err   # the product check: no false alarm
+    monkeypatch.setenv("AA_FRONT_RETRY", "1")
     monkeypatch.setenv("AA_FRONT_CHECK_POISON", "1")
     got, s = pkg.capi.run_scene(ctx, sc)
     s.close()

@@ -3,10 +3,12 @@
 * the partitioned global solve: nested dissection with forced top bisections, each rank
   forward/backward-sweeping its own part + the shared separators on a partial right-hand side,
   an all-reduce of the separator rows in between (tests/cpp/part_solve.cpp, threads as ranks);
-* the host transport of the C ABI (aa_comm_create_host / aa_comm_allreduce_host) under
-  torch.distributed with gloo, world size 2 -- the transport the GPU partition tests use to put
-  several ranks on one GPU.
+* the multi-rank launch: torch.distributed.run ranks that never import torch, bound to the ROCm
+  runtime the library was built against (capi.check_runtime), rendezvous over aa-admm_amd/rdzv.py,
+  and the host transport of the C ABI (aa_comm_create_host / aa_comm_allreduce_host) over it --
+  the transport the GPU partition tests use to put several ranks on one GPU.
 """
+import json
 import os
 import shutil
 import socket
@@ -59,26 +61,51 @@ def test_fused_subtree_update_slots_never_overlap_live(tmp_path):
 
 
 WORKER = r"""
-import importlib, os, sys
+import importlib, json, os, sys
 import numpy as np
-import torch.distributed as dist
 sys.path.insert(0, os.environ["AA_REPO"])
 pkg = importlib.import_module("aa-admm_amd")
-dist.init_process_group("gloo")
-rank, size = dist.get_rank(), dist.get_world_size()
-comm = pkg.dist.host_comm(rank, size)
+group, report = pkg.dist.rank_setup(timeout=120)     # library + runtime check first, no torch
+assert "torch" not in sys.modules, "a rank process imported torch"
+rank, size = group.rank, group.size
+# the RCCL id path: librccl is loaded from the runtime's directory (ncclGetUniqueId itself needs a
+# GPU, so on the CPU only the load is exercised); the check is repeated after it
+try:
+    pkg.capi.Comm.unique_id()
+except pkg.capi.AAError:
+    pass
+report = pkg.capi.check_runtime()
+comm = pkg.dist.host_comm(group)
 assert comm.info() == (rank, size)
 a = np.arange(7, dtype=np.float64) * (rank + 1) + 0.1 * rank
 out = comm.allreduce_host(a.copy())
-want = sum(np.arange(7, dtype=np.float64) * (r + 1) + 0.1 * r for r in range(size))
-assert np.allclose(out, want, rtol=1e-15, atol=0), (out, want)
-# every rank holds the same bits (the transport broadcasts rank 0's sum)
-g = [None] * size
-dist.all_gather_object(g, out.tobytes())
+want = np.zeros(7)
+for r in range(size):   # the transport sums in rank order: exactly this
+    want += np.arange(7, dtype=np.float64) * (r + 1) + 0.1 * r
+assert np.array_equal(out, want), (out, want)
+# every rank holds the same bits
+g = group.all_gather_json(out.tobytes().hex())
 assert all(x == g[0] for x in g)
+assert group.allreduce_scalar(rank + 0.5, "max") == size - 0.5
+assert group.broadcast_bytes(b"id-from-0" if rank == 0 else None) == b"id-from-0"
+group.barrier()
 comm.close()
-dist.destroy_process_group()
-print("RANK_OK", rank)
+with open(os.path.join(os.environ["AA_OUT"], f"rank{rank}.json"), "w") as f:   # ranks share stdout
+    json.dump(report["bound"], f)
+group.close()
+"""
+
+TORCH_FIRST = r"""
+import importlib, os, sys
+import torch   # a framework with its own bundled ROCm runtime, loaded BEFORE the library
+sys.path.insert(0, os.environ["AA_REPO"])
+pkg = importlib.import_module("aa-admm_amd")
+try:
+    pkg.dist.rank_setup(timeout=5)
+except RuntimeError as e:
+    print("REFUSED", str(e)[:200])
+else:
+    print("ACCEPTED")
 """
 
 
@@ -88,15 +115,80 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_host_transport_gloo_world2(tmp_path, pkg):
+def _torchrun(script, nproc, env, timeout=300):
+    return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+                           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(script)],
+                          capture_output=True, text=True, timeout=timeout, env=env)
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_host_transport_world_n_runs_on_the_built_runtime(nproc, tmp_path, pkg):
+    """torch.distributed.run ranks (the launch bench.py --gpus N makes): every rank loads
+    libaa_admm.so before anything else and binds the ROCm runtime `ldd libaa_admm.so` names --
+    libamdhip64, libhsa-runtime64, rocBLAS, rocSOLVER and (dlopened) RCCL, by dladdr AND by every
+    mapped copy in /proc/self/maps -- never torch's bundled build; the torch-free group then runs
+    the host transport (rank-order sums, identical bits on every rank) and its collectives."""
     w = tmp_path / "worker.py"
     w.write_text(WORKER)
-    env = dict(os.environ, AA_REPO=REPO, OMP_NUM_THREADS="1")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                        "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(w)],
-                       capture_output=True, text=True, timeout=300, env=env)
+    env = dict(os.environ, AA_REPO=REPO, AA_OUT=str(tmp_path), OMP_NUM_THREADS="1")
+    r = _torchrun(w, nproc, env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    assert r.stdout.count("RANK_OK") == 2
+    want = pkg.capi.expected_runtime_dir()
+    for k in range(nproc):
+        bound = json.load(open(tmp_path / f"rank{k}.json"))
+        assert set(bound) == set(pkg.capi.RUNTIME_LIBS)
+        for k, path in bound.items():
+            assert os.path.dirname(path) == want and "torch" not in path, (k, path)
+
+
+def test_runtime_check_refuses_a_process_bound_to_another_rocm(tmp_path):
+    """The check is not vacuous: a process that imported torch first (torch 2.10+rocm7.0 bundles
+    libamdhip64 / rocBLAS / rocSOLVER / RCCL under the SONAMEs of /opt/rocm) is refused."""
+    w = tmp_path / "torch_first.py"
+    w.write_text(TORCH_FIRST)
+    r = subprocess.run([sys.executable, str(w)], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, AA_REPO=REPO))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "REFUSED" in r.stdout and "torch" in r.stdout, r.stdout
+
+
+GROUP_WORKER = r"""
+import importlib, os, sys
+import numpy as np
+sys.path.insert(0, os.environ["AA_REPO"])
+rdzv = importlib.import_module("aa-admm_amd.rdzv")
+g = rdzv.Group.from_env(timeout=60)
+rng = np.random.default_rng(g.rank)
+a = rng.standard_normal(100_003)
+parts = g.all_gather_json(a.tolist())
+want = np.array(parts[0])
+for p in parts[1:]:
+    want = want + np.array(p)
+got = g.allreduce_array(a.copy())
+assert np.array_equal(got, want)
+if os.environ.get("AA_MISMATCH") == "1":
+    try:
+        g.barrier() if g.rank == 0 else g.allreduce_scalar(1.0)
+    except rdzv.GroupError as e:
+        with open(os.path.join(os.environ["AA_OUT"], f"mismatch{g.rank}"), "w") as f:
+            f.write(str(e))
+        sys.exit(0)
+    sys.exit(3)
+g.close()
+open(os.path.join(os.environ["AA_OUT"], f"ok{g.rank}"), "w").close()
+"""
+
+
+@pytest.mark.parametrize("mismatch", ["0", "1"])
+def test_rdzv_group_sums_in_rank_order_and_names_mismatches(mismatch, tmp_path):
+    w = tmp_path / "gw.py"
+    w.write_text(GROUP_WORKER)
+    r = _torchrun(w, 4, dict(os.environ, AA_REPO=REPO, AA_OUT=str(tmp_path), AA_MISMATCH=mismatch), timeout=200)
+    if mismatch == "0":
+        assert r.returncode == 0 and all((tmp_path / f"ok{k}").exists() for k in range(4)), r.stderr[-3000:]
+    else:   # rank 0 sees the first frame of another collective and says so
+        f = tmp_path / "mismatch0"
+        assert f.exists() and "collective mismatch" in f.read_text(), r.stderr[-3000:]
 
 
 def test_solo_rehearsal_comm_host_semantics(pkg):
