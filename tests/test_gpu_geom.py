@@ -398,3 +398,41 @@ def test_gpu_c3_eps_regime_matches_reference(pkg, ctx):
     assert (c < eps).any() and (b < eps).any()
     assert abs(first(c, eps * (1 - 1e-15)) - first(b, eps * (1 - 1e-15))) <= 5
     assert abs(c.min() / b.min() - 1.0) <= 0.1
+
+
+@pytest.mark.parametrize("case,key", [("geom_airport3k_aa10", "pq_airport3k"), ("geom_costa2k_wire_aa5", "wire_costa2k")])
+def test_gpu_quality_reports_match_reference_apps(case, key, pkg, ctx, tmp_path):
+    """The applications' before/after report files (geom_report; PlanarityOpt.cpp:263-275,
+    WireMeshOpt.cpp:306-325) from the GPU solution, with the distances to the reference surface
+    taken by the solver's own closest-point BVH: the reference app's values
+    (tests/golden/quality_reports.npz) within 1e-4 of each file's largest value (the solution's
+    parity bar is 1e-6; corner angles of short edges amplify it)."""
+    import io
+    gr = pkg.geom_report
+    q = np.load(os.path.join(GOLDEN, "quality_reports.npz"))
+    d = np.load(os.path.join(GOLDEN, case + ".npz"))
+    sc, ref = load_geom_case(case)
+    got, g = pkg.capi.run_geom(ctx, sc)
+    closest = lambda P: g.closest_points(0, P)   # noqa: E731
+    buf = io.StringIO()
+    if key == "pq_airport3k":
+        sizes, idx = q[key + "__face_sizes"], q[key + "__face_idx"]
+        faces = np.split(idx, np.cumsum(sizes)[:-1])
+        gr.planarity_report(d["x0"], got["x"], [list(map(int, f)) for f in faces], d["s0_V"], d["s0_F"],
+                            result_dir=str(tmp_path), closest=closest, out=buf)
+        names = ["planarityErrBefore", "planatityErrAfter"]
+    else:
+        faces = d["g1_idx"].reshape(-1, 4, 3)[:, :, 0].tolist()
+        gr.wiremesh_report(d["x0"], got["x"], faces, d["s0_V"], d["s0_F"], float(d["g2_params"][0, 0]),
+                           result_dir=str(tmp_path), closest=closest, out=buf)
+        names = [f"{t}_wiremeshErr{w}" for t in ("edge", "angle", "ref") for w in ("Before", "After")]
+    g.close()
+    for name in names:
+        want = q[f"{key}__{name}"]
+        have = np.loadtxt(os.path.join(tmp_path, name + ".txt"))
+        tol = (1e-10 if name.endswith("Before") else 1e-4) * np.abs(want).max()
+        assert np.abs(have - want).max() <= tol, (name, np.abs(have - want).max() / np.abs(want).max())
+    num = lambda ln: [float(t.rstrip(",")) for t in re.findall(r"[-+0-9.e]+,?", ln.split(":", 1)[-1]) if t.rstrip(",")]  # noqa: E731
+    for a, b in zip(buf.getvalue().splitlines(), q[key + "__stdout"]):
+        assert a.split(":")[0] == b.split(":")[0]
+        np.testing.assert_allclose(num(a), num(b), rtol=1e-4, atol=1e-12)
