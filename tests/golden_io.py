@@ -80,7 +80,7 @@ def case_names(extras=True):
     own outputs directly)."""
     names = sorted(f[:-4] for f in os.listdir(GOLDEN)
                    if f.endswith(".npz") and f not in ("elements.npz", "geom_elements.npz")
-                   and not f.startswith(("geom_", "full_", "mesh_", "eps_")))
+                   and not f.startswith(("geom_", "full_", "mesh_", "eps_", "quality_")))
     if extras:
         return names
     out = []
