@@ -926,11 +926,11 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
                                                  const double* __restrict__ Gc, const long long* __restrict__ ell,
                                                  const double* __restrict__ B0, const double* __restrict__ B1,
                                                  double* __restrict__ Y, double* __restrict__ U, const Ctrl* ctrl,
-                                                 int gate_reject, long long* clk, int clk_stride, int node_off) {
+                                                 int gate_reject, long long* clk, int clk_stride, int node_off, int tree0) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int K = NR / 3;
-    const SubTree T = trees[blockIdx.x];
+    const SubTree T = trees[tree0 + blockIdx.x];
     const int tid = threadIdx.x;
     // the subtree's supernode records, staged in LDS once: a row item then needs one (coalesced)
     // load, its item, before its factor stream, instead of the item and then its record
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(BLOCK) void k_fwd_sub(const SubTree* __restrict__ t
     }
     __syncthreads();
     // optional phase clock (AA_SUB_TIMING): kernel start, then after every barrier
-    long long* ck = clk ? clk + (size_t)blockIdx.x * clk_stride : nullptr;
+    long long* ck = clk ? clk + (size_t)(tree0 + blockIdx.x) * clk_stride : nullptr;
     if (ck && tid == 0) ck[0] = (long long)__builtin_amdgcn_s_memrealtime();
     // kSubU: every update vector consumed inside the subtree lives in LDS (its slot planned by the
     // host over the levels' lifetimes), so a front pull is one LDS read after its ELL offset and
@@ -1019,11 +1019,11 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
                                                  const double* __restrict__ Y, double* __restrict__ X0,
                                                  double* __restrict__ X1, const int* __restrict__ xg,
                                                  const Ctrl* ctrl, int gate_reject,
-                                                 long long* clk, int clk_stride, int node_off) {
+                                                 long long* clk, int clk_stride, int node_off, int tree0) {
     if (solve_gated(ctrl, gate_reject)) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     constexpr int K = NR / 3;
-    const SubTree T = trees[blockIdx.x];
+    const SubTree T = trees[tree0 + blockIdx.x];
     const int tid = threadIdx.x;
     SubNode* sn = reinterpret_cast<SubNode*>(reinterpret_cast<char*>(lds) + node_off);   // as k_fwd_sub
     {
@@ -1045,7 +1045,7 @@ __global__ __launch_bounds__(BLOCK) void k_bwd_sub(const SubTree* __restrict__ t
             for (int k = 0; k < NR; ++k) d[k] = v[k];
         }
     __syncthreads();
-    long long* ck = clk ? clk + (size_t)blockIdx.x * clk_stride : nullptr;
+    long long* ck = clk ? clk + (size_t)(tree0 + blockIdx.x) * clk_stride : nullptr;
     if (ck && tid == 0) ck[0] = (long long)__builtin_amdgcn_s_memrealtime();
     int ph = 1;
     for (int l = T.nlvl - 1; l >= 0; --l) {
@@ -1373,6 +1373,31 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         n_sub_ = (int)strees.size();
         plan_sub_lds(F, kids, p, nb, beg, uoff, bnd_off, ell_w, ell_off, ell, bnd, fidx, bidx, sub_all, strees, snodes, KS,
                      stats, s);
+        // ---- branches (AA_SOLVE_BRANCHES, see direct_solve.hpp): disjoint subtrees of the tree
+        // solved on parallel streams, the supernodes above them ("top") after the join
+        plan_branches(F, inc, fused, kids, p, nb, stats);
+        if (nbr_ > 1) {
+            int dev = 0;
+            AA_HIP(hipStreamGetDevice(s, &dev));
+            for (int b = 0; b < nbr_; ++b) side_[b].create(dev);
+        }
+        sub_rng_.assign(nbr_ + 1, {0, 0});
+        if (nbr_ > 1) {   // fused subtrees grouped by branch (a SubTree is self-contained: reorder freely)
+            std::vector<int> ord(strees.size());
+            for (size_t t = 0; t < ord.size(); ++t) ord[t] = (int)t;
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return brn_[sub_all[a][0]] < brn_[sub_all[b][0]]; });
+            std::vector<SubTree> st2;
+            for (int t : ord) st2.push_back(strees[t]);
+            strees.swap(st2);
+            for (size_t k = 0; k < ord.size(); ++k) {
+                const int b = brn_[sub_all[ord[k]][0]];
+                if (b < 0 || b >= nbr_) throw Error(ERR_STATE, "DirectSolver: fused subtree outside the branches");
+                if (sub_rng_[b].second == 0) sub_rng_[b].first = (int)k;
+                ++sub_rng_[b].second;
+            }
+        } else {
+            sub_rng_[0] = {0, n_sub_};
+        }
         if (stats) {
             double by = 0;
             int nsn = 0;
@@ -1436,8 +1461,11 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     kernels_ = 0;
 
     int max_lds = 0;
+    lbr_.clear();
     for (auto& l : hl) {
         if (l.empty()) continue;
+        if (nbr_ > 1)   // contiguous per branch (then the top): every launch below takes a range
+            std::stable_sort(l.begin(), l.end(), [&](int a, int b) { return brn_[a] < brn_[b]; });
         Level L;
         int fr = 0, br = 0;
         bool fwave = false, bwave = false;
@@ -1554,6 +1582,23 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         L.br_count = (int)breds.size() - L.br_first;
         max_lds = std::max(max_lds, std::max(L.lds_fwd, L.lds_bwd));
         kernels_ += (L.fwd_count ? 1 : 0) + (L.bwd_count ? 1 : 0) + (L.bt_count ? 1 : 0) + (L.ft_count ? 1 : 0);
+        {   // per branch (and the top, slot nbr_): the sub-ranges of this level's four launches
+            auto ranges = [&](int first, int count, auto node_of, int BrRange::*f, int BrRange::*c, size_t base) {
+                for (int k = first; k < first + count; ++k) {
+                    const int b = nbr_ > 1 ? brn_[node_of(k)] : 0;
+                    BrRange& r = lbr_[base + b];
+                    if (r.*c == 0) r.*f = k;
+                    else if (r.*f + r.*c != k) throw Error(ERR_STATE, "DirectSolver: branch ranges not contiguous");
+                    ++(r.*c);
+                }
+            };
+            const size_t base = lbr_.size();
+            lbr_.resize(base + nbr_ + 1);
+            ranges(L.fwd_first, L.fwd_count, [&](int k) { return tasks[k].node; }, &BrRange::fwd_first, &BrRange::fwd_count, base);
+            ranges(L.ft_first, L.ft_count, [&](int k) { return ft_sn[k]; }, &BrRange::ft_first, &BrRange::ft_count, base);
+            ranges(L.bwd_first, L.bwd_count, [&](int k) { return tasks[k].node; }, &BrRange::bwd_first, &BrRange::bwd_count, base);
+            ranges(L.bt_first, L.bt_count, [&](int k) { return bt_sn[k]; }, &BrRange::bt_first, &BrRange::bt_count, base);
+        }
         levels_.push_back(L);
         for (int sn : l) lev_of[sn] = (int)levels_.size() - 1;
         if (stats) {
@@ -1987,6 +2032,72 @@ void DirectSolver::plan_sub_lds(const SupernodalFactor& F, const std::vector<std
                      nu, sub_all.size(), sub_lds_u_, nx, sub_all.size(), sub_lds_x_);
 }
 
+// Branches: the supernodes that head the B heaviest disjoint subtrees (found by expanding the
+// heaviest non-fused node of the frontier, from the roots down, until there are B of them;
+// expanded nodes form the top), dealt to B streams by decreasing factor bytes (each to the
+// lightest stream so far). Every launch of a sweep below the top then runs once per branch on its
+// own stream: a branch's next level starts while another branch's level still drains, so the
+// levels' ramp and tail overlap instead of adding up. Same tasks, tiles and sums: bit-identical.
+void DirectSolver::plan_branches(const SupernodalFactor& F, const std::vector<char>& inc, const std::vector<char>& fused,
+                                 const std::vector<std::vector<int>>& kids, const std::vector<int>& p,
+                                 const std::vector<int>& nb, bool stats) {
+    nbr_ = 1;
+    brn_.assign(nn_, 0);
+    const char* e = std::getenv("AA_SOLVE_BRANCHES");
+    const char* st = std::getenv("AA_SOLVE_STREAM");
+    const int want = std::max(1, std::min(kMaxBranches, e ? std::atoi(e) : kBranches));
+    if (want < 2 || (st && st[0] == '1')) return;
+    // subtree weights (factor entries), children before parents by height
+    std::vector<int> order;
+    for (int sn = 0; sn < nn_; ++sn) if (inc[sn]) order.push_back(sn);
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return F.height[a] < F.height[b]; });
+    std::vector<double> wt(nn_, 0.0);
+    for (int sn : order) {
+        wt[sn] += 0.5 * p[sn] * (p[sn] + 1.0) + (double)p[sn] * nb[sn];
+        if (F.parent[sn] >= 0 && inc[F.parent[sn]]) wt[F.parent[sn]] += wt[sn];
+    }
+    std::vector<int> front, top;
+    for (int sn : order) if (F.parent[sn] < 0 || !inc[F.parent[sn]]) front.push_back(sn);
+    while ((int)front.size() < want) {
+        int best = -1;
+        for (size_t k = 0; k < front.size(); ++k) {
+            const int v = front[k];
+            if (fused[v] || kids[v].empty()) continue;
+            if (best < 0 || wt[v] > wt[front[best]]) best = (int)k;
+        }
+        if (best < 0) break;
+        const int v = front[best];
+        front.erase(front.begin() + best);
+        top.push_back(v);
+        for (int c : kids[v]) front.push_back(c);
+    }
+    if (front.size() < 2) return;
+    const int B = std::min<int>(want, (int)front.size());
+    std::sort(front.begin(), front.end(), [&](int a, int b) { return wt[a] > wt[b]; });
+    std::vector<double> load(B, 0.0);
+    for (int v : front) {
+        const int b = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        load[b] += wt[v];
+        std::vector<int> st2{v};
+        while (!st2.empty()) {
+            const int u = st2.back();
+            st2.pop_back();
+            brn_[u] = b;
+            for (int c : kids[u]) st2.push_back(c);
+        }
+    }
+    for (int v : top) brn_[v] = B;
+    nbr_ = B;
+    if (stats) {
+        double tw = 0;
+        for (int v : top) tw += 0.5 * p[v] * (p[v] + 1.0) + (double)p[v] * nb[v];
+        std::fprintf(stderr, "[solve] branches: %d streams, %zu top supernodes (%.1f MB/sweep), branch MB/sweep:", B, top.size(),
+                     8e-6 * tw);
+        for (double l : load) std::fprintf(stderr, " %.1f", 8e-6 * l);
+        std::fprintf(stderr, "\n");
+    }
+}
+
 void DirectSolver::solve(const double* b, double* x, const Ctrl* ctrl, int gate_reject, hipStream_t s) {
     solve_nr<3>(b, x, nullptr, nullptr, ctrl, gate_reject, s);
 }
@@ -2064,24 +2175,69 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     const int noff_f = (K * (sub_lds_f_ + sub_lds_u_) + 15) / 16 * 16, noff_b = (K * (sub_lds_b_ + sub_lds_x_) + 15) / 16 * 16;
     // queue heads and dependency counters of the streamed runs start from zero every solve
     if (stream_) AA_HIP(hipMemsetAsync(sync_.p, 0, sizeof(int) * ((size_t)n_heads_ + 2 * (size_t)nn_), s));
-#define SUBF(BL) hipLaunchKernelGGL((nt_rows_ ? k_fwd_sub<BL, NR, true> : k_fwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, true), s, sub_trees_.p, \
+#define SUBF(BL, T0, NT, ST) hipLaunchKernelGGL((nt_rows_ ? k_fwd_sub<BL, NR, true> : k_fwd_sub<BL, NR, false>), dim3(NT), dim3(BL), sub_lds_bytes(K, true), ST, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject, \
-                                    clk_on ? sub_clk_.p : nullptr, 64, noff_f)
-    if (n_sub_) switch (sub_block_) { case 1024: SUBF(1024); break; case 512: SUBF(512); break; default: SUBF(256); break; }
+                                    clk_on ? sub_clk_.p : nullptr, 64, noff_f, T0)
+#define SUBB(BL, T0, NT, ST) hipLaunchKernelGGL((nt_rows_ ? k_bwd_sub<BL, NR, true> : k_bwd_sub<BL, NR, false>), dim3(NT), dim3(BL), sub_lds_bytes(K, false), ST, sub_trees_.p, \
+                                    sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, sub_xg_.p, \
+                                    ctrl, gate_reject, clk_on ? sub_clk_.p + 64 * (size_t)n_sub_ : nullptr, 64, noff_b, T0)
+#define FWD(BL, F0, NC, LDS, ST) hipLaunchKernelGGL((nt_rows_ ? k_fwd<BL, NR, true> : k_fwd<BL, NR, false>), dim3(NC), dim3(BL), LDS, ST, T, F0, Gc_.p, \
+                                   ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
+#define BWD(BL, F0, NC, LDS, ST) hipLaunchKernelGGL((nt_rows_ ? k_bwd<BL, NR, true> : k_bwd<BL, NR, false>), dim3(NC), dim3(BL), LDS, ST, T, F0, Gr_.p, \
+                                   bnd_.p, Y_.p, x0, x1, ctrl, gate_reject)
+    auto sub_fwd = [&](int t0, int nt, hipStream_t st) {
+        if (nt) switch (sub_block_) { case 1024: SUBF(1024, t0, nt, st); break; case 512: SUBF(512, t0, nt, st); break; default: SUBF(256, t0, nt, st); break; }
+    };
+    auto sub_bwd = [&](int t0, int nt, hipStream_t st) {
+        if (nt) switch (sub_block_) { case 1024: SUBB(1024, t0, nt, st); break; case 512: SUBB(512, t0, nt, st); break; default: SUBB(256, t0, nt, st); break; }
+    };
+    // one level's forward (row tasks, then split-K tiles) / backward launches over a range
+    auto lvl_fwd = [&](const Level& L, const BrRange& r, hipStream_t st) {
+        if (r.fwd_count) switch (L.fblock) { case 64: FWD(64, r.fwd_first, r.fwd_count, K * L.lds_fwd, st); break;
+                                              case 128: FWD(128, r.fwd_first, r.fwd_count, K * L.lds_fwd, st); break;
+                                              default: FWD(256, r.fwd_first, r.fwd_count, K * L.lds_fwd, st); break; }
+        if (r.ft_count) launch_ftiles<NR>(L.ftw, r.ft_count, r.ft_first, b0, b1, 0, ctrl, gate_reject, st);
+    };
+    auto lvl_bwd = [&](const Level& L, const BrRange& r, hipStream_t st) {
+        if (r.bwd_count) switch (L.bblock) { case 64: BWD(64, r.bwd_first, r.bwd_count, K * L.lds_bwd, st); break;
+                                              case 128: BWD(128, r.bwd_first, r.bwd_count, K * L.lds_bwd, st); break;
+                                              default: BWD(256, r.bwd_first, r.bwd_count, K * L.lds_bwd, st); break; }
+        if (r.bt_count) launch_btiles<NR>(L.btw, r.bt_count, r.bt_first, x0, x1, 0, ctrl, gate_reject, st);
+    };
 #undef SUBF
+#undef SUBB
+#undef FWD
+#undef BWD
+    const int NB = nbr_;
+    if (NB > 1) {
+        // branches: fork, each branch's fused subtrees and levels on its stream, join, then the
+        // top's levels on s (see plan_branches)
+        AA_HIP(hipEventRecord(side_[0].fork_f, s));
+        for (int b = 1; b < NB; ++b) AA_HIP(hipStreamWaitEvent(side_[b].st, side_[0].fork_f, 0));
+        for (int b = 0; b < NB; ++b) {
+            hipStream_t st = b ? side_[b].st : s;
+            sub_fwd(sub_rng_[b].first, sub_rng_[b].second, st);
+            for (size_t li = 0; li < levels_.size(); ++li) lvl_fwd(levels_[li], lbr_[li * (NB + 1) + b], st);
+        }
+        for (int b = 1; b < NB; ++b) {
+            AA_HIP(hipEventRecord(side_[b].join_f, side_[b].st));
+            AA_HIP(hipStreamWaitEvent(s, side_[b].join_f, 0));
+        }
+        for (size_t li = 0; li < levels_.size(); ++li) lvl_fwd(levels_[li], lbr_[li * (NB + 1) + NB], s);
+    } else {
+        sub_fwd(0, n_sub_, s);
+    }
     size_t fs = 0;
-    for (int li = 0; li < (int)levels_.size(); ++li) {
+    for (int li = 0; li < (int)levels_.size() && NB == 1; ++li) {
         const Level& L = levels_[li];
         if (fs < fstreams_.size() && fstreams_[fs].l0 == li) {
             launch_fstream<NR>(fstreams_[fs], b0, b1, ctrl, gate_reject, s);
             li = fstreams_[fs++].l1 - 1;
             continue;
         }
-#define FWD(BL) hipLaunchKernelGGL((nt_rows_ ? k_fwd<BL, NR, true> : k_fwd<BL, NR, false>), dim3(L.fwd_count), dim3(BL), K * L.lds_fwd, s, T, L.fwd_first, Gc_.p, \
-                                   ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject)
-        if (L.fwd_count) switch (L.fblock) { case 64: FWD(64); break; case 128: FWD(128); break; default: FWD(256); break; }
-#undef FWD
-        if (L.ft_count) launch_ftiles<NR>(L.ftw, L.ft_count, L.ft_first, b0, b1, 0, ctrl, gate_reject, s);
+        BrRange r;
+        r.fwd_first = L.fwd_first; r.fwd_count = L.fwd_count; r.ft_first = L.ft_first; r.ft_count = L.ft_count;
+        lvl_fwd(L, r, s);
     }
     // partitioned: the top rows of Y hold this GPU's share of the forward result (linear in b
     // and in the update vectors); their sum over the GPUs is the full forward result. When the
@@ -2111,6 +2267,23 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     } else if (comm_ && top_beg_ < n_) {
         comm_->allreduce_sum(Y_.p + NR * (size_t)top_beg_, Y_.p + NR * (size_t)top_beg_, NR * (size_t)(n_ - top_beg_), s);
     }
+    if (NB > 1) {   // the backward mirrors the forward: the top first, then the branches
+        for (int li = (int)levels_.size() - 1; li >= 0; --li) lvl_bwd(levels_[li], lbr_[li * (NB + 1) + NB], s);
+        AA_HIP(hipEventRecord(side_[0].fork_b, s));
+        for (int b = 1; b < NB; ++b) AA_HIP(hipStreamWaitEvent(side_[b].st, side_[0].fork_b, 0));
+        for (int b = 0; b < NB; ++b) {
+            hipStream_t st = b ? side_[b].st : s;
+            for (int li = (int)levels_.size() - 1; li >= 0; --li) lvl_bwd(levels_[li], lbr_[li * (NB + 1) + b], st);
+            sub_bwd(sub_rng_[b].first, sub_rng_[b].second, st);
+        }
+        for (int b = 1; b < NB; ++b) {
+            AA_HIP(hipEventRecord(side_[b].join_b, side_[b].st));
+            AA_HIP(hipStreamWaitEvent(s, side_[b].join_b, 0));
+        }
+        AA_CHECK_LAUNCH();
+        if (clk_on) --sub_timing_;
+        return;
+    }
     size_t bs = 0;
     for (int li = (int)levels_.size() - 1; li >= 0; --li) {
         const Level& L = levels_[li];
@@ -2119,17 +2292,11 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
             li = bstreams_[bs++].l0;
             continue;
         }
-#define BWD(BL) hipLaunchKernelGGL((nt_rows_ ? k_bwd<BL, NR, true> : k_bwd<BL, NR, false>), dim3(L.bwd_count), dim3(BL), K * L.lds_bwd, s, T, L.bwd_first, Gr_.p, \
-                                   bnd_.p, Y_.p, x0, x1, ctrl, gate_reject)
-        if (L.bwd_count) switch (L.bblock) { case 64: BWD(64); break; case 128: BWD(128); break; default: BWD(256); break; }
-#undef BWD
-        if (L.bt_count) launch_btiles<NR>(L.btw, L.bt_count, L.bt_first, x0, x1, 0, ctrl, gate_reject, s);
+        BrRange r;
+        r.bwd_first = L.bwd_first; r.bwd_count = L.bwd_count; r.bt_first = L.bt_first; r.bt_count = L.bt_count;
+        lvl_bwd(L, r, s);
     }
-#define SUBB(BL) hipLaunchKernelGGL((nt_rows_ ? k_bwd_sub<BL, NR, true> : k_bwd_sub<BL, NR, false>), dim3(n_sub_), dim3(BL), sub_lds_bytes(K, false), s, sub_trees_.p, \
-                                    sub_levels_.p, sub_nodes_.p, sub_items_.p, sub_items2_.p, Gr_.p, bnd_.p, Y_.p, x0, x1, sub_xg_.p, \
-                                    ctrl, gate_reject, clk_on ? sub_clk_.p + 64 * (size_t)n_sub_ : nullptr, 64, noff_b)
-    if (n_sub_) switch (sub_block_) { case 1024: SUBB(1024); break; case 512: SUBB(512); break; default: SUBB(256); break; }
-#undef SUBB
+    sub_bwd(0, n_sub_, s);
     AA_CHECK_LAUNCH();
     if (clk_on) {
         --sub_timing_;

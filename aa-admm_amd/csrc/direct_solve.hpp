@@ -110,7 +110,36 @@ public:
     struct FTile { int beg, p, R, c0, r0, nc, rid, ell_w; long long goff, ell_off, poff, toff; int dep, need, pad0, pad1; };
     struct FRed { int beg, p, r0, nr, nt, ell_w; long long uoff, ell_off, poff; int sig, pad; };
 
+    // Branches (AA_SOLVE_BRANCHES=B, default kBranches; single GPU, not with AA_SOLVE_STREAM): the
+    // tree below its top supernodes split into B disjoint groups of subtrees, each swept on its own
+    // stream (fork/join by events, so a captured step records them as parallel graph branches)
+    static constexpr int kMaxBranches = 8, kBranches = 1;
+    struct BrRange { int fwd_first = 0, fwd_count = 0, ft_first = 0, ft_count = 0, bwd_first = 0, bwd_count = 0,
+                     bt_first = 0, bt_count = 0; };
+
 private:
+    struct SideStream {   // branch b's stream (b >= 1; branch 0 runs on the caller's) and its events
+        hipStream_t st = nullptr;
+        hipEvent_t fork_f = nullptr, join_f = nullptr, fork_b = nullptr, join_b = nullptr;
+        void create(int dev) {
+            if (st) return;
+            AA_HIP(hipSetDevice(dev));
+            AA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            for (hipEvent_t* e : {&fork_f, &join_f, &fork_b, &join_b}) AA_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        }
+        ~SideStream() {
+            for (hipEvent_t e : {fork_f, join_f, fork_b, join_b}) if (e) (void)hipEventDestroy(e);
+            if (st) (void)hipStreamDestroy(st);
+        }
+    };
+    int nbr_ = 1;
+    std::vector<int> brn_;                        // branch of every supernode (nbr_ = top)
+    std::vector<BrRange> lbr_;                    // [level][nbr_ + 1]
+    std::vector<std::pair<int, int>> sub_rng_;    // fused subtrees per branch: (first, count)
+    SideStream side_[kMaxBranches];
+    void plan_branches(const SupernodalFactor& F, const std::vector<char>& inc, const std::vector<char>& fused,
+                       const std::vector<std::vector<int>>& kids, const std::vector<int>& p, const std::vector<int>& nb,
+                       bool stats);
     struct Level {
         int fwd_first = 0, fwd_count = 0, bwd_first = 0, bwd_count = 0;
         int bt_first = 0, bt_count = 0, br_first = 0, br_count = 0;   // split-K backward tiles

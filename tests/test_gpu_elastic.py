@@ -516,3 +516,29 @@ def test_gpu_lane_pair_local_step_matches_reference(which, pkg, ctx, monkeypatch
         test_gpu_full_drop40_matches_reference(pkg, ctx)
     else:
         test_gpu_matches_reference_golden(which, pkg, ctx)
+
+
+@pytest.mark.parametrize("branches,pipe,graph", [("2", "1", "1"), ("4", "1", "1"), ("2", "0", "1"), ("3", "1", "0")])
+def test_gpu_solve_branches_bit_identical(pkg, ctx, monkeypatch, capfd, branches, pipe, graph):
+    """The global solve swept as parallel branches (AA_SOLVE_BRANCHES: disjoint subtrees on their
+    own streams, the top after the join; DirectSolver::plan_branches) runs the same tasks, tiles and
+    sums as the single-stream sweep: bit-identical trajectories -- two-set and one-set solves
+    (reject path), captured (hipGraph branches) and eager."""
+    sc = scenes.tet_drop(40, 16, 20, iters=30, n_steps=2)
+    monkeypatch.setenv("AA_Z_PIPELINE", pipe)
+    monkeypatch.setenv("AA_SOLVE_MIN_SUBTREES", "32")
+    monkeypatch.setenv("AA_SOLVE_STATS", "1")
+    if graph == "0":
+        monkeypatch.setenv("AA_ADMM_NO_GRAPH", "1")
+    monkeypatch.setenv("AA_SOLVE_BRANCHES", "1")
+    off, _ = pkg.capi.run_scene(ctx, sc)
+    capfd.readouterr()
+    monkeypatch.setenv("AA_SOLVE_BRANCHES", branches)
+    on, _ = pkg.capi.run_scene(ctx, sc)
+    err = capfd.readouterr().err
+    m = re.search(r"\[solve\] branches: (\d+) streams", err)
+    assert m and int(m.group(1)) == int(branches), err[-2000:]
+    print("rejects", sum(int(r["reject"].sum()) for r in off))   # each re-ran a one-set solve
+    for a, b in zip(off, on):
+        for k in ("prim", "comb", "reject", "x", "v"):
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))

@@ -432,7 +432,23 @@ def test_gpu_quality_reports_match_reference_apps(case, key, pkg, ctx, tmp_path)
         have = np.loadtxt(os.path.join(tmp_path, name + ".txt"))
         tol = (1e-10 if name.endswith("Before") else 1e-4) * np.abs(want).max()
         assert np.abs(have - want).max() <= tol, (name, np.abs(have - want).max() / np.abs(want).max())
-    num = lambda ln: [float(t.rstrip(",")) for t in re.findall(r"[-+0-9.e]+,?", ln.split(":", 1)[-1]) if t.rstrip(",")]  # noqa: E731
+    num = lambda ln: [float(t) for t in re.findall(r"[-+]?\d+(?:\.\d*)?(?:e[-+]?\d+)?", ln.split(":", 1)[-1])]  # noqa: E731
     for a, b in zip(buf.getvalue().splitlines(), q[key + "__stdout"]):
         assert a.split(":")[0] == b.split(":")[0]
         np.testing.assert_allclose(num(a), num(b), rtol=1e-4, atol=1e-12)
+
+
+@pytest.mark.parametrize("builder", [lambda gs: gs.pq_heightfield(90, 90, iters=40, aa_m=10),
+                                     lambda gs: gs.wire_grid(90, 90, iters=40, aa_m=20)])
+def test_gpu_geom_solve_branches_bit_identical(builder, pkg, ctx, monkeypatch):
+    """Geometry: the global solve as parallel branches (AA_SOLVE_BRANCHES=2 / 4) is bit-identical
+    to the single-stream sweep (the same tasks, tiles and sums)."""
+    sc = builder(pkg.geom_scenes)
+    monkeypatch.setenv("AA_SOLVE_BRANCHES", "1")
+    want, g = pkg.capi.run_geom(ctx, sc)
+    g.close()
+    for b in ("2", "4"):
+        monkeypatch.setenv("AA_SOLVE_BRANCHES", b)
+        got, g = pkg.capi.run_geom(ctx, sc)
+        g.close()
+        assert np.array_equal(got["comb"], want["comb"]) and np.array_equal(got["x"], want["x"]), b
