@@ -4,7 +4,8 @@
 // rocSOLVER / rocBLAS on the solver's stream instead of the host's right-looking loop.
 //   assembly   scatter-add of A's pivot columns, then of each child's update matrix (child order,
 //              one launch each: every front entry receives its terms in the host loop's order)
-//   factor     dpotrf (L11), dtrsm (L21 = F21 L11^-T), dsyrk (F22 -= L21 L21^T)
+//   factor     L11 by a blocked Cholesky (k_potf2 diagonal blocks + dtrsm / dsyrk; not rocsolver_dpotrf,
+//              see potrf()), dtrsm (L21 = F21 L11^-T), dsyrk (F22 -= L21 L21^T)
 //   outputs    dtrtri (Linv = L11^-1), dtrmm (M = L21 Linv), transposed to the host's row-major
 //              layouts on the device; F22 stays on the device when the parent is factored here
 #include <hip/hip_runtime.h>
@@ -88,6 +89,44 @@ __global__ void k_count_nonfinite(const double* __restrict__ a, int ld, int rows
         int t = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sc[w];
         if (t) atomicAdd(out, t);
+    }
+}
+
+// Unblocked Cholesky of one kb x kb diagonal block (kb <= kPotfBlock) of the column-major matrix
+// at A (leading dimension lda), lower triangle, in LDS: column j scaled by 1 / sqrt(a_jj), then the
+// trailing triangle updated, one workgroup. A pivot that is not > 0 (or NaN) stops the block and
+// stores its global index + 1 in *info (the first failing pivot, as rocsolver's info).
+constexpr int kPotfBlock = 128;
+__global__ __launch_bounds__(256) void k_potf2(double* __restrict__ A, int lda, int kb, int k0, int* info) {
+    __shared__ double a[kPotfBlock * (kPotfBlock + 1)];   // column-major, padded leading dimension
+    constexpr int LD = kPotfBlock + 1;
+    if (*info != 0) return;   // an earlier block failed
+    const int tid = threadIdx.x;
+    for (int k = tid; k < kb * kb; k += blockDim.x) {
+        const int i = k % kb, j = k / kb;
+        a[j * LD + i] = i >= j ? A[(size_t)j * lda + i] : 0.0;
+    }
+    __syncthreads();
+    for (int j = 0; j < kb; ++j) {
+        const double d = a[j * LD + j];
+        if (!(d > 0.0)) {   // uniform: every thread read the same value
+            if (tid == 0) *info = k0 + j + 1;
+            return;
+        }
+        const double ljj = sqrt(d), inv = 1.0 / ljj;
+        __syncthreads();
+        for (int i = j + tid; i < kb; i += blockDim.x) a[j * LD + i] = i == j ? ljj : a[j * LD + i] * inv;
+        __syncthreads();
+        const int m = kb - j - 1;   // trailing triangle: (r, c), j < c <= r < kb
+        for (int k = tid; k < m * m; k += blockDim.x) {
+            const int r = j + 1 + k % m, c = j + 1 + k / m;
+            if (r >= c) a[c * LD + r] -= a[j * LD + r] * a[j * LD + c];
+        }
+        __syncthreads();
+    }
+    for (int k = tid; k < kb * kb; k += blockDim.x) {
+        const int i = k % kb, j = k / kb;
+        if (i >= j) A[(size_t)j * lda + i] = a[j * LD + i];
     }
 }
 
@@ -201,7 +240,8 @@ public:
         double* Md = nb > 0 ? M_.get((size_t)nb * p) : nullptr;
         auto attempt = [&](int* out) {
             AA_HIP(hipMemsetAsync(info_.p, 0, 3 * sizeof(int), s_));
-            rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
+            if (own_potrf_) potrf(h_, F, f, p);
+            else rb_check(rocsolver_dpotrf(h_, rocblas_fill_lower, p, F, f, info_.p), "rocsolver_dpotrf");
             if (nb > 0) {
                 rb_check(rocblas_dtrsm(h_, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
                                        rocblas_diagonal_non_unit, nb, p, &one, F, f, F + p, f), "rocblas_dtrsm");
@@ -375,6 +415,29 @@ public:
     double max_dev = 0;   // largest first-attempt product deviation (AA_SETUP_TIMES)
 
 private:
+    // Cholesky of the p x p leading block of the column-major front F (lower), blocked right-looking:
+    // per 128-column block k_potf2 on the diagonal block, then rocblas_dtrsm for the block's rows
+    // below it and rocblas_dsyrk for the trailing p x p triangle. Replaces rocsolver_dpotrf, which
+    // returns wrong factors (info 0) when several processes run it on one GPU at the same time
+    // (tools/front_stress.hip); rocBLAS trsm / syrk / gemm are unaffected. info_.p[0]:
+    // the first failing pivot + 1.
+    void potrf(rocblas_handle h, double* F, int f, int p) {
+        const double one = 1.0, mone = -1.0;
+        for (int k0 = 0; k0 < p; k0 += kPotfBlock) {
+            const int kb = std::min(kPotfBlock, p - k0), rest = p - k0 - kb;
+            double* Akk = F + (size_t)k0 * f + k0;
+            hipLaunchKernelGGL(k_potf2, dim3(1), dim3(256), 0, s_, Akk, f, kb, k0, info_.p);
+            AA_CHECK_LAUNCH();
+            if (rest > 0) {   // (after a failed pivot the rest runs on garbage; info already says so)
+                rb_check(rocblas_dtrsm(h, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                                       rocblas_diagonal_non_unit, rest, kb, &one, Akk, f, Akk + kb, f), "rocblas_dtrsm");
+                rb_check(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, rest, kb, &mone, Akk + kb, f, &one,
+                                       Akk + (size_t)kb * f + kb, f), "rocblas_dsyrk");
+            }
+        }
+    }
+    // AA_FRONT_POTRF=rocsolver: rocsolver_dpotrf instead of potrf() above (single-process A/B)
+    bool own_potrf_ = !(std::getenv("AA_FRONT_POTRF") && std::strcmp(std::getenv("AA_FRONT_POTRF"), "rocsolver") == 0);
     // AA_FRONT_DUMP: the kept front and the first attempt's outputs of front s, column-major
     // doubles, for a replay in one process (tools/front_replay.py)
     void dump(const char* dir, int s, int f, int p, int nb, const double* Fk, const double* F, const double* L,

@@ -37,8 +37,9 @@ def run_ranks(case, nranks, out, transport="host", extra_env=None, timeout=240):
     env = dict(os.environ, AA_CASE=case, AA_OUT=str(out), AA_TRANSPORT=transport, AA_DEVICE="0", AA_COMM_VERIFY="1",
                OMP_NUM_THREADS="4", **(extra_env or {}))
     env.pop("AA_FRONT_RETRY", None)   # a wrong first factorization fails the run (dense_gpu.hip front check)
-    dump = os.path.join(REPO, "gpurun_out", "front_dump")
+    dump = os.environ.get("AA_TEST_FRONT_DUMP", "/tmp/aa_front_dump")   # f x f doubles per matrix: not under gpurun_out
     os.makedirs(dump, exist_ok=True)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     env["AA_FRONT_DUMP"] = dump
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
                         "--master-addr=127.0.0.1", f"--master-port={_free_port()}",

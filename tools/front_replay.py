@@ -40,8 +40,15 @@ def _cmp(name, got, want, lower=False):
     diff[~np.isfinite(got)] = np.inf
     dev = float(diff.max() / scale)
     idx = np.argwhere(diff > TOL * scale)
-    return {"output": name, "rel_dev": dev, "n_wrong": int(len(idx)),
-            "first_wrong": [[int(i), int(j), float(got[i, j]), float(want[i, j])] for i, j in idx[:5]]}
+    out = {"output": name, "shape": list(got.shape), "rel_dev": dev, "n_wrong": int(len(idx)),
+           "first_wrong": [[int(i), int(j), float(got[i, j]), float(want[i, j])] for i, j in idx[:5]]}
+    if len(idx):   # where: bounding box and the 64 x 64 tiles holding wrong entries (a kernel's blocks)
+        out["rows"] = [int(idx[:, 0].min()), int(idx[:, 0].max())]
+        out["cols"] = [int(idx[:, 1].min()), int(idx[:, 1].max())]
+        tiles, cnt = np.unique(idx // 64, axis=0, return_counts=True)
+        out["tiles64"] = [[int(a), int(b), int(c)] for (a, b), c in zip(tiles[:40], cnt[:40])]
+        out["n_tiles64"] = int(len(tiles))
+    return out
 
 
 def replay(kept_path: str) -> dict:
