@@ -2043,9 +2043,11 @@ void DirectSolver::plan_branches(const SupernodalFactor& F, const std::vector<ch
                                  const std::vector<int>& nb, bool stats) {
     nbr_ = 1;
     brn_.assign(nn_, 0);
+    const char* er = std::getenv("AA_SOLVE_BRANCHES_REJECT");
+    branch_reject_ = er && er[0] == '1';
     const char* e = std::getenv("AA_SOLVE_BRANCHES");
     const char* st = std::getenv("AA_SOLVE_STREAM");
-    const int want = std::max(1, std::min(kMaxBranches, e ? std::atoi(e) : kBranches));
+    const int want = std::max(1, std::min(kMaxBranches, e ? std::atoi(e) : default_branches));
     if (want < 2 || (st && st[0] == '1')) return;
     // subtree weights (factor entries), children before parents by height
     std::vector<int> order;
@@ -2208,7 +2210,9 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
 #undef SUBB
 #undef FWD
 #undef BWD
-    const int NB = nbr_;
+    // the reject path's gated one-set solve (skipped in most iterations) on one stream unless
+    // AA_SOLVE_BRANCHES_REJECT=1: a skipped solve costs its launches, twice the streams twice them
+    const int NB = (gate_reject && !branch_reject_) ? 1 : nbr_;
     if (NB > 1) {
         // branches: fork, each branch's fused subtrees and levels on its stream, join, then the
         // top's levels on s (see plan_branches)

@@ -113,7 +113,8 @@ public:
     // Branches (AA_SOLVE_BRANCHES=B, default kBranches; single GPU, not with AA_SOLVE_STREAM): the
     // tree below its top supernodes split into B disjoint groups of subtrees, each swept on its own
     // stream (fork/join by events, so a captured step records them as parallel graph branches)
-    static constexpr int kMaxBranches = 8, kBranches = 1;
+    static constexpr int kMaxBranches = 8;
+    int default_branches = 1;   // set by the caller before build(); AA_SOLVE_BRANCHES overrides
     struct BrRange { int fwd_first = 0, fwd_count = 0, ft_first = 0, ft_count = 0, bwd_first = 0, bwd_count = 0,
                      bt_first = 0, bt_count = 0; };
 
@@ -133,6 +134,7 @@ private:
         }
     };
     int nbr_ = 1;
+    bool branch_reject_ = false;                  // AA_SOLVE_BRANCHES_REJECT: the gated reject solve branched too
     std::vector<int> brn_;                        // branch of every supernode (nbr_ = top)
     std::vector<BrRange> lbr_;                    // [level][nbr_ + 1]
     std::vector<std::pair<int, int>> sub_rng_;    // fused subtrees per branch: (first, count)

@@ -447,6 +447,10 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     conc_fork_ = std::getenv("AA_CONC_FORK") ? std::atoi(std::getenv("AA_CONC_FORK")) : 1;
     // Z variant + Anderson: the two-set layout whether pipelined or not (same sums, same bits)
     stamp("factor");
+    // the sweeps as two parallel branches (DirectSolver::plan_branches): measured on C4 (one GPU,
+    // Z variant) 407-408 -> 412-416 it/s; three or four branches, and the geometry configs, slower
+    // 
+    solver_.default_branches = (P == 1 && st_.variant == AA_VARIANT_Z) ? 2 : 1;
     solver_.build(F, s(), P > 1 ? &tree.part : nullptr, rank_, top_beg_, comm_, pipe_z_ ? 2 : 1,
                   st_.variant == AA_VARIANT_Z && st_.acceleration_type == 1);
     stamp("solver build + upload");

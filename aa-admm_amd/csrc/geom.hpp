@@ -148,7 +148,8 @@ private:
     void enqueue_iteration(int m);
     void enqueue_iteration_plain(int m);
     void enqueue_u_update(double* red, hipStream_t st);
-    // Constraint groups on parallel graph branches (AA_CONCURRENT=0 keeps one stream): each
+    // Constraint groups on parallel graph branches (opt-in, AA_GEOM_CONCURRENT=1; measured slower,
+    // DESIGN.md §3.4 -- off by default, one stream): each
     // group's z / u kernels write only its own z, u, rhs slots and residual partials, so the
     // groups other than the heaviest run on side_ beside it (joined before the next consumer)
     bool conc_ = false;
