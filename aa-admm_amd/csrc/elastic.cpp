@@ -518,6 +518,7 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
         dg.vol.upload(hg.vol, s());
         GroupDev& d = dg.d;
         d.kind = hg.kind; d.mat = hg.material; d.count = cnt; d.nv = hg.nv; d.ncol = hg.ncol; d.dim = 3 * hg.ncol;
+        d.pinned = std::any_of(idx.begin(), idx.end(), [&](int q) { return q >= nf_; }) ? 1 : 0;
         d.zoff = zoff; d.yrow = yrow;
         d.idx = dg.idx.p; d.G = dg.G.p; d.w = dg.w.p; d.vol = dg.vol.p;
         d.mu = hg.lame.mu; d.lambda = hg.lame.lambda; d.k = hg.lame.lambda + (2.0 / 3.0) * hg.lame.mu;

@@ -13,6 +13,7 @@ struct GroupDev {
     int mat;             // 0 linear, 1 NeoHookean, 2 StVK
     int count;           // elements
     int nv, ncol, dim;   // 4/3/9 for tets, 3/2/6 for tris
+    int pinned;          // some element of the group has a pinned node (C_fix terms exist)
     long long zoff;      // z/u offset: component c of element e at zoff + c*count + e
     long long yrow;      // first vertex slot of this group in the slot array y (slot e*nv + a, 3 doubles)
     const int* idx;      // [nv][count] internal node ids

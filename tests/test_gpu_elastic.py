@@ -542,3 +542,59 @@ def test_gpu_solve_branches_bit_identical(pkg, ctx, monkeypatch, capfd, branches
     for a, b in zip(off, on):
         for k in ("prim", "comb", "reject", "x", "v"):
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
+
+
+RHO0_WORKER = r"""
+import importlib, json, os, sys
+import numpy as np
+sys.path.insert(0, os.environ["AA_REPO"]); sys.path.insert(0, os.path.join(os.environ["AA_REPO"], "tests"))
+sys.path.insert(0, os.path.join(os.environ["AA_REPO"], "tests", "golden"))
+pkg = importlib.import_module("aa-admm_amd")
+assert pkg.capi.LIB_PATH.endswith("libaa_admm_rho0.so"), pkg.capi.LIB_PATH
+from golden_io import GOLDEN, check_full_golden, compare, load_case
+from test_gpu_elastic import tolerances
+from make_golden import scene_digest
+scenes = pkg.scenes
+ctx = pkg.capi.Context(0)
+out = {}
+for name in ("cantilever_z_nh_aa6", "drop6_z_nh_aa6", "cant8_z_stvk_noaa"):
+    sc, ref = load_case(name)
+    got, _ = pkg.capi.run_scene(ctx, sc)
+    tc, tx = tolerances(name)
+    out[name] = compare(ref, got, tc, tx)
+    np.save(os.path.join(os.environ["AA_OUT"], name + ".npy"), np.concatenate([g["comb"] for g in got]))
+ref = np.load(os.path.join(GOLDEN, "full_drop40_z_nh_aa6.npz"))
+sc = scenes.tet_drop(40, 16, 20, iters=10, n_steps=3)
+assert np.array_equal(scene_digest(sc), ref["digest"])
+got, _ = pkg.capi.run_scene(ctx, sc)
+out["full_drop40_z_nh_aa6"] = check_full_golden(got, ref)
+json.dump(out, open(os.path.join(os.environ["AA_OUT"], "rho0.json"), "w"))
+"""
+
+
+def test_gpu_lbfgs_rho0_variant_matches_goldens(pkg, ctx, tmp_path):
+    """The exact-arithmetic build of the hyperelastic L-BFGS (libaa_admm_rho0.so, AA_LBFGS_RHO=0:
+    the two-loop recursion divides by y.s as mcloptlib's LBFGS.hpp:272-287 does, instead of the
+    default's multiplication by a stored rho = 1 / y.s) holds the NeoHookean / StVK reference goldens
+    at the default build's bars: configs[0] (cantilever_z_nh_aa6), the 6-cube drop, the StVK
+    cantilever and the 64 000-tet C4-recipe drop. Its combined-residual curves differ from the
+    default build's by rounding only (the rho products move the L-BFGS iterates by ulps, inside its
+    1e-6 gradient tolerance)."""
+    import json
+    import subprocess
+    import sys
+    lib = os.path.join(os.path.dirname(pkg.capi.LIB_PATH), "libaa_admm_rho0.so")
+    assert os.path.exists(lib), "build the rho0 variant (make -C aa-admm_amd)"
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    w = tmp_path / "rho0_worker.py"
+    w.write_text(RHO0_WORKER)
+    r = subprocess.run([sys.executable, str(w)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, AA_ADMM_LIB=lib, AA_REPO=repo, AA_OUT=str(tmp_path)))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.load(open(tmp_path / "rho0.json"))
+    assert all(not v for v in res.values()), res
+    for name in ("cantilever_z_nh_aa6", "drop6_z_nh_aa6"):   # the default build on the same scenes
+        sc, ref = load_case(name)
+        got, _ = pkg.capi.run_scene(ctx, sc)
+        a, b = np.concatenate([g["comb"] for g in got]), np.load(tmp_path / (name + ".npy"))
+        assert a.shape == b.shape and np.abs(a - b).max() <= 1e-6 * a[0], name
