@@ -94,40 +94,37 @@ __global__ void k_count_nonfinite(const double* __restrict__ a, int ld, int rows
 
 // Unblocked Cholesky of one kb x kb diagonal block (kb <= kPotfBlock) of the column-major matrix
 // at A (leading dimension lda), lower triangle, in LDS: column j scaled by 1 / sqrt(a_jj), then the
-// trailing triangle updated, one workgroup. A pivot that is not > 0 (or NaN) stops the block and
-// stores its global index + 1 in *info (the first failing pivot, as rocsolver's info).
+// trailing triangle updated, one workgroup of 256 threads = a thread per row x two column groups
+// (no index division: the first version's k / m, k % m per trailing entry cost ~390 us per block).
+// A pivot that is not > 0 (or NaN) stops the block and stores its global index + 1 in *info (the
+// first failing pivot, as rocsolver's info). Every entry is updated by j ascending.
 constexpr int kPotfBlock = 128;
 __global__ __launch_bounds__(256) void k_potf2(double* __restrict__ A, int lda, int kb, int k0, int* info) {
     __shared__ double a[kPotfBlock * (kPotfBlock + 1)];   // column-major, padded leading dimension
     constexpr int LD = kPotfBlock + 1;
     if (*info != 0) return;   // an earlier block failed
-    const int tid = threadIdx.x;
-    for (int k = tid; k < kb * kb; k += blockDim.x) {
-        const int i = k % kb, j = k / kb;
-        a[j * LD + i] = i >= j ? A[(size_t)j * lda + i] : 0.0;
-    }
+    const int r = threadIdx.x % kPotfBlock, cg = threadIdx.x / kPotfBlock;   // row, column group 0 / 1
+    if (r < kb)
+        for (int c = cg; c < kb; c += 2) a[c * LD + r] = r >= c ? A[(size_t)c * lda + r] : 0.0;
     __syncthreads();
     for (int j = 0; j < kb; ++j) {
         const double d = a[j * LD + j];
         if (!(d > 0.0)) {   // uniform: every thread read the same value
-            if (tid == 0) *info = k0 + j + 1;
+            if (threadIdx.x == 0) *info = k0 + j + 1;
             return;
         }
         const double ljj = sqrt(d), inv = 1.0 / ljj;
+        __syncthreads();   // d read by all before column j is rewritten
+        if (cg == 0 && r >= j && r < kb) a[j * LD + r] = r == j ? ljj : a[j * LD + r] * inv;
         __syncthreads();
-        for (int i = j + tid; i < kb; i += blockDim.x) a[j * LD + i] = i == j ? ljj : a[j * LD + i] * inv;
-        __syncthreads();
-        const int m = kb - j - 1;   // trailing triangle: (r, c), j < c <= r < kb
-        for (int k = tid; k < m * m; k += blockDim.x) {
-            const int r = j + 1 + k % m, c = j + 1 + k / m;
-            if (r >= c) a[c * LD + r] -= a[j * LD + r] * a[j * LD + c];
+        if (r > j && r < kb) {
+            const double lrj = a[j * LD + r];
+            for (int c = j + 1 + cg; c <= r; c += 2) a[c * LD + r] -= lrj * a[j * LD + c];
         }
         __syncthreads();
     }
-    for (int k = tid; k < kb * kb; k += blockDim.x) {
-        const int i = k % kb, j = k / kb;
-        if (i >= j) A[(size_t)j * lda + i] = a[j * LD + i];
-    }
+    if (r < kb)
+        for (int c = cg; c <= r && c < kb; c += 2) A[(size_t)c * lda + r] = a[c * LD + r];
 }
 
 template <class T>

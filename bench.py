@@ -734,7 +734,7 @@ def main():
             roof["read_peak_measured"] = None
             roof["read_peak_error"] = str(e)[:120]
     if roof is not None:   # HBM bytes per solve from the committed PMC passes (tools/gpu.sh pmc)
-        pmc = next((q for q in (os.path.join(REPO, "profiles", f"r{k}_{args.config}_pmc.json") for k in (5, 4, 3, 2, 1))
+        pmc = next((q for q in (os.path.join(REPO, "profiles", f"r{k}_{args.config}_pmc.json") for k in (6, 5, 4, 3, 2, 1))
                     if os.path.exists(q)), "")
         if pmc and comm is None:
             # the PMC group of the same solve the roofline times: two-set (6 RHS) when pipelined
