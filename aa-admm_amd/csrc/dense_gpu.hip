@@ -94,18 +94,19 @@ __global__ void k_count_nonfinite(const double* __restrict__ a, int ld, int rows
 
 // Unblocked Cholesky of one kb x kb diagonal block (kb <= kPotfBlock) of the column-major matrix
 // at A (leading dimension lda), lower triangle, in LDS: column j scaled by 1 / sqrt(a_jj), then the
-// trailing triangle updated, one workgroup of 256 threads = a thread per row x two column groups
-// (no index division: the first version's k / m, k % m per trailing entry cost ~390 us per block).
+// trailing triangle updated, one workgroup of 256 threads = a thread per row x four column groups
+// (measured on C4 setup, 394 blocks: 128-column blocks with k / m, k % m per trailing entry 390 us
+// per block, with two column groups 216 us, with a wave-uniform predicated loop 268 us).
 // A pivot that is not > 0 (or NaN) stops the block and stores its global index + 1 in *info (the
 // first failing pivot, as rocsolver's info). Every entry is updated by j ascending.
-constexpr int kPotfBlock = 128;
+constexpr int kPotfBlock = 64, kPotfGroups = 256 / kPotfBlock;
 __global__ __launch_bounds__(256) void k_potf2(double* __restrict__ A, int lda, int kb, int k0, int* info) {
     __shared__ double a[kPotfBlock * (kPotfBlock + 1)];   // column-major, padded leading dimension
-    constexpr int LD = kPotfBlock + 1;
+    constexpr int LD = kPotfBlock + 1, NG = kPotfGroups;
     if (*info != 0) return;   // an earlier block failed
-    const int r = threadIdx.x % kPotfBlock, cg = threadIdx.x / kPotfBlock;   // row, column group 0 / 1
+    const int r = threadIdx.x % kPotfBlock, cg = threadIdx.x / kPotfBlock;   // row, column group
     if (r < kb)
-        for (int c = cg; c < kb; c += 2) a[c * LD + r] = r >= c ? A[(size_t)c * lda + r] : 0.0;
+        for (int c = cg; c < kb; c += NG) a[c * LD + r] = r >= c ? A[(size_t)c * lda + r] : 0.0;
     __syncthreads();
     for (int j = 0; j < kb; ++j) {
         const double d = a[j * LD + j];
@@ -119,12 +120,12 @@ __global__ __launch_bounds__(256) void k_potf2(double* __restrict__ A, int lda, 
         __syncthreads();
         if (r > j && r < kb) {
             const double lrj = a[j * LD + r];
-            for (int c = j + 1 + cg; c <= r; c += 2) a[c * LD + r] -= lrj * a[j * LD + c];
+            for (int c = j + 1 + cg; c <= r; c += NG) a[c * LD + r] -= lrj * a[j * LD + c];
         }
         __syncthreads();
     }
     if (r < kb)
-        for (int c = cg; c <= r && c < kb; c += 2) A[(size_t)c * lda + r] = a[c * LD + r];
+        for (int c = cg; c <= r && c < kb; c += NG) A[(size_t)c * lda + r] = a[c * LD + r];
 }
 
 template <class T>
@@ -413,7 +414,7 @@ public:
 
 private:
     // Cholesky of the p x p leading block of the column-major front F (lower), blocked right-looking:
-    // per 128-column block k_potf2 on the diagonal block, then rocblas_dtrsm for the block's rows
+    // per 64-column block k_potf2 on the diagonal block, then rocblas_dtrsm for the block's rows
     // below it and rocblas_dsyrk for the trailing p x p triangle. Replaces rocsolver_dpotrf, which
     // returns wrong factors (info 0) when several processes run it on one GPU at the same time
     // (tools/front_stress.hip); rocBLAS trsm / syrk / gemm are unaffected. info_.p[0]:

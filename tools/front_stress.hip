@@ -58,14 +58,14 @@ static double max_rel_diff(const double* da, const double* db, size_t n) {
 }
 
 // the product's replacement (aa-admm_amd/csrc/dense_gpu.hip RocFrontBackend::potrf), same code
-constexpr int kPotfBlock = 128;
+constexpr int kPotfBlock = 64, kPotfGroups = 256 / kPotfBlock;
 __global__ __launch_bounds__(256) void k_potf2(double* __restrict__ A, int lda, int kb, int k0, int* info) {
     __shared__ double a[kPotfBlock * (kPotfBlock + 1)];   // column-major, padded leading dimension
-    constexpr int LD = kPotfBlock + 1;
+    constexpr int LD = kPotfBlock + 1, NG = kPotfGroups;
     if (*info != 0) return;   // an earlier block failed
-    const int r = threadIdx.x % kPotfBlock, cg = threadIdx.x / kPotfBlock;   // row, column group 0 / 1
+    const int r = threadIdx.x % kPotfBlock, cg = threadIdx.x / kPotfBlock;   // row, column group
     if (r < kb)
-        for (int c = cg; c < kb; c += 2) a[c * LD + r] = r >= c ? A[(size_t)c * lda + r] : 0.0;
+        for (int c = cg; c < kb; c += NG) a[c * LD + r] = r >= c ? A[(size_t)c * lda + r] : 0.0;
     __syncthreads();
     for (int j = 0; j < kb; ++j) {
         const double d = a[j * LD + j];
@@ -79,12 +79,12 @@ __global__ __launch_bounds__(256) void k_potf2(double* __restrict__ A, int lda, 
         __syncthreads();
         if (r > j && r < kb) {
             const double lrj = a[j * LD + r];
-            for (int c = j + 1 + cg; c <= r; c += 2) a[c * LD + r] -= lrj * a[j * LD + c];
+            for (int c = j + 1 + cg; c <= r; c += NG) a[c * LD + r] -= lrj * a[j * LD + c];
         }
         __syncthreads();
     }
     if (r < kb)
-        for (int c = cg; c <= r && c < kb; c += 2) A[(size_t)c * lda + r] = a[c * LD + r];
+        for (int c = cg; c <= r && c < kb; c += NG) A[(size_t)c * lda + r] = a[c * LD + r];
 }
 
 static void potrf_blocked(rocblas_handle h, hipStream_t s, double* F, int f, int p, int* info) {
