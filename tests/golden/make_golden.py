@@ -230,6 +230,25 @@ def full_c4(tmp):
     print("full_c4_block_z_nh_aa6", [len(s["prim"]) for s in steps])
 
 
+def full_c4_2steps(tmp):
+    """full_c4 over TWO time steps of 10 iterations (the second starts from the reference's own
+    first-step state: velocity update, pins, the Anderson restart between steps) --
+    full_c4_block_z_nh_aa6_2steps.npz. About three hours of the reference's serial setup here."""
+    sc = scenes.tet_drop(100, 40, 50, iters=10, n_steps=2)
+    steps = run_ref(sc, tmp)
+    rng = np.random.default_rng(6)
+    sample = np.sort(rng.choice(sc.n_nodes, 512, replace=False)).astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "full_c4_block_z_nh_aa6_2steps.npz"), digest=scene_digest(sc), sample=sample,
+                        nrec=np.array([len(s["prim"]) for s in steps]),
+                        prim=np.concatenate([s["prim"] for s in steps]), comb=np.concatenate([s["comb"] for s in steps]),
+                        reject=np.concatenate([s["reject"] for s in steps]),
+                        x_sample=np.stack([s["x"][sample] for s in steps]),
+                        v_sample=np.stack([s["v"][sample] for s in steps]),
+                        x_sum=np.stack([s["x"].sum(0) for s in steps]), v_sum=np.stack([s["v"].sum(0) for s in steps]),
+                        step_ms=np.array([s["step_ms"] for s in steps]))
+    print("full_c4_block_z_nh_aa6_2steps", [len(s["prim"]) for s in steps])
+
+
 def residual_files(tmp):
     """The reference's own Solver::save() output (Solver.hpp:130-155: result/residual-<m>.txt,
     written by every step()) for one (u,x)-variant and one z-variant scene, kept verbatim as data
@@ -255,6 +274,10 @@ def main(only=None):
     if only == ["--full"]:
         with tempfile.TemporaryDirectory() as tmp:
             full_drop40(tmp)
+        return
+    if only == ["--full-c4-2steps"]:
+        with tempfile.TemporaryDirectory() as tmp:
+            full_c4_2steps(tmp)
         return
     if only == ["--full-c4"]:
         with tempfile.TemporaryDirectory() as tmp:
