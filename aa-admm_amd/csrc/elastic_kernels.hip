@@ -245,12 +245,19 @@ struct LqHist {
     using type = typename std::conditional<HV == LQ_HIST_YLDS, dev::HyperLbfgsLds, dev::HyperLbfgs>::type;
 };
 
-template <int NV, int HV>
+// CHUNK (AA_LQ_CHUNK=1): the wave claims its elements in chunks of 64 one chunk AHEAD (a
+// wave-uniform range [p0, p1) plus the next chunk's base nx, claimed while the current one is
+// worked on), so a refill's element ids are known without waiting for the queue atomic: the refill
+// chain is node ids -> positions instead of atomic -> node ids -> positions. The last chunks (the
+// queue within `margin` elements of its end) are claimed at the refill, as CHUNK = 0 does, so no
+// wave sits on unstarted elements while others run dry. Same elements, same arithmetic per
+// element: bit-identical outputs.
+template <int NV, int HV, int CHUNK = 0>
 __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double* __restrict__ xfull,
                                                        const double* __restrict__ u, double* __restrict__ z,
                                                        double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
                                                        int* __restrict__ queue, int refill,
-                                                       unsigned long long* __restrict__ stats) {
+                                                       unsigned long long* __restrict__ stats, int margin = 0) {
     if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
     unsigned trips = 0, refills = 0;
     __shared__ unsigned hist[101];   // diagnostics only: per-block histogram, flushed at the end
@@ -273,6 +280,10 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     // wave pays the gathers' latency once per refill instead of on every trip in which some
     // lane finishes
     bool active = false, pending = false, exhausted = false;
+    // CHUNK: the wave's claimed, unstarted range [p0, p1); nxv = lane 0's last queue atomic
+    // result; ahead = a 64-chunk claim is in flight; qpos = the last queue position seen
+    int p0 = 0, p1 = 0, nxv = 0, qpos = 0;
+    bool ahead = false;
     auto finalize = [&]() {
 #pragma unroll
         for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * g.count + e] = x[i];
@@ -292,15 +303,47 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
         if (mask && (__popcll(mask) >= refill || !__any(active))) {
             ++refills;
             const int leader = __ffsll((long long)mask) - 1;
-            int b = 0;
-            if (lane == leader) b = atomicAdd(queue, __popcll(mask));
+            const int k = __popcll(mask), rank = __popcll(mask & ((1ull << lane) - 1ull));
+            int b = 0, my = 0;
+            if constexpr (CHUNK == 0) {
+                if (lane == leader) b = atomicAdd(queue, k);
+            } else if (!ahead && qpos + 64 <= g.count - margin) {   // the next chunk, ahead of need
+                // (issued before the finalize, like CHUNK = 0's claim, so its round trip hides
+                // under the finalize's gathers when this refill already needs it)
+                if (lane == 0) nxv = atomicAdd(queue, 64);
+                ahead = true;
+            }
             if (pending) {
                 finalize();
                 pending = false;
             }
-            b = __shfl(b, leader, 64);
+            if constexpr (CHUNK == 0) {
+                b = __shfl(b, leader, 64);
+                my = b + rank;
+            } else {
+                // exec is full here (the refill test is wave-uniform, all lanes stay in the loop
+                // until the wave breaks), so lane 0 issues the claims and readfirstlane reads it
+                const int avail = p1 - p0;
+                if (avail >= k) {
+                    my = p0 + rank;
+                    p0 += k;
+                } else {
+                    int hi;
+                    if (ahead) {   // the chunk claimed a refill ago: 64 more
+                        hi = __builtin_amdgcn_readfirstlane(nxv);
+                        p1 = hi + 64;
+                    } else {       // first refill, or the tail: claim exactly what is missing, now
+                        if (lane == 0) nxv = atomicAdd(queue, k - avail);
+                        hi = __builtin_amdgcn_readfirstlane(nxv);
+                        p1 = hi + (k - avail);
+                    }
+                    my = rank < avail ? p0 + rank : hi + (rank - avail);
+                    p0 = hi + (k - avail);
+                    qpos = hi;
+                    ahead = false;
+                }
+            }
             if (need) {
-                const int my = b + __popcll(mask & ((1ull << lane) - 1ull));
                 if (my >= g.count) {
                     exhausted = true;
                 } else {
@@ -1627,7 +1670,10 @@ LocalQueue make_local_queue(int device, int* counter) {
     const char* sp = std::getenv("AA_LQ_SPLIT");
     q.split = sp ? sp[0] == '1' : false;
     if (q.split) q.ahead = false, q.hist = LQ_HIST_REGS;
-    const void* kq = q.split ? (const void*)k_local_z_hq2<4>
+    const char* ck = std::getenv("AA_LQ_CHUNK");
+    q.chunk = ck && ck[0] == '1' && !q.split && !q.ahead && q.hist == LQ_HIST_REGS;
+    const void* kq = q.chunk ? (const void*)k_local_z_hq<4, LQ_HIST_REGS, 1>
+                   : q.split ? (const void*)k_local_z_hq2<4>
                    : q.ahead ? (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hqa<4, LQ_HIST_YLDS>
                                                        : (const void*)k_local_z_hqa<4, LQ_HIST_REGS>)
                              : (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hq<4, LQ_HIST_YLDS>
@@ -1664,6 +1710,9 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
         else if (queue->ahead)
             hipLaunchKernelGGL((k_local_z_hqa<4, LQ_HIST_REGS>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
                                ctrl, queue->counter, refill, queue->margin, queue->stats);
+        else if (queue->chunk)
+            hipLaunchKernelGGL((k_local_z_hq<4, LQ_HIST_REGS, 1>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf,
+                               mode, ctrl, queue->counter, refill, queue->stats, queue->margin);
         else if (queue->hist == LQ_HIST_YLDS)
             hipLaunchKernelGGL((k_local_z_hq<4, LQ_HIST_YLDS>), grid, dim3(kBlock), lds, s, g, xfull, u, z, y, nf, mode,
                                ctrl, queue->counter, refill, queue->stats);

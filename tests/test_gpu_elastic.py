@@ -285,6 +285,24 @@ def test_gpu_local_queue_lds_history_bit_identical(pkg, ctx, monkeypatch, ahead)
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
 
 
+@pytest.mark.parametrize("margin", ["0", "0.05"])
+def test_gpu_local_queue_chunked_claim_bit_identical(pkg, ctx, monkeypatch, margin):
+    """The work queue with 64-element chunks claimed one ahead (AA_LQ_CHUNK=1, opt-in) against the
+    per-refill claim: each element is still solved by one lane with the same operations
+    (TetEnergyTerm.cpp:151-162), only which lane and when differ, so bit-identical trajectories.
+    AA_LQ_MARGIN=0 runs the claim-ahead path to the queue's end; 0.05 of the resident lanes
+    switches to exact claims for the tail."""
+    sc = scenes.tet_drop(16, 6, 8, iters=30, n_steps=2)
+    monkeypatch.setenv("AA_LQ_MARGIN", margin)
+    monkeypatch.setenv("AA_LQ_CHUNK", "0")
+    base, _ = pkg.capi.run_scene(ctx, sc)
+    monkeypatch.setenv("AA_LQ_CHUNK", "1")
+    chunk, _ = pkg.capi.run_scene(ctx, sc)
+    for a, b in zip(base, chunk):
+        for k in ("prim", "comb", "reject", "x", "v"):
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+
+
 def test_gpu_element_tables(pkg, ctx):
     """The device prox functions and the Anderson COD solve on the reference's own element
     tables (elements.npz, made by oracle/_ref/ref_element from TetEnergyTerm.cpp:74-96,151-162,
