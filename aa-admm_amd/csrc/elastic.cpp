@@ -601,7 +601,13 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     lzq_.alloc(1);
     if (const char* q = std::getenv("AA_LOCAL_QUEUE")) use_queue_ = q[0] != '0';
     lq_ = make_local_queue(ctx_->device, lzq_.p);
-    if (conc_) lq2_ = make_local_queue(ctx_->device, lzq2_.p);
+    if (conc_) {
+        lq2_ = make_local_queue(ctx_->device, lzq2_.p);
+        // the concurrent pass keeps the plain refill: at 402 registers a wave leaves room on its
+        // SIMD for the Anderson kernels it runs beside; the fused refill's 452 do not (C4: the
+        // main step 25 us faster, the iteration 100 us slower with both passes fused)
+        lq2_.fused = false;
+    }
     if (const char* q = std::getenv("AA_LQ_STATS"); q && q[0] == '1') {
         lq_stats_.alloc(kLqStats);
         lq_stats_.zero(s());

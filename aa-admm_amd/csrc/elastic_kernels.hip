@@ -141,6 +141,27 @@ __device__ __forceinline__ void gather_P(const GroupDev& g, int e, const double*
 // (the element's rows of W z + C - u, Solver.cpp:105/175), vertex a of a free node receives
 // f_a = sum_c G[c][a] y_c, scattered to its node's run of slots (spos, node order); the rhs
 // kernel then streams each node's run (no coefficient array, no gathers).
+// (write_slots_pre: the same with the element's slot positions and coefficients already loaded)
+template <int NV>
+__device__ __forceinline__ void write_slots_pre(const int* pos, const double* gk, double w, const double* zz,
+                                                const double* Cp, const double* uu, double* __restrict__ y) {
+    constexpr int NC = ncol_of(NV);
+    double yc[3 * NC];
+#pragma unroll
+    for (int i = 0; i < 3 * NC; ++i) yc[i] = w * (w * zz[i] - w * Cp[i] - uu[i]);
+#pragma unroll
+    for (int a = 0; a < NV; ++a) {
+        if (pos[a] < 0) continue;   // pinned: no rhs row
+        double f0 = 0, f1 = 0, f2 = 0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const double gc = gk[c * NV + a];
+            f0 += gc * yc[3 * c]; f1 += gc * yc[3 * c + 1]; f2 += gc * yc[3 * c + 2];
+        }
+        double* o = y + 3 * (size_t)pos[a];
+        o[0] = f0; o[1] = f1; o[2] = f2;
+    }
+}
 template <int NV>
 __device__ __forceinline__ void write_slots(const GroupDev& g, int e, int nf, double w, const double* zz,
                                             const double* Cp, const double* uu, double* __restrict__ y) {
@@ -240,6 +261,16 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
 // HV: where the L-BFGS history lives -- LQ_HIST_REGS (default): all of it in registers
 // (dev::HyperLbfgs); LQ_HIST_YLDS: the y half in LDS (dev::HyperLbfgsLds, dynamic LDS kLqLdsBytes,
 // AA_LQ_LDS=1; measured slower). Bit-identical.
+// the work queue's claim. The address offset comes from an opaque VGPR so the compiler's
+// wave-aggregation rewrite of a uniform-address atomic does not apply: that rewrite reads the
+// result back (readfirstlane) inside the leader's branch, i.e. waits for the atomic's round trip
+// at once, before the finished elements' stores and loads that it could overlap
+__device__ __forceinline__ int queue_claim(int* queue, int n) {
+    int off;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(off));
+    return atomicAdd(queue + off, n);
+}
+
 template <int HV>
 struct LqHist {
     using type = typename std::conditional<HV == LQ_HIST_YLDS, dev::HyperLbfgsLds, dev::HyperLbfgs>::type;
@@ -282,8 +313,11 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
     bool active = false, pending = false, exhausted = false;
     // CHUNK: the wave's claimed, unstarted range [p0, p1); nxv = lane 0's last queue atomic
     // result; ahead = a 64-chunk claim is in flight; qpos = the last queue position seen
-    int p0 = 0, p1 = 0, nxv = 0, qpos = 0;
-    bool ahead = false;
+    // (nxs: nxv read back at the end of the refill that issued it -- a wait there costs nothing, the
+    // refill's later gathers have returned; a read at the next refill would wait for that refill's
+    // finalize stores too, the vector memory counter being in order)
+    int p0 = 0, p1 = 0, nxv = 0, nxs = 0, qpos = 0;
+    bool ahead = false, fresh = false;
     auto finalize = [&]() {
 #pragma unroll
         for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * g.count + e] = x[i];
@@ -306,12 +340,13 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
             const int k = __popcll(mask), rank = __popcll(mask & ((1ull << lane) - 1ull));
             int b = 0, my = 0;
             if constexpr (CHUNK == 0) {
-                if (lane == leader) b = atomicAdd(queue, k);
+                if (lane == leader) b = queue_claim(queue, k);
             } else if (!ahead && qpos + 64 <= g.count - margin) {   // the next chunk, ahead of need
                 // (issued before the finalize, like CHUNK = 0's claim, so its round trip hides
                 // under the finalize's gathers when this refill already needs it)
                 if (lane == 0) nxv = atomicAdd(queue, 64);
                 ahead = true;
+                fresh = true;
             }
             if (pending) {
                 finalize();
@@ -329,8 +364,8 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
                     p0 += k;
                 } else {
                     int hi;
-                    if (ahead) {   // the chunk claimed a refill ago: 64 more
-                        hi = __builtin_amdgcn_readfirstlane(nxv);
+                    if (ahead) {   // the chunk claimed ahead: 64 more
+                        hi = fresh ? __builtin_amdgcn_readfirstlane(nxv) : nxs;
                         p1 = hi + 64;
                     } else {       // first refill, or the tail: claim exactly what is missing, now
                         if (lane == 0) nxv = atomicAdd(queue, k - avail);
@@ -341,6 +376,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
                     p0 = hi + (k - avail);
                     qpos = hi;
                     ahead = false;
+                    fresh = false;
                 }
             }
             if (need) {
@@ -361,6 +397,149 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
                     vol = g.vol[e];
                     if (L.start(g.mat, g.mu, g.lambda, g.k, vol, v, x)) {
                         finalize();
+                        if (stats) atomicAdd(&hist[0], 1u);
+                    } else {
+                        active = true;
+                    }
+                }
+            }
+            if constexpr (CHUNK != 0) {
+                if (fresh) {   // claimed at this refill, not used yet: read it back now
+                    nxs = __builtin_amdgcn_readfirstlane(nxv);
+                    fresh = false;
+                }
+            }
+        }
+        if (active && L.iterate(g.mat, g.mu, g.lambda, g.k, vol, v, x, &fail)) {
+            active = false;
+            pending = true;
+            if (stats) atomicAdd(&hist[min(L.k_it, 100)], 1u);
+        }
+    }
+    if (stats) {
+        if (lane == 0) {
+            atomicAdd(stats + 101, (unsigned long long)trips);
+            atomicAdd(stats + 102, (unsigned long long)refills);
+            atomicAdd(stats + 103, 1ull);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 101; i += blockDim.x)
+            if (hist[i]) atomicAdd(stats + i, (unsigned long long)hist[i]);
+    }
+    if (fail && ctrl) ctrl->fail = 1;
+}
+
+// k_local_z_hq with the refill's loads regrouped (the default for the main local step; AA_LQ_FUSED=0
+// the plain refill; groups with pinned nodes keep it -- their Cp needs the finished element's
+// positions). The plain refill is a chain of dependent round trips: the finished element's node
+// ids, its positions (for Cp, 0 without pins), then its slot positions, then the new element's
+// node ids and positions (tools/isa_serial.py; 27 % of the wave's cycles parked on s_waitcnt). Here
+// the loads go out in three groups, unconditionally for every lane (indices clamped; a lane without
+// a finished or a new element loads valid data it does not use, so no branch splits a group):
+// the queue claim with the finished element's coefficients, u, w and slot positions; the new
+// element's node ids, with the finished element's stores issued while they are in flight; the new
+// element's positions, coefficients, u, w and vol. A start point that already passes the gradient
+// test leaves its element pending (written at the next refill) instead of writing it at once.
+// Same arithmetic in the same order: bit-identical. 452 registers (one wave per SIMD, as the
+// plain kernel's 402) -- too many to leave the Anderson kernels room beside it, so the concurrent
+// combined-residual pass keeps the plain refill (ElasticSolver::initialize). C4 (same box, two A/B
+// pairs): local_z 433 / 435 -> 422 / 418 us.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_local_z_hqf(GroupDev g, const double* __restrict__ xfull,
+                                                        const double* __restrict__ u, double* __restrict__ z,
+                                                        double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
+                                                        int* __restrict__ queue, int refill,
+                                                        unsigned long long* __restrict__ stats) {
+    static_assert(NV == 4, "the fused refill is for tets");
+    if (mode != LZ_INIT && gated(ctrl, mode == LZ_REDO)) return;
+    unsigned trips = 0, refills = 0;
+    __shared__ unsigned hist[101];
+    if (stats) {
+        for (int i = threadIdx.x; i < 101; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+    }
+    constexpr int NC = ncol_of(NV), D = 3 * NC;
+    const int lane = threadIdx.x & 63;
+    dev::HyperLbfgs L;
+    double v[D], x[D];
+    double vol = 0;
+    int e = 0, fail = 0;
+    bool active = false, pending = false, exhausted = false;
+    const size_t n = g.count;
+    for (;;) {
+        const bool need = !active && !exhausted;
+        const unsigned long long mask = __ballot(need);
+        if (!__any(active || need)) break;
+        ++trips;
+        if (mask && (__popcll(mask) >= refill || !__any(active))) {
+            ++refills;
+            const int leader = __ffsll((long long)mask) - 1;
+            const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+            int b = 0;
+            if (lane == leader) b = queue_claim(queue, __popcll(mask));
+            // the finished element's slot data (every lane: e is a valid element or 0)
+            int so[NV];
+            double go[NC * NV], uo[D], wo = 1.0;
+            if (y) {   // kernel-uniform
+#pragma unroll
+                for (int a = 0; a < NV; ++a) so[a] = g.spos[a * n + e];
+#pragma unroll
+                for (int k = 0; k < NC * NV; ++k) go[k] = g.G[k * n + e];
+                load_u<D>(g, e, u, uo);
+                wo = g.w[e];
+            }
+            b = __shfl(b, leader, 64);
+            const int my = b + rank;
+            const int en = min(my, g.count - 1);
+            int id[NV];   // the new element's node ids first: its positions wait on them
+#pragma unroll
+            for (int a = 0; a < NV; ++a) id[a] = g.idx[a * n + en];
+            if (pending) {   // the finished element's outputs while the ids are in flight
+#pragma unroll
+                for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * n + e] = x[i];
+                if (y) {
+                    double Cp[D];
+#pragma unroll
+                    for (int i = 0; i < D; ++i) Cp[i] = 0;
+                    write_slots_pre<NV>(so, go, wo, x, Cp, uo, y);
+                }
+                pending = false;
+            }
+            double xp[3 * NV], gn[NC * NV], un[D];
+#pragma unroll
+            for (int a = 0; a < NV; ++a) {
+                xp[3 * a] = xfull[3 * (size_t)id[a]];
+                xp[3 * a + 1] = xfull[3 * (size_t)id[a] + 1];
+                xp[3 * a + 2] = xfull[3 * (size_t)id[a] + 2];
+            }
+#pragma unroll
+            for (int k = 0; k < NC * NV; ++k) gn[k] = g.G[k * n + en];
+            load_u<D>(g, en, u, un);
+            const double wn = g.w[en], voln = g.vol[en];
+            if (need) {
+                if (my >= g.count) {
+                    exhausted = true;
+                } else {
+                    e = my;
+                    double F[D];   // gather_F's sums, in its order
+#pragma unroll
+                    for (int i = 0; i < D; ++i) F[i] = 0;
+#pragma unroll
+                    for (int a = 0; a < NV; ++a)
+#pragma unroll
+                        for (int c = 0; c < NC; ++c) {
+                            const double gc = gn[c * NV + a];
+                            F[3 * c + 0] += gc * xp[3 * a]; F[3 * c + 1] += gc * xp[3 * a + 1];
+                            F[3 * c + 2] += gc * xp[3 * a + 2];
+                        }
+#pragma unroll
+                    for (int i = 0; i < D; ++i) {
+                        v[i] = F[i] + un[i] / wn;
+                        x[i] = v[i];
+                    }
+                    vol = voln;
+                    if (L.start(g.mat, g.mu, g.lambda, g.k, vol, v, x)) {
+                        pending = true;
                         if (stats) atomicAdd(&hist[0], 1u);
                     } else {
                         active = true;
@@ -1672,7 +1851,11 @@ LocalQueue make_local_queue(int device, int* counter) {
     if (q.split) q.ahead = false, q.hist = LQ_HIST_REGS;
     const char* ck = std::getenv("AA_LQ_CHUNK");
     q.chunk = ck && ck[0] == '1' && !q.split && !q.ahead && q.hist == LQ_HIST_REGS;
-    const void* kq = q.chunk ? (const void*)k_local_z_hq<4, LQ_HIST_REGS, 1>
+    const char* fu = std::getenv("AA_LQ_FUSED");
+    // default on (AA_LQ_FUSED=0: the plain refill); the caller turns it off for the concurrent pass
+    q.fused = (fu ? fu[0] == '1' : true) && !q.split && !q.ahead && !q.chunk && q.hist == LQ_HIST_REGS;
+    const void* kq = q.fused ? (const void*)k_local_z_hqf<4>
+                   : q.chunk ? (const void*)k_local_z_hq<4, LQ_HIST_REGS, 1>
                    : q.split ? (const void*)k_local_z_hq2<4>
                    : q.ahead ? (q.hist == LQ_HIST_YLDS ? (const void*)k_local_z_hqa<4, LQ_HIST_YLDS>
                                                        : (const void*)k_local_z_hqa<4, LQ_HIST_REGS>)
@@ -1710,6 +1893,9 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
         else if (queue->ahead)
             hipLaunchKernelGGL((k_local_z_hqa<4, LQ_HIST_REGS>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
                                ctrl, queue->counter, refill, queue->margin, queue->stats);
+        else if (queue->fused && !g.pinned)   // pinned groups keep the plain refill (their Cp needs positions)
+            hipLaunchKernelGGL((k_local_z_hqf<4>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode, ctrl,
+                               queue->counter, refill, queue->stats);
         else if (queue->chunk)
             hipLaunchKernelGGL((k_local_z_hq<4, LQ_HIST_REGS, 1>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf,
                                mode, ctrl, queue->counter, refill, queue->stats, queue->margin);

@@ -78,6 +78,7 @@ struct LocalQueue {
     int resident = 0, refill = 60, margin = 0;
     bool ahead = false;  // AA_LQ_AHEAD=1: k_local_z_hqa (one-element lookahead per lane)
     bool split = false;  // AA_LQ_SPLIT=1: k_local_z_hq2 (each element's L-BFGS over a lane pair)
+    bool fused = false;  // AA_LQ_FUSED=1: k_local_z_hqf (the refill's loads regrouped; groups without pins)
     bool chunk = false;  // AA_LQ_CHUNK=1: k_local_z_hq<4, REGS, 1> (64-element chunks claimed one ahead)
     int hist = 0;        // LqHistory: where the L-BFGS history lives (AA_LQ_LDS=1: y half in LDS)
     size_t lds_bytes = 0;

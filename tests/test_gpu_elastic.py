@@ -285,6 +285,26 @@ def test_gpu_local_queue_lds_history_bit_identical(pkg, ctx, monkeypatch, ahead)
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
 
 
+@pytest.mark.parametrize("scene", ["drop_x", "drop_h", "cantilever_pinned"])
+def test_gpu_local_queue_fused_refill_bit_identical(pkg, ctx, monkeypatch, scene):
+    """The default work queue's refill with its loads regrouped (k_local_z_hqf) against the plain
+    refill (AA_LQ_FUSED=0): each element's L-BFGS (TetEnergyTerm.cpp:151-162) and its outputs --
+    z and the rhs slots w (w z - u) (Solver.cpp:105/175) -- are the same operations in the same
+    order, so bit-identical trajectories; a pinned group (the cantilever) keeps the plain refill."""
+    if scene == "cantilever_pinned":
+        sc = scenes.cantilever(12, 3, 3, iters=30, n_steps=2)
+    else:
+        sc = scenes.tet_drop(16, 6, 8, iters=30, n_steps=2,
+                             variant=scenes.VARIANT_X if scene == "drop_x" else scenes.VARIANT_H)
+    monkeypatch.setenv("AA_LQ_FUSED", "0")
+    base, _ = pkg.capi.run_scene(ctx, sc)
+    monkeypatch.setenv("AA_LQ_FUSED", "1")
+    fused, _ = pkg.capi.run_scene(ctx, sc)
+    for a, b in zip(base, fused):
+        for k in ("prim", "comb", "reject", "x", "v"):
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+
+
 @pytest.mark.parametrize("margin", ["0", "0.05"])
 def test_gpu_local_queue_chunked_claim_bit_identical(pkg, ctx, monkeypatch, margin):
     """The work queue with 64-element chunks claimed one ahead (AA_LQ_CHUNK=1, opt-in) against the
