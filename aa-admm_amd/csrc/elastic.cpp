@@ -584,7 +584,8 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     if (conc_) {
         du2_.alloc(Z_); dz2_.alloc(Z_); dx2_.alloc(3 * (size_t)nf_);
         ctrl_c_.alloc(1);
-        lzq2_.alloc(1);
+        lzq2_.alloc(2);   // claim counter, finished blocks (queue_reset_last)
+        AA_HIP(hipMemset(lzq2_.p, 0, 2 * sizeof(int)));
         if (!side_) AA_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
         if (!ev_fork_) AA_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
         if (!ev_join_) AA_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
@@ -598,7 +599,8 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     if (comm_) { red_gab_.alloc(2 * (size_t)nbg_); red_gab_.zero(s()); ga_ = red_gab_.p; gb_ = red_gab_.p + nbg_; }
     else { ga_ = pa_; gb_ = pb_; }
     ctrl_.alloc(1);
-    lzq_.alloc(1);
+    lzq_.alloc(2);   // claim counter, finished blocks (queue_reset_last)
+    AA_HIP(hipMemset(lzq_.p, 0, 2 * sizeof(int)));
     if (const char* q = std::getenv("AA_LOCAL_QUEUE")) use_queue_ = q[0] != '0';
     lq_ = make_local_queue(ctx_->device, lzq_.p);
     if (conc_) {

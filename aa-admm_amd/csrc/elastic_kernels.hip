@@ -261,6 +261,21 @@ __global__ __launch_bounds__(kBlock) void k_local_z(GroupDev g, const double* __
 // HV: where the L-BFGS history lives -- LQ_HIST_REGS (default): all of it in registers
 // (dev::HyperLbfgs); LQ_HIST_YLDS: the y half in LDS (dev::HyperLbfgsLds, dynamic LDS kLqLdsBytes,
 // AA_LQ_LDS=1; measured slower). Bit-identical.
+// end of a work-queue launch: the last block to finish resets the queue -- claim counter
+// queue[0], finished blocks queue[1] -- for the next launch, which follows a kernel boundary; this
+// replaces a memset node (a fill kernel and its dependency gap) before every launch. A gated
+// launch returns before claiming and leaves both at 0.
+__device__ __forceinline__ void queue_reset_last(int* queue) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned d = atomicAdd(reinterpret_cast<unsigned*>(queue + 1), 1u);
+        if (d == gridDim.x - 1) {
+            atomicExch(queue, 0);
+            atomicExch(queue + 1, 0);
+        }
+    }
+}
+
 // the work queue's claim. The address offset comes from an opaque VGPR so the compiler's
 // wave-aggregation rewrite of a uniform-address atomic does not apply: that rewrite reads the
 // result back (readfirstlane) inside the leader's branch, i.e. waits for the atomic's round trip
@@ -427,6 +442,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
             if (hist[i]) atomicAdd(stats + i, (unsigned long long)hist[i]);
     }
     if (fail && ctrl) ctrl->fail = 1;
+    queue_reset_last(queue);
 }
 
 // k_local_z_hq with the refill's loads regrouped (the default for the main local step; AA_LQ_FUSED=0
@@ -564,6 +580,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hqf(GroupDev g, const double
             if (hist[i]) atomicAdd(stats + i, (unsigned long long)hist[i]);
     }
     if (fail && ctrl) ctrl->fail = 1;
+    queue_reset_last(queue);
 }
 
 // k_local_z_hq with each element's L-BFGS split over a lane pair (dev::HyperLbfgs2, AA_LQ_SPLIT=1,
@@ -1879,7 +1896,8 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
     if (g.count == 0) return;
     const int nb = blocks_for(g.count);
     if (g.kind == 0 && g.mat != 0 && !red && queue && queue->counter) {   // hyperelastic, no partials: work queue
-        AA_HIP(hipMemsetAsync(queue->counter, 0, sizeof(int), s));
+        // k_local_z_hq / k_local_z_hqf reset the queue themselves (queue_reset_last)
+        if (queue->split || queue->ahead) AA_HIP(hipMemsetAsync(queue->counter, 0, sizeof(int), s));
         const int resident = std::max(1, queue->resident), refill = queue->refill;
         const dim3 grid(std::min(nb, resident));
         const size_t lds = queue->lds_bytes;
