@@ -923,12 +923,11 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
     prim_all(xfull_.p, z_.p, nullptr, 0);
     ev_end("prim");
     reduce_partials();
-    launch_control(CTL_PRIM_CHECK_Z, c, ga_, nullptr, nbg_, accel, hist_prim_.p, hist_comb_.p, hist_rej_.p, s());
+    // the reject test with the restore of the defaults fused (gated on the device: copies only
+    // when prim increased)
+    launch_check_restore_z(c, ga_, nbg_, accel, u_.p, xfull_.p, z_.p, dup, dxp, dzp, Z_, nx, s());
     if (accel) {   // reject branch (gated on the device; a no-op unless prim increased)
         ev_begin("reject");
-        launch_copy(u_.p, dup, Z_, c, 1, s());
-        launch_copy(xfull_.p, dxp, nx, c, 1, s());
-        launch_copy(z_.p, dzp, Z_, c, 1, s());
         // accelerator.replace(curr_z): the accelerator's iterate is z_ (restored above)
         for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, 0, 1, c, s());
         launch_rhs(nf_, dt_ptr_.p, nullptr, nullptr, y_.p, Mxbar_.p, pdt2_, b_.p, c, 1, s());

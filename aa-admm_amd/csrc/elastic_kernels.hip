@@ -1253,6 +1253,41 @@ __global__ __launch_bounds__(kBlock) void k_check_restore_ux(Ctrl* ctrl, const d
     }
 }
 
+// Z reject test (Solver.cpp:159-168, k_control CTL_PRIM_CHECK_Z) fused with the restore of the
+// defaults (u, x, z = default_{u,x,z} of the previous iteration, Solver.cpp:170-176): one launch
+// instead of the control kernel and three gated copies. Every block sums the prim partials itself
+// with k_control's 1024-thread order (the same bits, so the same decision); block 0 records it.
+__global__ __launch_bounds__(kCtlBlock) void k_check_restore_z(Ctrl* ctrl, const double* __restrict__ red, int nb,
+                                                               int accel, double* __restrict__ u,
+                                                               double* __restrict__ x, double* __restrict__ z,
+                                                               const double* __restrict__ du,
+                                                               const double* __restrict__ dx,
+                                                               const double* __restrict__ dz, long long nz,
+                                                               long long nx) {
+    if (ctrl->done) return;
+    __shared__ double sm[kCtlBlock / 64];
+    double a = thread_sum_strided(red, nb);
+    a = block_sum(a, sm);   // thread 0 holds k_control's sum
+    __shared__ int rej;
+    if (threadIdx.x == 0) {
+        const double prim = sqrt(a);
+        rej = (accel && ctrl->prev_prim < prim) ? 1 : 0;
+        if (blockIdx.x == 0) {
+            ctrl->prim = prim;
+            ctrl->reject = rej;
+            if (rej) ctrl->nrej += 1;
+        }
+    }
+    __syncthreads();
+    if (!rej) return;
+    const long long n = 2 * nz + nx;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        if (i < nz) u[i] = du[i];
+        else if (i < nz + nx) x[i - nz] = dx[i - nz];
+        else z[i - nz - nx] = dz[i - nz - nx];
+    }
+}
+
 // UX reject (Solver.cpp:150-154): (u, x) = defaults and accelerator->reset(u, x) stores them
 __global__ __launch_bounds__(kBlock) void k_restore_ux(double* __restrict__ u, double* __restrict__ x,
                                                        double* __restrict__ cur, const double* __restrict__ du,
@@ -2096,6 +2131,16 @@ void launch_check_restore_ux(Ctrl* ctrl, const double* red, int nb, int accel, d
                              const double* du, const double* dx, long long nz, long long nx, hipStream_t s) {
     const int grid = accel ? grid_for(nz + nx) : 1;
     hipLaunchKernelGGL(k_check_restore_ux, dim3(grid), dim3(kBlock), 0, s, ctrl, red, nb, accel, u, x, cur, du, dx, nz, nx);
+    AA_CHECK_LAUNCH();
+}
+
+void launch_check_restore_z(Ctrl* ctrl, const double* red, int nb, int accel, double* u, double* x, double* z,
+                            const double* du, const double* dx, const double* dz, long long nz, long long nx,
+                            hipStream_t s) {
+    // 512 blocks: each sums the ~4k partials (L2 hits) before its share of the copy
+    const int grid = accel ? 512 : 1;
+    hipLaunchKernelGGL(k_check_restore_z, dim3(grid), dim3(kCtlBlock), 0, s, ctrl, red, nb, accel, u, x, z, du, dx, dz,
+                       nz, nx);
     AA_CHECK_LAUNCH();
 }
 

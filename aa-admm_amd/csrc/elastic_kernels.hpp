@@ -111,6 +111,10 @@ void launch_rhs(int nf, const int* ptr, const int* row, const double* val, const
                 const double* xsrc = nullptr, double* xlast = nullptr, const double* red_final = nullptr,
                 int nb_final = 0);
 // UX reject test + restore fused (replaces CTL_PRIM_CHECK + launch_restore_ux)
+// Z variant: k_control's CTL_PRIM_CHECK_Z and the reject branch's three restores in one launch
+void launch_check_restore_z(Ctrl* ctrl, const double* red, int nb, int accel, double* u, double* x, double* z,
+                            const double* du, const double* dx, const double* dz, long long nz, long long nx,
+                            hipStream_t s);
 void launch_check_restore_ux(Ctrl* ctrl, const double* red, int nb, int accel, double* u, double* x, double* cur,
                              const double* du, const double* dx, long long nz, long long nx, hipStream_t s);
 // UX reject: u = du, x = dx, cur = (du, dx) (gate: reject)
