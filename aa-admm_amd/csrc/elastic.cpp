@@ -889,6 +889,26 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
     // (per-kernel-class timing) pass
     const bool side = pipe && it > 0 && conc_;
     hipStream_t sst = instrument_ ? s() : side_;
+    // k-1's pass beside this iteration's work: its local step (one wave per SIMD) leaves room for
+    // memory-bound waves beside it. Where it forks (AA_CONC_FORK, same-box A/B on C4): after the
+    // local step (0) 412 / 412 it/s, after the Anderson reduce (1: the reduce then streams at full
+    // occupancy) 415 / 419, after the mix (2) 393 / 396, in line 399 / 400; right after the
+    // two-set solve (-1: the pass's local step would fill the GPU while this iteration's prim check
+    // and gated reject branch -- ~20 launches that exit at once, ~110 us -- go by) 404 / 404 against
+    // 426 / 423: the Anderson step then runs alone, and that overlap was worth more)
+    // (the instrumented pass runs it in line before the Anderson step, outside its timing bracket)
+    auto fork_side = [&](int at) {
+        if (!side || at != (instrument_ ? 0 : conc_fork_)) return;
+        if (sst != s()) {
+            AA_HIP(hipEventRecord(ev_fork_, s()));
+            AA_HIP(hipStreamWaitEvent(sst, ev_fork_, 0));
+        }
+        if (sst == s()) ev_begin("comb");
+        comb_finish_z(CTL_COMB_ZP, sst, ctrl_c_.p, red_c_.p, red_c_.p + nbg_, &lq2_, dup, dzp);
+        if (sst == s()) ev_end("comb");
+        if (sst != s()) AA_HIP(hipEventRecord(ev_join_, sst));
+        join_wait_ = sst != s();
+    };
     ev_begin("grad");
     for (auto& g : groups_) launch_u_and_y(g.d, xfull_.p, z_.p, u_.p, y_.p, nf_, accel ? 1 : 0, 0, c, s());
     ev_end("grad");
@@ -901,6 +921,7 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         ev_end("solve");
         if (side) {   // the pass's control block: k-1's prim / reject, before this iteration's
             launch_ctrl_fork(c, ctrl_c_.p, s());   // check; its nrej / fail for a rollback
+            fork_side(-1);
         } else {
             ev_begin("comb");
             comb_finish_z(CTL_COMB_ZP, s(), c, pa_, pb_, &lq_, dup, dzp);
@@ -955,25 +976,6 @@ void ElasticSolver::enqueue_iteration_z(bool accel, int it) {
         ev_begin("local_z");
         local_z_all(xfull_.p, u_.p, dzc, y_.p, LZ_NORMAL, false);
         ev_end("local_z");
-        // k-1's pass beside this iteration's Anderson step and comb rhs: its local step (one
-        // wave per SIMD) leaves room for their memory-bound waves (the two local steps cannot
-        // share a SIMD, so the fork comes after this iteration's local step). Where exactly
-        // (AA_CONC_FORK, same-box A/B on C4): after the local step (0) 412 / 412 it/s, after the
-        // Anderson reduce (1, default: the reduce then streams at full occupancy) 415 / 419,
-        // after the mix (2) 393 / 396, in line 399 / 400
-        // (the instrumented pass runs it in line before the Anderson step, outside its timing bracket)
-        auto fork_side = [&](int at) {
-            if (!side || at != (instrument_ ? 0 : conc_fork_)) return;
-            if (sst != s()) {
-                AA_HIP(hipEventRecord(ev_fork_, s()));
-                AA_HIP(hipStreamWaitEvent(sst, ev_fork_, 0));
-            }
-            if (sst == s()) ev_begin("comb");
-            comb_finish_z(CTL_COMB_ZP, sst, ctrl_c_.p, red_c_.p, red_c_.p + nbg_, &lq2_, dup, dzp);
-            if (sst == s()) ev_end("comb");
-            if (sst != s()) AA_HIP(hipEventRecord(ev_join_, sst));
-            join_wait_ = sst != s();
-        };
         fork_side(0);
         Seg2 G{dzc, Z_, nullptr, 0};
         Seg2 out{z_.p, Z_, nullptr, 0};
