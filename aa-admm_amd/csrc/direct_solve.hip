@@ -1762,12 +1762,18 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
     {
         const char* st = std::getenv("AA_SOLVE_STREAM");
         stream_ = packed_ && st && st[0] == '1';   // measured slower on C4: opt-in
+        // a gated solve that is skipped (the Anderson reject path's, most iterations) costs one
+        // dependent launch (~4.6 us in a graph) per level: its tile runs as one launch each cut
+        // that; taken, a streamed run is slower than its levels
+        const char* sg = std::getenv("AA_SOLVE_STREAM_GATED");
+        stream_gated_ = packed_ && !node_part && (sg ? sg[0] == '1' : true);   // (one GPU)
     }
+    stream_plan_ = stream_ || stream_gated_;
     fstreams_.clear();
     bstreams_.clear();
     std::vector<int> forder, border, bndx(bnd.size(), -1);
     long long xs_rows = 0;
-    if (stream_) {
+    if (stream_plan_) {
         const int nL = (int)levels_.size();
         auto runs = [&](bool fwd) {
             std::vector<std::pair<int, int>> r;
@@ -1862,9 +1868,9 @@ void DirectSolver::build(const SupernodalFactor& F, hipStream_t s, const std::ve
         if (stats)
             for (auto& S : bstreams_)
                 std::fprintf(stderr, "[solve] streamed backward levels [%d, %d): %d tiles, one launch\n", S.l0, S.l1, S.count);
-        if (fstreams_.empty() && bstreams_.empty()) stream_ = false;
+        if (fstreams_.empty() && bstreams_.empty()) stream_ = stream_gated_ = stream_plan_ = false;
     }
-    if (stream_) {
+    if (stream_plan_) {
         forder_.upload(forder.empty() ? std::vector<int>{0} : forder, s);
         border_.upload(border.empty() ? std::vector<int>{0} : border, s);
         bndx_.upload(bndx.empty() ? std::vector<int>{-1} : bndx, s);
@@ -2176,7 +2182,8 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     const bool clk_on = sub_timing_ > 0 && cst == hipStreamCaptureStatusNone && n_sub_ > 0;
     const int noff_f = (K * (sub_lds_f_ + sub_lds_u_) + 15) / 16 * 16, noff_b = (K * (sub_lds_b_ + sub_lds_x_) + 15) / 16 * 16;
     // queue heads and dependency counters of the streamed runs start from zero every solve
-    if (stream_) AA_HIP(hipMemsetAsync(sync_.p, 0, sizeof(int) * ((size_t)n_heads_ + 2 * (size_t)nn_), s));
+    const bool st_on = stream_plan_ && (stream_ || (gate_reject == 1 && stream_gated_));
+    if (st_on) AA_HIP(hipMemsetAsync(sync_.p, 0, sizeof(int) * ((size_t)n_heads_ + 2 * (size_t)nn_), s));
 #define SUBF(BL, T0, NT, ST) hipLaunchKernelGGL((nt_rows_ ? k_fwd_sub<BL, NR, true> : k_fwd_sub<BL, NR, false>), dim3(NT), dim3(BL), sub_lds_bytes(K, true), ST, sub_trees_.p, \
                                     sub_levels_.p, sub_nodes_.p, sub_items_.p, Gc_.p, ell_.p, b0, b1, Y_.p, U_.p, ctrl, gate_reject, \
                                     clk_on ? sub_clk_.p : nullptr, 64, noff_f, T0)
@@ -2234,7 +2241,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     size_t fs = 0;
     for (int li = 0; li < (int)levels_.size() && NB == 1; ++li) {
         const Level& L = levels_[li];
-        if (fs < fstreams_.size() && fstreams_[fs].l0 == li) {
+        if (st_on && fs < fstreams_.size() && fstreams_[fs].l0 == li) {
             launch_fstream<NR>(fstreams_[fs], b0, b1, ctrl, gate_reject, s);
             li = fstreams_[fs++].l1 - 1;
             continue;
@@ -2291,7 +2298,7 @@ void DirectSolver::solve_nr(const double* b0, double* x0, const double* b1, doub
     size_t bs = 0;
     for (int li = (int)levels_.size() - 1; li >= 0; --li) {
         const Level& L = levels_[li];
-        if (bs < bstreams_.size() && bstreams_[bs].l1 - 1 == li) {
+        if (st_on && bs < bstreams_.size() && bstreams_[bs].l1 - 1 == li) {
             launch_bstream<NR>(bstreams_[bs], x0, x1, ctrl, gate_reject, s);
             li = bstreams_[bs++].l0;
             continue;

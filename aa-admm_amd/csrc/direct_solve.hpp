@@ -200,7 +200,9 @@ private:
     // instead of waiting for its kernel boundary. Same tiles, partials and sums: bit-identical.
     struct Stream { int l0, l1, first, count, head; };   // levels [l0, l1), queue order_[first, +count)
     std::vector<Stream> fstreams_, bstreams_;
-    bool stream_ = false;
+    bool stream_ = false;        // every solve streams its tile runs (AA_SOLVE_STREAM=1)
+    bool stream_gated_ = false;  // the reject path's gated solves do (AA_SOLVE_STREAM_GATED, default on)
+    bool stream_plan_ = false;   // the runs are planned (either of the above)
     DevBuf<int> forder_, border_, bndx_;   // tile queues; per boundary entry its Xs_ row (-1: read x)
     DevBuf<int> sync_;   // [queue heads | forward counters (nn_) | backward counters (nn_)], zeroed per solve
     int n_heads_ = 0;

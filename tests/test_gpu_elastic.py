@@ -203,23 +203,29 @@ def test_gpu_z_pipelined_comb_bit_identical(builder, pkg, ctx, monkeypatch):
 def test_gpu_streamed_levels_bit_identical(pkg, ctx, monkeypatch, capfd, knobs):
     """Streamed tile levels (one launch per run of tile-only levels, tiles taken from a queue in
     level order, each waiting in-launch for its children's update vectors / its parent's x rows)
-    give bit-identical trajectories to one launch per level (AA_SOLVE_STREAM=0): same tiles,
-    partials and sums in the same order; only the scheduling differs."""
-    sc = scenes.tet_drop(40, 16, 20, iters=12, n_steps=2)
+    give bit-identical trajectories to one launch per level (AA_SOLVE_STREAM=0
+    AA_SOLVE_STREAM_GATED=0): same tiles, partials and sums in the same order; only the scheduling
+    differs -- for every solve (AA_SOLVE_STREAM=1) and for the Anderson reject path's gated
+    solves only (the default, AA_SOLVE_STREAM_GATED=1)."""
+    sc = scenes.tet_drop(20, 8, 10, iters=100, n_steps=2)   # 8 000 tets: 8 + 9 Anderson rejects
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     monkeypatch.setenv("AA_SOLVE_STATS", "1")
     monkeypatch.setenv("AA_SOLVE_STREAM", "0")
+    monkeypatch.setenv("AA_SOLVE_STREAM_GATED", "0")
     lev, _ = pkg.capi.run_scene(ctx, sc)
     capfd.readouterr()
-    monkeypatch.setenv("AA_SOLVE_STREAM", "1")
-    st, _ = pkg.capi.run_scene(ctx, sc)
-    err = capfd.readouterr().err
-    if knobs:
-        assert "streamed forward levels" in err and "streamed backward levels" in err, err[-2000:]
-    for a, b in zip(lev, st):
-        for k in ("prim", "comb", "reject", "x", "v"):
-            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (k, len(a["comb"]), len(b["comb"]))
+    assert sum(int(np.sum(h["reject"])) for h in lev) > 0   # the gated solves run
+    for stream, gated in (("1", "0"), ("0", "1")):
+        monkeypatch.setenv("AA_SOLVE_STREAM", stream)
+        monkeypatch.setenv("AA_SOLVE_STREAM_GATED", gated)
+        st, _ = pkg.capi.run_scene(ctx, sc)
+        err = capfd.readouterr().err
+        if knobs:
+            assert "streamed forward levels" in err and "streamed backward levels" in err, err[-2000:]
+        for a, b in zip(lev, st):
+            for k in ("prim", "comb", "reject", "x", "v"):
+                assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (stream, k, len(a["comb"]), len(b["comb"]))
 
 
 @pytest.mark.parametrize("knob", [("AA_SOLVE_PACKED", "0", "1"), ("AA_FACTOR_NT", "0", "1"),
@@ -373,22 +379,25 @@ def test_gpu_full_drop40_matches_reference(pkg, ctx):
     assert not fails, fails
 
 
-def test_gpu_full_c4_matches_reference(pkg, ctx):
+@pytest.mark.parametrize("fixture,n_steps", [("full_c4_block_z_nh_aa6", 1), ("full_c4_block_z_nh_aa6_2steps", 2)])
+def test_gpu_full_c4_matches_reference(pkg, ctx, fixture, n_steps):
     """BASELINE configs[3] at full size against the reference itself: make_tet_blocks(100,40,50) =
-    1 000 000 NeoHookean tets, 211 191 nodes, z-AA m=6, one time step of 10 iterations
-    (tests/golden/full_c4_block_z_nh_aa6.npz, make_golden.py --full-c4: the reference's own
-    SimplicialLDLT setup takes hours on the CPU, so the fixture holds one step). The bars of the
-    64k-tet golden: the residual curve relative to comb_0 (1e-6, L-BFGS prox path), equal reject
-    flags, positions / velocities on 512 sampled nodes and their column sums (1e-6 relative)."""
+    1 000 000 NeoHookean tets, 211 191 nodes, z-AA m=6, time steps of 10 iterations
+    (tests/golden/full_c4_block_z_nh_aa6.npz, make_golden.py --full-c4: one step;
+    full_c4_block_z_nh_aa6_2steps.npz, --full-c4-2steps: two steps, so the second starts from the
+    first's positions and velocities -- the reference's own SimplicialLDLT setup takes hours on the
+    CPU, so the fixtures are short). The bars of the 64k-tet golden: the residual curves relative
+    to comb_0 (1e-6, L-BFGS prox path), equal reject flags, positions / velocities on 512 sampled
+    nodes and their column sums (1e-6 relative), per step."""
     import sys
     from golden_io import check_full_golden
-    path = os.path.join(GOLDEN, "full_c4_block_z_nh_aa6.npz")
+    path = os.path.join(GOLDEN, fixture + ".npz")
     if not os.path.exists(path):
         pytest.skip("full-size C4 reference fixture not generated")
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
     from make_golden import scene_digest
     ref = np.load(path)
-    sc = scenes.tet_drop(100, 40, 50, iters=10, n_steps=1)
+    sc = scenes.tet_drop(100, 40, 50, iters=10, n_steps=n_steps)
     assert np.array_equal(scene_digest(sc), ref["digest"]), "regenerated scene differs from the fixture's"
     got, _ = pkg.capi.run_scene(ctx, sc)
     fails = check_full_golden(got, ref)
