@@ -608,7 +608,8 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
         // the concurrent pass keeps the plain refill: at 402 registers a wave leaves room on its
         // SIMD for the Anderson kernels it runs beside; the fused refill's 452 do not (C4: the
         // main step 25 us faster, the iteration 100 us slower with both passes fused)
-        lq2_.fused = false;
+        const char* fc = std::getenv("AA_LQ_FUSED_CONC");
+        lq2_.fused = lq2_.fused && fc && fc[0] == '1';
     }
     if (const char* q = std::getenv("AA_LQ_STATS"); q && q[0] == '1') {
         lq_stats_.alloc(kLqStats);

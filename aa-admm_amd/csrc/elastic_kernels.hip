@@ -460,7 +460,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hq(GroupDev g, const double*
 // plain kernel's 402) -- too many to leave the Anderson kernels room beside it, so the concurrent
 // combined-residual pass keeps the plain refill (ElasticSolver::initialize). C4 (same box, two A/B
 // pairs): local_z 433 / 435 -> 422 / 418 us.
-template <int NV>
+template <int NV, bool SLOTS = true>
 __global__ __launch_bounds__(kBlock) void k_local_z_hqf(GroupDev g, const double* __restrict__ xfull,
                                                         const double* __restrict__ u, double* __restrict__ z,
                                                         double* __restrict__ y, int nf, int mode, Ctrl* ctrl,
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hqf(GroupDev g, const double
             // the finished element's slot data (every lane: e is a valid element or 0)
             int so[NV];
             double go[NC * NV], uo[D], wo = 1.0;
-            if (y) {   // kernel-uniform
+            if (SLOTS && y) {   // kernel-uniform (SLOTS = false: a pass without slots, fewer live registers)
 #pragma unroll
                 for (int a = 0; a < NV; ++a) so[a] = g.spos[a * n + e];
 #pragma unroll
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(kBlock) void k_local_z_hqf(GroupDev g, const double
             if (pending) {   // the finished element's outputs while the ids are in flight
 #pragma unroll
                 for (int i = 0; i < D; ++i) z[g.zoff + (size_t)i * n + e] = x[i];
-                if (y) {
+                if (SLOTS && y) {
                     double Cp[D];
 #pragma unroll
                     for (int i = 0; i < D; ++i) Cp[i] = 0;
@@ -1947,8 +1947,12 @@ void launch_local_z(const GroupDev& g, const double* xfull, const double* u, dou
             hipLaunchKernelGGL((k_local_z_hqa<4, LQ_HIST_REGS>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
                                ctrl, queue->counter, refill, queue->margin, queue->stats);
         else if (queue->fused && !g.pinned)   // pinned groups keep the plain refill (their Cp needs positions)
-            hipLaunchKernelGGL((k_local_z_hqf<4>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode, ctrl,
-                               queue->counter, refill, queue->stats);
+        {
+            if (y) hipLaunchKernelGGL((k_local_z_hqf<4, true>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
+                                      ctrl, queue->counter, refill, queue->stats);
+            else hipLaunchKernelGGL((k_local_z_hqf<4, false>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf, mode,
+                                    ctrl, queue->counter, refill, queue->stats);
+        }
         else if (queue->chunk)
             hipLaunchKernelGGL((k_local_z_hq<4, LQ_HIST_REGS, 1>), grid, dim3(kBlock), 0, s, g, xfull, u, z, y, nf,
                                mode, ctrl, queue->counter, refill, queue->stats, queue->margin);
