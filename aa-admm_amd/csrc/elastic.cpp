@@ -605,11 +605,13 @@ void ElasticSolver::initialize(const aa_settings& s_in) {
     lq_ = make_local_queue(ctx_->device, lzq_.p);
     if (conc_) {
         lq2_ = make_local_queue(ctx_->device, lzq2_.p);
-        // the concurrent pass keeps the plain refill: at 402 registers a wave leaves room on its
-        // SIMD for the Anderson kernels it runs beside; the fused refill's 452 do not (C4: the
-        // main step 25 us faster, the iteration 100 us slower with both passes fused)
+        // the concurrent pass writes no rhs slots, so it runs the fused refill without their loads
+        // (k_local_z_hqf<4, false>: 412 registers, room beside it for the Anderson kernels; the
+        // slot-writing form's 452 leave none -- C4 with that on both passes: the main step 25 us
+        // faster, the iteration 100 us slower). Same box, 8 steps: 457.7 / 459.8 -> 459.2 / 464.8
+        // it/s. AA_LQ_FUSED_CONC=0: the plain refill here
         const char* fc = std::getenv("AA_LQ_FUSED_CONC");
-        lq2_.fused = lq2_.fused && fc && fc[0] == '1';
+        lq2_.fused = lq2_.fused && (fc ? fc[0] == '1' : true);
     }
     if (const char* q = std::getenv("AA_LQ_STATS"); q && q[0] == '1') {
         lq_stats_.alloc(kLqStats);
