@@ -108,7 +108,28 @@ def run_ref(scene, tmp):
     r = subprocess.run([drv, path_in, path_out], cwd=tmp, capture_output=True, text=True, env=env)
     if r.returncode != 0:
         raise RuntimeError(r.stderr)
-    return refio.read_ref_result(path_out, scene.n_nodes)
+    steps = refio.read_ref_result(path_out, scene.n_nodes)
+    if scene.variant != scenes.VARIANT_H and scene.accel:
+        z_reject_flags(steps, r.stdout)
+    return steps
+
+
+def z_reject_flags(steps, stdout):
+    """The z-AA reference (admm_anderson_xzu) writes no reject column to its residual file
+    (Solver.hpp:142-144: time, prim, comb), so the driver's flags read 0; it prints each step's
+    reject count instead ("reset number = N", Solver.cpp:253). A reject at iteration k happens iff
+    the fresh prim exceeds the previous recorded one (Solver.cpp:159); without one the recorded prim
+    is that fresh value, so every recorded rise prim_k > prim_{k-1} is a reject. Those flags are
+    the reference's flags exactly when their count equals the printed count (then `reject_exact`
+    is 1 for the step); otherwise they are a lower bound. Each step also keeps the printed count."""
+    counts = [int(ln.split("=")[1]) for ln in stdout.splitlines() if ln.strip().startswith("reset number")]
+    for k, st in enumerate(steps):
+        p = np.asarray(st["prim"])
+        flags = np.zeros(len(p), np.int32)
+        flags[1:] = p[1:] > p[:-1]
+        st["reject"] = flags
+        st["resets"] = counts[k] if k < len(counts) else -1
+        st["reject_exact"] = int(st["resets"] == int(flags.sum()))
 
 
 def element_tables(tmp):

@@ -27,6 +27,9 @@ def save_case(path, sc, steps):
         reject=np.concatenate([s["reject"] for s in steps]),
         xs=np.stack([s["x"] for s in steps]), vs=np.stack([s["v"] for s in steps]),
     )
+    if all("resets" in s for s in steps):   # z-AA reference: its printed per-step reject counts
+        d["ref_resets"] = np.array([s["resets"] for s in steps])
+        d["reject_exact"] = np.array([s["reject_exact"] for s in steps])
     for i, g in enumerate(sc.groups):
         d[f"g{i}_idx"] = g.idx
     if sc.rest is not None:

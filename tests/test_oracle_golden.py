@@ -45,3 +45,28 @@ def test_oracle_elements(oracle):
         ref = d[f"cod{i}_theta"]
         np.testing.assert_allclose(th, ref, rtol=0, atol=1e-6 * max(1.0, np.linalg.norm(ref)))
         i += 1
+
+
+def test_z_reference_reject_flags_are_the_references():
+    """The z-AA reference logs no reject column (admm_anderson_xzu/src/Solver.hpp:142-144), so
+    make_golden.py rebuilds its flags: a recorded prim rise is a reject (Solver.cpp:159-176), and
+    the per-step count it prints ("reset number", Solver.cpp:253) is kept as ref_resets. Every
+    accelerated z-AA fixture's flags must account for exactly that count (reject_exact), so the
+    flags the GPU tests compare are the reference's own, not a column of zeros."""
+    import os
+    from golden_io import GOLDEN
+    seen = 0
+    for name in case_names():
+        d = np.load(os.path.join(GOLDEN, name + ".npz"))
+        if "ref_resets" not in d.files:
+            continue
+        seen += 1
+        o = 0
+        for k, n in enumerate(d["nrec"]):
+            flags = d["reject"][o:o + n]
+            o += n
+            assert d["reject_exact"][k] == 1, (name, k)
+            assert int(flags.sum()) == int(d["ref_resets"][k]), (name, k)
+            p = d["prim"][o - n:o]
+            assert np.array_equal(flags[1:] == 1, p[1:] > p[:-1]), (name, k)
+    assert seen >= 5
