@@ -206,6 +206,7 @@ def full_drop40(tmp):
     rng = np.random.default_rng(4)
     sample = np.sort(rng.choice(sc.n_nodes, 512, replace=False)).astype(np.int32)
     np.savez_compressed(os.path.join(HERE, "full_drop40_z_nh_aa6.npz"), digest=scene_digest(sc), sample=sample,
+                        ref_resets=np.array([s["resets"] for s in steps]),
                         nrec=np.array([len(s["prim"]) for s in steps]),
                         prim=np.concatenate([s["prim"] for s in steps]), comb=np.concatenate([s["comb"] for s in steps]),
                         reject=np.concatenate([s["reject"] for s in steps]),
@@ -225,6 +226,7 @@ def full_bunny40(tmp):
     rng = np.random.default_rng(5)
     sample = np.sort(rng.choice(sc.n_nodes, 512, replace=False)).astype(np.int32)
     np.savez_compressed(os.path.join(HERE, "full_bunny40_z_nh_aa6.npz"), digest=scene_digest(sc), sample=sample,
+                        ref_resets=np.array([s["resets"] for s in steps]),
                         nrec=np.array([len(s["prim"]) for s in steps]),
                         prim=np.concatenate([s["prim"] for s in steps]), comb=np.concatenate([s["comb"] for s in steps]),
                         reject=np.concatenate([s["reject"] for s in steps]),

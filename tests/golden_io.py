@@ -207,6 +207,11 @@ def check_full_golden(got, ref, reject_slack=0):
         nrej = int((np.asarray(h["reject"]) != rr).sum())
         if nrej > reject_slack:
             fails.append(f"step {k}: {nrej} reject flags differ")
+        # the z-AA reference prints its per-step reject count (Solver.cpp:253) but logs no flags: a
+        # reject whose recomputed prim does not rise is invisible in the fixture's flags, the count
+        # still holds it
+        if "ref_resets" in ref.files and int(np.sum(h["reject"])) != int(ref["ref_resets"][k]):
+            fails.append(f"step {k}: {int(np.sum(h['reject']))} rejects, the reference {int(ref['ref_resets'][k])}")
         for key in ("x", "v"):
             want = ref[key + "_sample"][k]
             scale = np.abs(want).max()
